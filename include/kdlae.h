@@ -1,0 +1,100 @@
+/*
+ * kdlae.h — C ABI of the MI355X-native KDLAE path (libkdlae.so).
+ *
+ * The reference exposes no FFI: its boundary is the PyTorch nn.Module API
+ * (SURVEY.md §8b).  These entry points are what a ctypes/cffi binding of
+ * that module API binds; each one replaces the reference interface cited
+ * beside it.  All pointers are device pointers unless marked host; tensors
+ * are fp32, contiguous NCHW exactly as the reference consumes/produces them.
+ * `stream` is a hipStream_t (0 = null stream).  Nothing here allocates,
+ * frees or synchronises inside *_forward: activations, outputs and the
+ * workspace are caller-owned; the handle owns only packed weights.
+ *
+ * Error handling: every call returns KDLAE_OK (0) or one of the codes
+ * below; kdlae_last_error() returns a thread-local message describing the
+ * last failure on the calling thread.
+ */
+#ifndef KDLAE_H_
+#define KDLAE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  KDLAE_OK = 0,
+  KDLAE_EINVAL_SHAPE = 1,   /* e.g. H or W not divisible by 8 (reference: RuntimeError from pixel_unshuffle) */
+  KDLAE_EINVAL_CONFIG = 2,  /* ctor kwargs the HIP path does not support (message says which) */
+  KDLAE_EHIP = 3,           /* a HIP runtime call failed; message carries hipGetErrorString */
+  KDLAE_EPARAM = 4,         /* unknown / missing / wrongly sized state_dict entry */
+  KDLAE_ENOTIMPL = 5,       /* dual_pixel_task=True: NameError in the reference (KDLAE_model.py:305-321) */
+  KDLAE_ESTATE = 6          /* forward before commit_params, workspace too small, ... */
+};
+
+const char* kdlae_last_error(void);
+int kdlae_abi_version(void);
+
+/* ------------------------------------------------------------------ KDLAE-T
+ * Ctor kwargs of KDLAE_teacher (KDLAE/KDLAE_model.py:205-218).  Strings are
+ * mapped to flags: LayerNorm_type=='BiasFree' -> layernorm_biasfree=1,
+ * static=="train" -> static_train=1, params=='cat' -> params_cat=1.
+ */
+typedef struct kdlae_t_config {
+  int inp_channels;
+  int out_channels;
+  int dim;
+  int num_blocks[4];
+  int num_refinement_blocks;
+  int heads[4];
+  double ffn_expansion_factor;
+  int bias;
+  int layernorm_biasfree;
+  int dual_pixel_task;
+  int static_train;
+  int params_cat;
+} kdlae_t_config;
+
+typedef struct kdlae_t_handle kdlae_t_handle;
+
+/* replaces KDLAE_teacher.__init__ (KDLAE_model.py:205-268): validates the config, binds `device`. */
+int kdlae_t_create(const kdlae_t_config* cfg, int device, kdlae_t_handle** out);
+int kdlae_t_destroy(kdlae_t_handle* h);
+
+/* state_dict surface (KDLAE_model.py:220-268 key layout; load_state_dict at KDLAE_T.ipynb:1074-1075).
+ * kdlae_t_num_params / kdlae_t_param_info enumerate the expected keys and element counts;
+ * kdlae_t_set_param stages one entry from HOST memory (strict: unknown key or numel mismatch
+ * -> KDLAE_EPARAM); kdlae_t_commit_params packs every staged entry into the device layout
+ * (LN weight folded into 1x1 weights, NHWC/MFMA fragment order) and uploads it on `stream`. */
+int kdlae_t_num_params(const kdlae_t_handle* h);
+int kdlae_t_param_info(const kdlae_t_handle* h, int index, const char** name, int64_t* numel);
+int kdlae_t_set_param(kdlae_t_handle* h, const char* name, const float* host_data, int64_t numel);
+int kdlae_t_commit_params(kdlae_t_handle* h, void* stream);
+
+/* Device bytes of caller-owned scratch needed by kdlae_t_forward for a B x H x W batch. */
+int64_t kdlae_t_workspace_bytes(const kdlae_t_handle* h, int B, int H, int W);
+
+/* replaces KDLAE_teacher.forward (KDLAE_model.py:270-336):
+ *   img  [B, inp_channels, H, W]   ({"img"})
+ *   rate [B, 1, H, W]              ({"denoise_rate"}; read only when params_cat)
+ *   hq   [B, out_channels, H, W]   (out["hq"])
+ *   sr   [B, out_channels, 2H, 2W] (out["sr"]; must be NULL iff static_train == 0)
+ * H % 8 == 0 and W % 8 == 0 are required (else KDLAE_EINVAL_SHAPE).  Enqueued on `stream`. */
+int kdlae_t_forward(kdlae_t_handle* h, const float* img, const float* rate, int B, int H, int W,
+                    float* hq, float* sr, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Measurement hook for bench.py (no effect on results).  When a probe class is armed, every
+ * launch of that kernel class inside kdlae_t_forward is bracketed by a pair of HIP events on
+ * `stream`; kdlae_t_probe_read synchronises those events and returns the summed device time (ms),
+ * launch count and the algorithmic HBM bytes / FLOPs of the probed launches (SURVEY.md §8d model).
+ * Classes: 0 = off, 1 = 1x1/implicit-GEMM conv (MFMA), 2 = dwconv+Gram (MDTA pass 1),
+ * 3 = dwconv+GELU gate (GDFN).  A non-zero `level_filter` limits probing to blocks whose channel
+ * count equals it.  */
+int kdlae_t_probe_arm(kdlae_t_handle* h, int kernel_class, int level_filter);
+int kdlae_t_probe_read(kdlae_t_handle* h, double* ms, int64_t* launches, double* bytes, double* flops);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KDLAE_H_ */

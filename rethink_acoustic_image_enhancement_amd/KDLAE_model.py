@@ -1,0 +1,264 @@
+"""Drop-in KDLAE-T module whose forward runs on the MI355X HIP path (libkdlae.so).
+
+Same public surface as ``KDLAE/KDLAE_model.py`` in the reference:
+  * ``KDLAE_teacher(**ctor kwargs)`` with identical kwargs and defaults (:205-218);
+  * an identical submodule tree, so ``state_dict()`` keys / shapes match the released ``.pth``
+    files (``torch.load(p)['params']`` + strict ``load_state_dict``, KDLAE_T.ipynb:1074-1075) and
+    the BasicSR ``RestormerSuperResolutionParam2`` checkpoints (same 483 keys);
+  * ``forward({'img': [B,C,H,W], 'denoise_rate': [B,1,H,W]}) -> {'hq', 'sr'}`` (:270-336).
+
+The submodules here only own parameters.  ``KDLAE_teacher.forward`` hands device pointers to the C
+ABI (``kdlae_t_forward``), which enqueues the whole network on the current HIP stream.  There is
+no CPU path: a CPU tensor or a missing library raises.  The CPU restatement used to check this
+module lives in ``oracle/`` and is test infrastructure only.
+"""
+from __future__ import annotations
+
+import ctypes
+import numbers
+import warnings
+import weakref
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+class BiasFree_LayerNorm(nn.Module):
+    """Parameter holder for x / sqrt(var_C(x) + 1e-5) * w (KDLAE_model.py:38-52)."""
+
+    def __init__(self, normalized_shape):
+        super().__init__()
+        if isinstance(normalized_shape, numbers.Integral):
+            normalized_shape = (normalized_shape,)
+        self.normalized_shape = torch.Size(normalized_shape)
+        self.weight = nn.Parameter(torch.ones(self.normalized_shape))
+
+
+class WithBias_LayerNorm(nn.Module):
+    """Parameter holder for (x - mu) / sqrt(var + 1e-5) * w + b (KDLAE_model.py:54-70)."""
+
+    def __init__(self, normalized_shape):
+        super().__init__()
+        if isinstance(normalized_shape, numbers.Integral):
+            normalized_shape = (normalized_shape,)
+        self.normalized_shape = torch.Size(normalized_shape)
+        self.weight = nn.Parameter(torch.ones(self.normalized_shape))
+        self.bias = nn.Parameter(torch.zeros(self.normalized_shape))
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, dim, LayerNorm_type):
+        super().__init__()
+        self.body = BiasFree_LayerNorm(dim) if LayerNorm_type == "BiasFree" else WithBias_LayerNorm(dim)
+
+
+class FeedForward(nn.Module):
+    """GDFN parameters (KDLAE_model.py:89-99): hidden = int(dim * ffn_expansion_factor)."""
+
+    def __init__(self, dim, ffn_expansion_factor, bias):
+        super().__init__()
+        hidden = int(dim * ffn_expansion_factor)
+        self.project_in = nn.Conv2d(dim, 2 * hidden, kernel_size=1, bias=bias)
+        self.dwconv = nn.Conv2d(2 * hidden, 2 * hidden, kernel_size=3, padding=1, groups=2 * hidden, bias=bias)
+        self.project_out = nn.Conv2d(hidden, dim, kernel_size=1, bias=bias)
+
+
+class Attention(nn.Module):
+    """MDTA parameters (KDLAE_model.py:112-120)."""
+
+    def __init__(self, dim, num_heads, bias):
+        super().__init__()
+        self.num_heads = num_heads
+        self.temperature = nn.Parameter(torch.ones(num_heads, 1, 1))
+        self.qkv = nn.Conv2d(dim, 3 * dim, kernel_size=1, bias=bias)
+        self.qkv_dwconv = nn.Conv2d(3 * dim, 3 * dim, kernel_size=3, padding=1, groups=3 * dim, bias=bias)
+        self.project_out = nn.Conv2d(dim, dim, kernel_size=1, bias=bias)
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, dim, num_heads, ffn_expansion_factor, bias, LayerNorm_type):
+        super().__init__()
+        self.norm1 = LayerNorm(dim, LayerNorm_type)
+        self.attn = Attention(dim, num_heads, bias)
+        self.norm2 = LayerNorm(dim, LayerNorm_type)
+        self.ffn = FeedForward(dim, ffn_expansion_factor, bias)
+
+
+class OverlapPatchEmbed(nn.Module):
+    def __init__(self, in_c=3, embed_dim=48, bias=False):
+        super().__init__()
+        self.proj = nn.Conv2d(in_c, embed_dim, kernel_size=3, padding=1, bias=bias)
+
+
+class Downsample(nn.Module):
+    def __init__(self, n_feat):
+        super().__init__()
+        self.body = nn.Sequential(nn.Conv2d(n_feat, n_feat // 2, kernel_size=3, padding=1, bias=False),
+                                  nn.PixelUnshuffle(2))
+
+
+class Upsample(nn.Module):
+    def __init__(self, n_feat):
+        super().__init__()
+        self.body = nn.Sequential(nn.Conv2d(n_feat, n_feat * 2, kernel_size=3, padding=1, bias=False),
+                                  nn.PixelShuffle(2))
+
+
+def _stage(n, dim, heads, ffn, bias, ln):
+    return nn.Sequential(*[TransformerBlock(dim, heads, ffn, bias, ln) for _ in range(n)])
+
+
+class _Engine:
+    """One C-ABI handle per (module, device); re-packs weights when any parameter changes."""
+
+    def __init__(self, cfg: _lib.TConfig, device_index: int):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(L.kdlae_t_create(ctypes.byref(cfg), device_index, ctypes.byref(h)), "kdlae_t_create")
+        self.handle = h
+        self.device_index = device_index
+        self.signature = None
+        self.ws = None
+        self._fin = weakref.finalize(self, L.kdlae_t_destroy, h)
+
+    def sync_params(self, module: nn.Module, stream) -> None:
+        params = list(module.parameters())
+        sig = tuple((id(p), p._version, p.data_ptr()) for p in params)
+        if sig == self.signature:
+            return
+        L = _lib.lib()
+        for name, t in module.state_dict().items():
+            host = t.detach().to("cpu", torch.float32).contiguous()
+            _lib.check(L.kdlae_t_set_param(self.handle, name.encode(), ctypes.c_void_p(host.data_ptr()),
+                                           host.numel()), f"load {name}")
+        _lib.check(L.kdlae_t_commit_params(self.handle, ctypes.c_void_p(stream)), "kdlae_t_commit_params")
+        self.signature = sig
+
+    def workspace(self, nbytes: int, device) -> torch.Tensor:
+        if self.ws is None or self.ws.numel() < nbytes:
+            self.ws = None
+            self.ws = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+        return self.ws
+
+
+class KDLAE_teacher(nn.Module):
+    """KDLAE-T (KDLAE/KDLAE_model.py:204-336) with the forward on the MI355X HIP path."""
+
+    def __init__(self, inp_channels=3, out_channels=3, dim=48, num_blocks=[4, 6, 6, 8],
+                 num_refinement_blocks=4, heads=[1, 2, 4, 8], ffn_expansion_factor=2.66, bias=False,
+                 LayerNorm_type='WithBias', dual_pixel_task=False, static="train", params='cat'):
+        super().__init__()
+        self.params = params
+        self.static = static
+        self.dual_pixel_task = dual_pixel_task
+        self._cfg = dict(inp_channels=inp_channels, out_channels=out_channels, dim=dim,
+                         num_blocks=list(num_blocks), num_refinement_blocks=num_refinement_blocks,
+                         heads=list(heads), ffn_expansion_factor=ffn_expansion_factor, bias=bias,
+                         LayerNorm_type=LayerNorm_type, dual_pixel_task=dual_pixel_task, static=static,
+                         params=params)
+        d, nb, hd, f, ln = dim, num_blocks, heads, ffn_expansion_factor, LayerNorm_type
+        self.patch_embed = OverlapPatchEmbed(inp_channels, d)
+        self.encoder_level1 = _stage(nb[0], d, hd[0], f, bias, ln)
+        self.down1_2 = Downsample(d)
+        self.encoder_level2 = _stage(nb[1], 2 * d, hd[1], f, bias, ln)
+        self.down2_3 = Downsample(2 * d)
+        self.encoder_level3 = _stage(nb[2], 4 * d, hd[2], f, bias, ln)
+        self.down3_4 = Downsample(4 * d)
+        self.latent = _stage(nb[3], 8 * d, hd[3], f, bias, ln)
+        self.up4_3 = Upsample(8 * d)
+        self.reduce_chan_level3 = nn.Conv2d(8 * d, 4 * d, kernel_size=1, bias=bias)
+        self.decoder_level3 = _stage(nb[2], 4 * d, hd[2], f, bias, ln)
+        self.up3_2 = Upsample(4 * d)
+        self.reduce_chan_level2 = nn.Conv2d(4 * d, 2 * d, kernel_size=1, bias=bias)
+        self.decoder_level2 = _stage(nb[1], 2 * d, hd[1], f, bias, ln)
+        self.up2_1 = Upsample(2 * d)
+        self.decoder_level1 = _stage(nb[0], 2 * d, hd[0], f, bias, ln)
+        self.refinement = _stage(num_refinement_blocks, 2 * d, hd[0], f, bias, ln)
+        if dual_pixel_task:
+            self.skip_conv = nn.Conv2d(d, 2 * d, kernel_size=1, bias=bias)
+        self.output = nn.Conv2d(2 * d, out_channels, kernel_size=3, padding=1, bias=bias)
+        self.output_param = nn.Conv2d(out_channels + 1, 2 * d, kernel_size=3, dilation=2, padding=2, bias=bias)
+        self.refinement_out = _stage(num_refinement_blocks, 2 * d, hd[0], f, bias, ln)
+        self.output2 = nn.Conv2d(2 * d, out_channels, kernel_size=3, padding=1, bias=bias)
+        if static == "train":
+            hc = 2 * d
+            self.cen = nn.Conv2d(out_channels, hc, kernel_size=3, padding=1, bias=bias)
+            self.upen = Upsample(hc)
+            self.enhance = _stage(num_refinement_blocks, hc // 2, hd[0], f, bias, ln)
+            self.outputen = nn.Conv2d(hc // 2, out_channels, kernel_size=3, padding=1, bias=bias)
+        self._engines = {}
+        self._warned_grad = False
+
+    # ------------------------------------------------------------------ HIP plumbing
+    def _c_config(self) -> _lib.TConfig:
+        c = self._cfg
+        cfg = _lib.TConfig()
+        cfg.inp_channels, cfg.out_channels, cfg.dim = c["inp_channels"], c["out_channels"], c["dim"]
+        for i in range(4):
+            cfg.num_blocks[i] = int(c["num_blocks"][i])
+            cfg.heads[i] = int(c["heads"][i])
+        cfg.num_refinement_blocks = c["num_refinement_blocks"]
+        cfg.ffn_expansion_factor = float(c["ffn_expansion_factor"])
+        cfg.bias = int(bool(c["bias"]))
+        cfg.layernorm_biasfree = int(c["LayerNorm_type"] == "BiasFree")
+        cfg.dual_pixel_task = int(bool(c["dual_pixel_task"]))
+        cfg.static_train = int(c["static"] == "train")
+        cfg.params_cat = int(c["params"] == "cat")
+        return cfg
+
+    def engine(self, device: torch.device) -> _Engine:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        eng = self._engines.get(idx)
+        if eng is None:
+            eng = _Engine(self._c_config(), idx)
+            self._engines[idx] = eng
+        return eng
+
+    def forward(self, input):
+        img = input["img"]
+        denoise_rate = input["denoise_rate"]
+        if self.dual_pixel_task:
+            raise NotImplementedError("dual_pixel_task=True: the reference forward leaves out_hq undefined "
+                                      "(KDLAE_model.py:305-321)")
+        if img.device.type != "cuda":
+            raise RuntimeError("KDLAE_teacher (MI355X build) runs on ROCm devices only; move the model "
+                               "inputs to 'cuda' — there is no CPU fallback")
+        if img.dim() != 4 or img.shape[1] != self._cfg["inp_channels"]:
+            raise RuntimeError(f"expected img [B,{self._cfg['inp_channels']},H,W], got {tuple(img.shape)}")
+        B, _, H, W = img.shape
+        if H % 8 or W % 8:
+            raise RuntimeError(f"KDLAE_teacher needs H and W divisible by 8, got {H}x{W} "
+                               "(pad to a multiple of 8 as KDLAE_T.ipynb does)")
+        cat = self._cfg["params"] == "cat"
+        if cat and tuple(denoise_rate.shape) != (B, 1, H, W):
+            raise RuntimeError(f"denoise_rate must be [B,1,H,W]={B, 1, H, W}, got {tuple(denoise_rate.shape)}")
+        if torch.is_grad_enabled() and (img.requires_grad or any(p.requires_grad for p in self.parameters())):
+            if not self._warned_grad:
+                warnings.warn("KDLAE_teacher HIP forward is inference-only: outputs carry no autograd graph")
+                self._warned_grad = True
+        dev = img.device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        eng = self.engine(dev)
+        eng.sync_params(self, stream)
+        img_c = img.detach().to(torch.float32).contiguous()
+        rate_c = denoise_rate.detach().to(device=dev, dtype=torch.float32).contiguous() if cat else None
+        oc = self._cfg["out_channels"]
+        hq = torch.empty((B, oc, H, W), device=dev, dtype=torch.float32)
+        sr = torch.empty((B, oc, 2 * H, 2 * W), device=dev, dtype=torch.float32) if self.static == "train" else None
+        L = _lib.lib()
+        nbytes = L.kdlae_t_workspace_bytes(eng.handle, B, H, W)
+        if nbytes < 0:
+            _lib.check(1, "kdlae_t_workspace_bytes")
+        ws = eng.workspace(nbytes, dev)
+        rc = L.kdlae_t_forward(eng.handle, ctypes.c_void_p(img_c.data_ptr()),
+                               ctypes.c_void_p(rate_c.data_ptr() if rate_c is not None else 0), B, H, W,
+                               ctypes.c_void_p(hq.data_ptr()), ctypes.c_void_p(sr.data_ptr() if sr is not None else 0),
+                               ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(stream))
+        _lib.check(rc, "kdlae_t_forward")
+        return {"hq": hq, "sr": sr}
+
+
+# BasicSR registers the same network under this name (Train/basicsr/models/archs/restormer_arch.py:566)
+RestormerSuperResolutionParam2 = KDLAE_teacher

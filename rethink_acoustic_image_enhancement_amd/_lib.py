@@ -1,0 +1,87 @@
+"""ctypes binding of libkdlae.so (the C ABI declared in include/kdlae.h).
+
+The product path has no CPU fallback: if the shared library is missing or a call fails, a
+RuntimeError is raised.  Build it with ``make -C rethink_acoustic_image_enhancement_amd/csrc``
+(or ``python -c 'import __graft_entry__ as g; g.build()'``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkdlae.so")
+
+c_int, c_int64, c_double, c_void_p, c_char_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_double,
+                                                ctypes.c_void_p, ctypes.c_char_p)
+
+ERRORS = {0: "OK", 1: "EINVAL_SHAPE", 2: "EINVAL_CONFIG", 3: "EHIP", 4: "EPARAM", 5: "ENOTIMPL",
+          6: "ESTATE"}
+
+# Every entry point include/kdlae.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "kdlae_last_error", "kdlae_abi_version",
+    "kdlae_t_create", "kdlae_t_destroy", "kdlae_t_num_params", "kdlae_t_param_info",
+    "kdlae_t_set_param", "kdlae_t_commit_params", "kdlae_t_workspace_bytes", "kdlae_t_forward",
+    "kdlae_t_probe_arm", "kdlae_t_probe_read",
+)
+
+
+class TConfig(ctypes.Structure):
+    """kdlae_t_config (include/kdlae.h) = KDLAE_teacher ctor kwargs (KDLAE_model.py:205-218)."""
+
+    _fields_ = [
+        ("inp_channels", c_int), ("out_channels", c_int), ("dim", c_int),
+        ("num_blocks", c_int * 4), ("num_refinement_blocks", c_int), ("heads", c_int * 4),
+        ("ffn_expansion_factor", c_double), ("bias", c_int), ("layernorm_biasfree", c_int),
+        ("dual_pixel_task", c_int), ("static_train", c_int), ("params_cat", c_int),
+    ]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libkdlae.so once; raise loudly if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: the KDLAE HIP path has no CPU fallback. Build it with "
+            "`make -C rethink_acoustic_image_enhancement_amd/csrc` (hipcc, gfx950).")
+    L = ctypes.CDLL(LIB_PATH)
+    L.kdlae_last_error.restype = c_char_p
+    L.kdlae_abi_version.restype = c_int
+    L.kdlae_t_create.argtypes = [ctypes.POINTER(TConfig), c_int, ctypes.POINTER(c_void_p)]
+    L.kdlae_t_destroy.argtypes = [c_void_p]
+    L.kdlae_t_num_params.argtypes = [c_void_p]
+    L.kdlae_t_param_info.argtypes = [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]
+    L.kdlae_t_set_param.argtypes = [c_void_p, c_char_p, c_void_p, c_int64]
+    L.kdlae_t_commit_params.argtypes = [c_void_p, c_void_p]
+    L.kdlae_t_workspace_bytes.argtypes = [c_void_p, c_int, c_int, c_int]
+    L.kdlae_t_workspace_bytes.restype = c_int64
+    L.kdlae_t_forward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                  c_void_p, c_int64, c_void_p]
+    L.kdlae_t_probe_arm.argtypes = [c_void_p, c_int, c_int]
+    L.kdlae_t_probe_read.argtypes = [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int64),
+                                     ctypes.POINTER(c_double), ctypes.POINTER(c_double)]
+    for name in EXPORTS:
+        if name not in ("kdlae_last_error", "kdlae_abi_version", "kdlae_t_workspace_bytes"):
+            getattr(L, name).restype = c_int
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    msg = lib().kdlae_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        err = last_error()
+        code = ERRORS.get(rc, str(rc))
+        if rc == 5:
+            raise NotImplementedError(f"{what}: {err}")
+        raise RuntimeError(f"{what} failed ({code}): {err}")

@@ -1,0 +1,127 @@
+// Direct 3x3 convolutions whose input or output has <= 4 channels (VALU; too thin for MFMA).
+//
+//   small-in  (Cin <= 4,  Cout % 16 == 0): patch_embed 3->48 (KDLAE_model.py:173),
+//             output_param 4->96 dilation 2 on cat[out, denoise_rate] (:259, :316), cen 3->96 (:265)
+//   small-out (Cout <= 4, Cin % 4 == 0):  output 96->3 (:258, :314), output2 96->3 + inp_img (:261,
+//             :319-321), outputen 48->3 (:268, :329)
+// Zero padding = dilation.  Input of small-in is any strided 4-D tensor (NCHW or NHWC view);
+// output of small-out is NCHW (optionally + NCHW residual) or an NHWC view that also receives an
+// extra NCHW channel — the torch.cat([out, denoise_rate]) of :316 folded into the producer.
+#include "kernels.h"
+
+namespace kdlae {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// thread = (16-channel output group, pixel); all lanes of a wave share the group -> LDS broadcast
+__global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
+  extern __shared__ float wsm[];  // [Cout][36] (ci-major, zero for ci >= Cin) then bias[Cout]
+  const int nw = p.Cout * 36;
+  for (int i = threadIdx.x; i < nw; i += 256) {
+    const int co = i / 36, k = i - (i / 36) * 36;
+    wsm[i] = (k / 9) < p.Cin ? p.w[co * p.Cin * 9 + k] : 0.f;
+  }
+  for (int i = threadIdx.x; i < p.Cout; i += 256) wsm[nw + i] = p.bias ? p.bias[i] : 0.f;
+  __syncthreads();
+  const int HW = p.H * p.W;
+  const long long P = (long long)p.Bn * HW;
+  const int ngroups = p.Cout / 16;
+  const long long total = P * ngroups;
+  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+    const int og = (int)(idx / P);
+    const long long pix = idx - (long long)og * P;
+    const int b = (int)(pix / HW);
+    const int pl = (int)(pix - (long long)b * HW);
+    const int y = pl / p.W, x = pl - (pl / p.W) * p.W;
+    float in[36];
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + (t / 3 - 1) * p.dil, xx = x + (t % 3 - 1) * p.dil;
+        const bool ok = ci < p.Cin && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+        const long long off = ok ? b * p.sb + ci * p.sc + yy * p.sy + xx * p.sx : 0;
+        const float v = p.in[off];
+        in[ci * 9 + t] = ok ? v : 0.f;
+      }
+    }
+    float* o = p.out + pix * p.ldo + og * 16;
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      f32x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = og * 16 + j4 * 4 + e;
+        const float* wr = wsm + co * 36;
+        float a = wsm[nw + co];
+#pragma unroll
+        for (int k = 0; k < 36; ++k) a = fmaf(in[k], wr[k], a);
+        r[e] = a;
+      }
+      *reinterpret_cast<f32x4*>(o + j4 * 4) = r;
+    }
+  }
+}
+
+hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s) {
+  const long long total = (long long)p.Bn * p.H * p.W * (p.Cout / 16);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  const size_t lds = (size_t)(p.Cout * 36 + p.Cout) * sizeof(float);
+  hipLaunchKernelGGL(conv_small_in_kernel, dim3((unsigned)blocks), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+// thread = pixel; weights transposed in LDS to [tap][ci][4] so every read is a broadcast float4
+__global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
+  extern __shared__ __attribute__((aligned(16))) float wso[];  // [9][Cin][4]
+  const int nw = 9 * p.Cin * 4;
+  for (int i = threadIdx.x; i < nw; i += 256) {
+    const int o = i & 3, ci = (i >> 2) % p.Cin, t = (i >> 2) / p.Cin;
+    wso[i] = o < p.Cout ? p.w[(o * p.Cin + ci) * 9 + t] : 0.f;
+  }
+  __syncthreads();
+  const int HW = p.H * p.W;
+  const long long P = (long long)p.Bn * HW;
+  for (long long pix = blockIdx.x * 256LL + threadIdx.x; pix < P; pix += (long long)gridDim.x * 256) {
+    const int b = (int)(pix / HW);
+    const int pl = (int)(pix - (long long)b * HW);
+    const int y = pl / p.W, x = pl - (pl / p.W) * p.W;
+    const float* Xb = p.in + (long long)b * HW * p.ld;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      if ((unsigned)yy >= (unsigned)p.H || (unsigned)xx >= (unsigned)p.W) continue;
+      const float* xr = Xb + (yy * p.W + xx) * p.ld;
+      const f32x4* wt = reinterpret_cast<const f32x4*>(wso + t * p.Cin * 4);
+      for (int c = 0; c < p.Cin; c += 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(xr + c);
+        acc += v.x * wt[c] + v.y * wt[c + 1] + v.z * wt[c + 2] + v.w * wt[c + 3];
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      if (o >= p.Cout) break;
+      float v = acc[o] + (p.bias ? p.bias[o] : 0.f);
+      if (p.out_nchw) {
+        const long long oi = ((long long)b * p.Cout + o) * HW + pl;
+        if (p.res) v += p.res[oi];
+        p.out[oi] = v;
+      } else {
+        p.out[pix * p.ldo + o] = v;
+      }
+    }
+    if (!p.out_nchw && p.extra) p.out[pix * p.ldo + p.Cout] = p.extra[(long long)b * HW + pl];
+  }
+}
+
+hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s) {
+  const long long P = (long long)p.Bn * p.H * p.W;
+  long long blocks = (P + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  const size_t lds = (size_t)9 * p.Cin * 4 * sizeof(float);
+  hipLaunchKernelGGL(conv_small_out_kernel, dim3((unsigned)blocks), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace kdlae

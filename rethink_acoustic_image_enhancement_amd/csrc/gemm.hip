@@ -1,0 +1,254 @@
+// MFMA f32 implicit-GEMM convolution for gfx950 (CDNA4), NHWC activations.
+//
+// out[p][n] = epilogue( sum_k A'[p][k] * W[n][k] )
+//   pointwise (ksize 1): k = input channel               — every 1x1 Conv2d of KDLAE-T
+//                          (qkv / project_out / project_in / ffn.project_out / reduce_chan,
+//                           KDLAE/KDLAE_model.py:95,99,118,120,238,243)
+//   implicit 3x3 (ksize 3): k = tap * Cin_pad + c, zero padding = dilation
+//                          (Downsample/Upsample body convs :186,:196, upen :266)
+//   A' = A, or the LayerNorm of A over channels when `ln` is set (BiasFree :50-52 / WithBias
+//        :67-70); the LN weight is pre-folded into W and the LN bias into `bias`.
+//   epilogue: + bias[n] (+ residual R[p][n], TransformerBlock :160-161) (ReLU), stored plain or
+//             through the PixelUnshuffle(2) / PixelShuffle(2) index map (:187, :197), so the
+//             shuffle never materialises.
+//
+// Work decomposition: a block is 8 waves; each wave owns 2 x 16 pixel rows, holding its A rows
+// for the current k-chunk in VGPRs (float4 per lane per 16-deep k-group: 16 rows x 64 B
+// contiguous per wave load).  The packed weight chunk [NT tiles][KG groups] is staged once into
+// LDS and shared by all 8 waves; when the whole K fits one chunk it stays resident while the
+// block walks a contiguous run of 256-row pixel tiles.  v_mfma_f32_16x16x4_f32 is an exact f32
+// fma chain (no xf32 on gfx950), so numerics equal an f32 dot product with a permuted k order.
+#include "kernels.h"
+
+namespace kdlae {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int NT, int KG, bool CONV3>
+__global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];  // [NT][KG][64]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int nc = blockIdx.y;
+  const int HW = p.H * p.W;
+  const bool resident = (p.kchunks == 1);
+  int staged = -1;
+
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int b = tile / p.tiles_per_img;
+    const int tin = tile - b * p.tiles_per_img;
+    const int row0 = tin * kGemmRows + wave * (kGemmRT * 16);
+    // uniform per-image bases; per-lane offsets stay 32-bit (HW * ld < 2^31 is checked on host)
+    const float* __restrict__ Ab = p.A + (long long)b * HW * p.lda;
+
+    f32x4 acc[NT][kGemmRT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kc = 0; kc < p.kchunks; ++kc) {
+      const int wkey = p.w_img_stride ? b : 0;
+      if (!resident || staged != wkey) {
+        __syncthreads();
+        const float* wbase = p.Wp + (long long)wkey * p.w_img_stride;
+        for (int idx = tid; idx < NT * KG * 64; idx += kGemmThreads) {
+          const int t = idx / (KG * 64);
+          const int rem = idx - t * (KG * 64);
+          const int g = rem >> 6, l = rem & 63;
+          const int gt = nc * NT + t, gg = kc * KG + g;
+          f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (gt < p.ntiles && gg < p.kgroups)
+            v = *reinterpret_cast<const f32x4*>(wbase + ((long long)(gt * p.kgroups + gg) * 64 + l) * 4);
+          wlds[idx] = v;
+        }
+        __syncthreads();
+        staged = wkey;
+      }
+
+      // ---- A rows for this k-chunk: unconditional loads from clamped offsets, then select
+      f32x4 a[kGemmRT][KG];
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r) {
+        const int prow = row0 + r * 16 + li;
+        const bool pv = prow < HW;
+        if (!CONV3) {
+          const int off0 = prow * p.lda + 4 * lq + kc * KG * 16;
+#pragma unroll
+          for (int g = 0; g < KG; ++g) {
+            const bool ok = pv && (kc * KG + g) < p.kgroups;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(Ab + (ok ? off0 + g * 16 : 0));
+            a[r][g] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        } else {
+          const int py = prow / p.W;
+          const int px = prow - py * p.W;
+#pragma unroll
+          for (int g = 0; g < KG; ++g) {
+            const int gg = kc * KG + g;
+            const int tap = gg / p.cg_per_tap;
+            const int cgi = gg - tap * p.cg_per_tap;
+            const int ty = tap / 3;
+            const int yy = py + (ty - 1) * p.dil;
+            const int xx = px + (tap - 3 * ty - 1) * p.dil;
+            const bool ok = pv && gg < p.kgroups && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+            const int off = (yy * p.W + xx) * p.lda + cgi * 16 + 4 * lq;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(Ab + (ok ? off : 0));
+            a[r][g] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      }
+
+      if (p.ln) {
+        const float wb = (p.ln == 2) ? 1.f : 0.f;
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) {
+          float mean, rstd;
+          if (p.stats) {
+            const int prow = min(row0 + r * 16 + li, HW - 1);
+            const float2 st = *reinterpret_cast<const float2*>(p.stats + 2 * ((long long)b * HW + prow));
+            mean = st.x;
+            rstd = st.y;
+          } else {
+            // the whole LN row is in this k-chunk (host: kchunks == 1, kgroups * 16 == ln_C)
+            float s = 0.f;
+#pragma unroll
+            for (int g = 0; g < KG; ++g) s += (a[r][g].x + a[r][g].y) + (a[r][g].z + a[r][g].w);
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            mean = s / (float)p.ln_C;
+            float v2 = 0.f;
+#pragma unroll
+            for (int g = 0; g < KG; ++g) {
+              const f32x4 d = a[r][g] - mean;
+              const float dd = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+              v2 += (g < p.kgroups) ? dd : 0.f;
+            }
+            v2 += __shfl_xor(v2, 16);
+            v2 += __shfl_xor(v2, 32);
+            rstd = 1.0f / sqrtf(v2 / (float)p.ln_C + 1e-5f);
+          }
+          const float sh = mean * wb;
+#pragma unroll
+          for (int g = 0; g < KG; ++g) a[r][g] = (a[r][g] - sh) * rstd;
+        }
+      }
+
+      // ---- MFMA over the chunk: one LDS b128 read of B feeds kGemmRT x 4 MFMAs.
+      // Tiles / groups past the end were zero-filled in LDS and A, so no per-tile branches.
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const f32x4 bw = wlds[(t * KG + g) * 64 + lane];
+#pragma unroll
+          for (int r = 0; r < kGemmRT; ++r) {
+            acc[t][r] = mfma4(a[r][g].x, bw.x, acc[t][r]);
+            acc[t][r] = mfma4(a[r][g].y, bw.y, acc[t][r]);
+            acc[t][r] = mfma4(a[r][g].z, bw.z, acc[t][r]);
+            acc[t][r] = mfma4(a[r][g].w, bw.w, acc[t][r]);
+          }
+        }
+      }
+    }
+
+    // ---- epilogue: D[row = 4*lq + e][col = li] of each 16x16 tile
+    float* __restrict__ Ob = p.out;
+    const float* __restrict__ Rb = p.R ? p.R + (long long)b * HW * p.ldr : nullptr;
+    if (p.out_mode == 0) Ob += (long long)b * HW * p.ldo;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n0 = (nc * NT + t) * 16;
+      if (n0 >= p.N) continue;
+      const int n = n0 + li;
+      const bool nv = n < p.N;
+      const float bn = (p.bias && nv) ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r) {
+        const int pl0 = row0 + r * 16 + 4 * lq;
+        float res[4] = {0.f, 0.f, 0.f, 0.f};
+        if (Rb) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool ok = nv && pl0 + e < HW;
+            const float rv = Rb[ok ? (pl0 + e) * p.ldr + n : 0];
+            res[e] = ok ? rv : 0.f;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int pl = pl0 + e;
+          if (pl < HW && nv) {
+            float v = acc[t][r][e] + bn + res[e];
+            if (p.relu) v = fmaxf(v, 0.f);
+            if (p.out_mode == 0) {
+              Ob[pl * p.ldo + n] = v;
+            } else {
+              const int y = pl / p.W, x = pl - y * p.W;
+              long long dst;
+              int ch;
+              if (p.out_mode == 1) {
+                const int Wo = p.W >> 1, Ho = p.H >> 1;
+                dst = (long long)b * Ho * Wo + (y >> 1) * Wo + (x >> 1);
+                ch = n * 4 + (y & 1) * 2 + (x & 1);
+              } else {
+                dst = (long long)b * 4 * HW + (2 * y + ((n >> 1) & 1)) * (2 * p.W) + 2 * x + (n & 1);
+                ch = n >> 2;
+              }
+              Ob[dst * p.ldo + ch] = v;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+#define KDLAE_GEMM_VARIANTS(X) \
+  X(3, 3, false) X(6, 3, false) X(9, 3, false) X(12, 3, false) \
+  X(3, 6, false) X(6, 6, false) X(9, 6, false) X(12, 6, false) \
+  X(3, 8, false) X(6, 8, false) X(9, 8, false) \
+  X(3, 12, false) X(6, 12, false) \
+  X(3, 16, false) X(6, 16, false) \
+  X(3, 3, true) X(3, 6, true) X(6, 6, true) X(12, 6, true) X(6, 12, true) X(12, 3, true)
+
+bool gemm_has_variant(int NT, int KG, bool conv3) {
+#define X(a, b, c) if (NT == a && KG == b && conv3 == c) return true;
+  KDLAE_GEMM_VARIANTS(X)
+#undef X
+  return false;
+}
+
+template <int NT, int KG, bool C3>
+static hipError_t launch_variant(const GemmParams& p, int grid_x, hipStream_t s) {
+  const size_t lds = (size_t)NT * KG * 64 * sizeof(f32x4);
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<NT, KG, C3>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr_done = true;
+  }
+  const int nchunks = (p.ntiles + NT - 1) / NT;
+  dim3 grid(grid_x, nchunks);
+  hipLaunchKernelGGL((conv_gemm_kernel<NT, KG, C3>), grid, dim3(kGemmThreads), lds, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int grid_x, hipStream_t s) {
+  const bool c3 = p.ksize == 3;
+#define X(a, b, c) if (NT == a && KG == b && c3 == c) return launch_variant<a, b, c>(p, grid_x, s);
+  KDLAE_GEMM_VARIANTS(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+}  // namespace kdlae

@@ -1,0 +1,877 @@
+// KDLAE-T host runtime: config validation, state_dict staging, weight packing into the device
+// layout, workspace planning and the forward launch sequence (one HIP stream, no host syncs).
+//
+// Forward = KDLAE_teacher.forward (KDLAE/KDLAE_model.py:270-336) restated on NHWC views:
+//   patch_embed -> encoder_level1 (written straight into the second half of the level-1 concat
+//   buffer, so torch.cat at :299 is free) -> down1_2 (implicit-GEMM 3x3 + PixelUnshuffle store) ->
+//   ... -> latent -> up4_3 (3x3 + PixelShuffle store into the first half of the level-3 concat
+//   buffer, :288-289) -> reduce_chan_level3 -> ... -> output / output_param / refinement_out /
+//   output2 + img -> hq; static=="train": cen -> upen -> enhance -> outputen -> sr (:324-329).
+// Each TransformerBlock (:159-163) is 7 launches:
+//   [LN1+qkv GEMM] [dwconv+Gram] [slot reduce] [softmax+fold into W_proj] [A.v.proj GEMM + residual]
+//   [LN2+project_in GEMM] [dwconv+GELU gate] [project_out GEMM + residual]   (+ LN stats when K is chunked)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kdlae.h"
+#include "kernels.h"
+
+namespace kdlae {
+
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return fail(KDLAE_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+static inline int ru16(int x) { return (x + 15) / 16 * 16; }
+static inline long long ceil_div(long long a, long long b) { return (a + b - 1) / b; }
+static constexpr size_t kNone = (size_t)-1;
+
+// ----------------------------------------------------------------------------- packed weights
+struct Gemm {
+  size_t w = kNone, bias = kNone;  // offsets (floats) into the device weight arena
+  int ntiles = 0, kgroups = 0, N = 0, K = 0, ksize = 1, cg_per_tap = 0;
+  int NT = 0, KG = 0;
+  int n_true = 0, k_true = 0;  // un-padded sizes (FLOP accounting)
+};
+struct SmallW {
+  size_t w = kNone, bias = kNone;
+  int Cout = 0, Cin = 0;
+};
+struct BlockW {
+  int C = 0, heads = 0, Ch = 0, hid = 0, hidS = 0;
+  Gemm qkv, pin, pout, proj_gemm;  // proj_gemm: geometry of the per-image M GEMM
+  size_t dwqkv = kNone, dwqkv_b = kNone, proj = kNone, proj_b = kNone, temp = kNone;
+  size_t dwffn = kNone, dwffn_b = kNone;
+};
+
+static void choose_variant(Gemm& g, bool prefer_single_k) {
+  static const int nts[] = {3, 6, 9, 12};
+  static const int kgs[] = {3, 6, 8, 12, 16};
+  double best = 1e30;
+  for (int nt : nts)
+    for (int kg : kgs) {
+      if (!gemm_has_variant(nt, kg, g.ksize == 3)) continue;
+      const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
+      const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
+      double cost = waste * (1.0 + 0.12 * (nch - 1)) * (kch > 1 ? 1.08 : 1.0);
+      if (prefer_single_k && kch > 1) cost *= 1.3;
+      cost *= 1.0 + 0.002 * (nt * kg > 96 ? nt * kg - 96 : 0);  // big LDS chunks lower occupancy
+      if (cost < best - 1e-9) {
+        best = cost;
+        g.NT = nt;
+        g.KG = kg;
+      }
+    }
+}
+
+struct Arena {
+  std::vector<float> h;
+  size_t add(const std::vector<float>& v) {
+    size_t off = (h.size() + 63) / 64 * 64;
+    h.resize(off + v.size());
+    std::copy(v.begin(), v.end(), h.begin() + off);
+    return off;
+  }
+};
+
+}  // namespace kdlae
+
+using namespace kdlae;
+
+struct kdlae_t_handle {
+  kdlae_t_config cfg{};
+  int device = 0;
+  std::vector<std::pair<std::string, int64_t>> keys;  // expected state_dict keys (ordered)
+  std::unordered_map<std::string, int> key_index;
+  std::unordered_map<std::string, std::vector<float>> staged;
+  bool committed = false;
+  float* dev = nullptr;  // weight arena
+  size_t dev_floats = 0;
+  // model
+  std::vector<BlockW> enc1, enc2, enc3, latent, dec3, dec2, dec1, refinement, refinement_out, enhance;
+  SmallW patch_embed, output, output_param, output2, cen, outputen;
+  Gemm down1_2, down2_3, down3_4, up4_3, up3_2, up2_1, upen, reduce3, reduce2;
+  // probe
+  int probe_class = 0, probe_level = 0;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  double probe_bytes = 0, probe_flops = 0;
+  long long probe_launches = 0;
+
+  const float* P(size_t off) const { return off == kNone ? nullptr : dev + off; }
+};
+
+namespace kdlae {
+
+static int hid_of(const kdlae_t_config& c, int dim) { return (int)((double)dim * c.ffn_expansion_factor); }
+
+static void add_key(kdlae_t_handle* h, const std::string& k, int64_t n) {
+  h->key_index[k] = (int)h->keys.size();
+  h->keys.emplace_back(k, n);
+}
+
+// Expected state_dict (KDLAE_model.py:220-268, TransformerBlock :150-157, Attention :113-120,
+// FeedForward :90-99, LayerNorm :73-79).
+static void build_keys(kdlae_t_handle* h) {
+  const kdlae_t_config& c = h->cfg;
+  auto conv = [&](const std::string& n, int co, int ci, int k, bool b) {
+    add_key(h, n + ".weight", (int64_t)co * ci * k * k);
+    if (b) add_key(h, n + ".bias", co);
+  };
+  auto block = [&](const std::string& p, int dim, int heads) {
+    const int hid = hid_of(c, dim);
+    add_key(h, p + ".norm1.body.weight", dim);
+    if (!c.layernorm_biasfree) add_key(h, p + ".norm1.body.bias", dim);
+    add_key(h, p + ".attn.temperature", heads);
+    conv(p + ".attn.qkv", 3 * dim, dim, 1, c.bias);
+    conv(p + ".attn.qkv_dwconv", 3 * dim, 1, 3, c.bias);
+    conv(p + ".attn.project_out", dim, dim, 1, c.bias);
+    add_key(h, p + ".norm2.body.weight", dim);
+    if (!c.layernorm_biasfree) add_key(h, p + ".norm2.body.bias", dim);
+    conv(p + ".ffn.project_in", 2 * hid, dim, 1, c.bias);
+    conv(p + ".ffn.dwconv", 2 * hid, 1, 3, c.bias);
+    conv(p + ".ffn.project_out", dim, hid, 1, c.bias);
+  };
+  auto stage = [&](const std::string& n, int cnt, int dim, int heads) {
+    for (int i = 0; i < cnt; ++i) block(n + "." + std::to_string(i), dim, heads);
+  };
+  const int d = c.dim;
+  const int* nb = c.num_blocks;
+  const int* hd = c.heads;
+  const int nr = c.num_refinement_blocks;
+  conv("patch_embed.proj", d, c.inp_channels, 3, false);
+  stage("encoder_level1", nb[0], d, hd[0]);
+  conv("down1_2.body.0", d / 2, d, 3, false);
+  stage("encoder_level2", nb[1], 2 * d, hd[1]);
+  conv("down2_3.body.0", d, 2 * d, 3, false);
+  stage("encoder_level3", nb[2], 4 * d, hd[2]);
+  conv("down3_4.body.0", 2 * d, 4 * d, 3, false);
+  stage("latent", nb[3], 8 * d, hd[3]);
+  conv("up4_3.body.0", 16 * d, 8 * d, 3, false);
+  conv("reduce_chan_level3", 4 * d, 8 * d, 1, c.bias);
+  stage("decoder_level3", nb[2], 4 * d, hd[2]);
+  conv("up3_2.body.0", 8 * d, 4 * d, 3, false);
+  conv("reduce_chan_level2", 2 * d, 4 * d, 1, c.bias);
+  stage("decoder_level2", nb[1], 2 * d, hd[1]);
+  conv("up2_1.body.0", 4 * d, 2 * d, 3, false);
+  stage("decoder_level1", nb[0], 2 * d, hd[0]);
+  stage("refinement", nr, 2 * d, hd[0]);
+  conv("output", c.out_channels, 2 * d, 3, c.bias);
+  conv("output_param", 2 * d, c.out_channels + 1, 3, c.bias);
+  stage("refinement_out", nr, 2 * d, hd[0]);
+  conv("output2", c.out_channels, 2 * d, 3, c.bias);
+  if (c.static_train) {
+    const int hc = 2 * d;
+    conv("cen", hc, c.out_channels, 3, c.bias);
+    conv("upen.body.0", 2 * hc, hc, 3, false);
+    stage("enhance", nr, hc / 2, hd[0]);
+    conv("outputen", c.out_channels, hc / 2, 3, c.bias);
+  }
+}
+
+static int validate(const kdlae_t_config& c) {
+  if (c.dual_pixel_task)
+    return fail(KDLAE_ENOTIMPL, "dual_pixel_task=True: the reference forward raises NameError (out_hq undefined, KDLAE_model.py:305-321)");
+  if (c.dim <= 0 || c.dim % 16)
+    return fail(KDLAE_EINVAL_CONFIG, "dim must be a positive multiple of 16 on the HIP path");
+  if (c.inp_channels < 1 || c.inp_channels > 4 || c.out_channels < 1 || c.out_channels > 3)
+    return fail(KDLAE_EINVAL_CONFIG, "inp_channels must be 1..4 and out_channels 1..3");
+  if (c.inp_channels != c.out_channels)
+    return fail(KDLAE_EINVAL_CONFIG, "inp_channels must equal out_channels (hq = out + inp_img, KDLAE_model.py:321)");
+  for (int i = 0; i < 4; ++i)
+    if (c.num_blocks[i] < 0 || c.heads[i] <= 0) return fail(KDLAE_EINVAL_CONFIG, "bad num_blocks/heads");
+  if (c.num_refinement_blocks < 0) return fail(KDLAE_EINVAL_CONFIG, "bad num_refinement_blocks");
+  auto head_ok = [&](int C, int heads) {
+    if (C % heads) return false;
+    const int ch = C / heads;
+    if (ch % 16) return false;
+    const int ct = ch / 16;
+    return ct == 1 || ct == 2 || ct == 3 || ct == 4 || ct == 6;
+  };
+  const int d = c.dim;
+  const int levels[4] = {d, 2 * d, 4 * d, 8 * d};
+  for (int i = 0; i < 4; ++i)
+    if (!head_ok(levels[i], c.heads[i]))
+      return fail(KDLAE_EINVAL_CONFIG, "channels per head must be 16*{1,2,3,4,6} at every level");
+  if (!head_ok(2 * d, c.heads[0]))
+    return fail(KDLAE_EINVAL_CONFIG, "channels per head of decoder_level1/refinement must be 16*{1,2,3,4,6}");
+  if (c.ffn_expansion_factor <= 0) return fail(KDLAE_EINVAL_CONFIG, "bad ffn_expansion_factor");
+  return KDLAE_OK;
+}
+
+// ----------------------------------------------------------------------------- packing helpers
+struct Packer {
+  kdlae_t_handle* h;
+  Arena arena;
+  int err = KDLAE_OK;
+
+  const std::vector<float>* get(const std::string& k) {
+    auto it = h->staged.find(k);
+    if (it == h->staged.end()) {
+      if (err == KDLAE_OK) err = fail(KDLAE_EPARAM, "missing state_dict entry: " + k);
+      return nullptr;
+    }
+    return &it->second;
+  }
+
+  // generic fragment-order pack: Wf(n, k) over [ntiles*16] x [kgroups*16]
+  template <class F>
+  size_t pack(int ntiles, int kgroups, F Wf) {
+    std::vector<float> v((size_t)ntiles * kgroups * 256, 0.f);
+    for (int t = 0; t < ntiles; ++t)
+      for (int g = 0; g < kgroups; ++g)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 4; ++e) {
+            const int n = 16 * t + (l & 15), k = 16 * g + 4 * (l >> 4) + e;
+            v[(((size_t)t * kgroups + g) * 64 + l) * 4 + e] = Wf(n, k);
+          }
+    return arena.add(v);
+  }
+
+  // 1x1 conv [Cout][Cin] with optional LN(weight, bias) folded on the input side.
+  // row_map(n) -> source output row or -1 (padding); stored N = nstore.
+  template <class RowMap>
+  Gemm pointwise(const std::string& name, int Cout, int Cin, int Kpad, int nstore, RowMap row_map,
+                 const std::string& ln_prefix, bool conv_bias, bool prefer_single_k) {
+    Gemm g;
+    const std::vector<float>* W = get(name + ".weight");
+    const std::vector<float>* lnw = ln_prefix.empty() ? nullptr : get(ln_prefix + ".body.weight");
+    const std::vector<float>* lnb = nullptr;
+    if (!ln_prefix.empty() && !h->cfg.layernorm_biasfree) lnb = get(ln_prefix + ".body.bias");
+    const std::vector<float>* cb = conv_bias ? get(name + ".bias") : nullptr;
+    if (err) return g;
+    g.ntiles = (nstore + 15) / 16;
+    g.kgroups = Kpad / 16;
+    g.N = nstore;
+    g.K = Kpad;
+    g.ksize = 1;
+    g.n_true = Cout;
+    g.k_true = Cin;
+    g.w = pack(g.ntiles, g.kgroups, [&](int n, int k) -> float {
+      if (n >= nstore || k >= Cin) return 0.f;
+      const int src = row_map(n);
+      if (src < 0) return 0.f;
+      const float s = lnw ? (*lnw)[k] : 1.f;
+      return (*W)[(size_t)src * Cin + k] * s;
+    });
+    if (cb || lnb) {
+      std::vector<float> bv((size_t)g.ntiles * 16, 0.f);
+      for (int n = 0; n < nstore; ++n) {
+        const int src = row_map(n);
+        if (src < 0) continue;
+        double acc = cb ? (*cb)[src] : 0.0;
+        if (lnb)
+          for (int k = 0; k < Cin; ++k) acc += (double)(*W)[(size_t)src * Cin + k] * (*lnb)[k];
+        bv[n] = (float)acc;
+      }
+      g.bias = arena.add(bv);
+    }
+    choose_variant(g, prefer_single_k);
+    return g;
+  }
+
+  // 3x3 conv [Cout][Cin][3][3] as implicit GEMM, k = tap * Cin + c (Cin % 16 == 0)
+  Gemm conv3(const std::string& name, int Cout, int Cin) {
+    Gemm g;
+    const std::vector<float>* W = get(name + ".weight");
+    if (err) return g;
+    g.ksize = 3;
+    g.cg_per_tap = Cin / 16;
+    g.ntiles = (Cout + 15) / 16;
+    g.kgroups = 9 * Cin / 16;
+    g.N = Cout;
+    g.K = 9 * Cin;
+    g.n_true = Cout;
+    g.k_true = 9 * Cin;
+    g.w = pack(g.ntiles, g.kgroups, [&](int n, int k) -> float {
+      if (n >= Cout) return 0.f;
+      const int tap = k / Cin, c = k - tap * Cin;
+      return (*W)[((size_t)n * Cin + c) * 9 + tap];
+    });
+    choose_variant(g, false);
+    return g;
+  }
+
+  SmallW small(const std::string& name, int Cout, int Cin, bool bias) {
+    SmallW s;
+    s.Cout = Cout;
+    s.Cin = Cin;
+    const std::vector<float>* W = get(name + ".weight");
+    const std::vector<float>* B = bias ? get(name + ".bias") : nullptr;
+    if (err) return s;
+    s.w = arena.add(*W);
+    if (B) s.bias = arena.add(*B);
+    return s;
+  }
+
+  BlockW block(const std::string& p, int C, int heads) {
+    BlockW b;
+    const kdlae_t_config& c = h->cfg;
+    b.C = C;
+    b.heads = heads;
+    b.Ch = C / heads;
+    b.hid = hid_of(c, C);
+    b.hidS = ru16(b.hid);
+    const int hid = b.hid, hidS = b.hidS;
+    b.qkv = pointwise(p + ".attn.qkv", 3 * C, C, C, 3 * C, [](int n) { return n; }, p + ".norm1", c.bias, true);
+    const std::vector<float>* dw = get(p + ".attn.qkv_dwconv.weight");
+    const std::vector<float>* dwb = c.bias ? get(p + ".attn.qkv_dwconv.bias") : nullptr;
+    const std::vector<float>* pw = get(p + ".attn.project_out.weight");
+    const std::vector<float>* pb = c.bias ? get(p + ".attn.project_out.bias") : nullptr;
+    const std::vector<float>* tp = get(p + ".attn.temperature");
+    const std::vector<float>* fw = get(p + ".ffn.dwconv.weight");
+    const std::vector<float>* fb = c.bias ? get(p + ".ffn.dwconv.bias") : nullptr;
+    if (err) return b;
+    {
+      std::vector<float> v((size_t)9 * 3 * C);
+      for (int ch = 0; ch < 3 * C; ++ch)
+        for (int t = 0; t < 9; ++t) v[(size_t)t * 3 * C + ch] = (*dw)[(size_t)ch * 9 + t];
+      b.dwqkv = arena.add(v);
+      if (dwb) b.dwqkv_b = arena.add(*dwb);
+    }
+    b.proj = arena.add(*pw);
+    if (pb) {
+      std::vector<float> v((size_t)C, 0.f);
+      std::copy(pb->begin(), pb->end(), v.begin());
+      b.proj_b = arena.add(v);
+    }
+    b.temp = arena.add(*tp);
+    b.proj_gemm.ntiles = C / 16;
+    b.proj_gemm.kgroups = C / 16;
+    b.proj_gemm.N = C;
+    b.proj_gemm.K = C;
+    b.proj_gemm.n_true = C;
+    b.proj_gemm.k_true = C;
+    b.proj_gemm.bias = b.proj_b;
+    choose_variant(b.proj_gemm, true);
+    // FFN: project_in rows [x1 (hid) | x2 (hid)] -> stored [x1 padded to hidS | x2 padded to hidS]
+    auto rmap = [hid, hidS](int n) -> int {
+      if (n < hidS) return n < hid ? n : -1;
+      const int m = n - hidS;
+      return m < hid ? hid + m : -1;
+    };
+    b.pin = pointwise(p + ".ffn.project_in", 2 * hid, C, C, 2 * hidS, rmap, p + ".norm2", c.bias, true);
+    {
+      std::vector<float> v((size_t)9 * 2 * hidS, 0.f), vb((size_t)2 * hidS, 0.f);
+      for (int n = 0; n < 2 * hidS; ++n) {
+        const int src = rmap(n);
+        if (src < 0) continue;
+        for (int t = 0; t < 9; ++t) v[(size_t)t * 2 * hidS + n] = (*fw)[(size_t)src * 9 + t];
+        if (fb) vb[n] = (*fb)[src];
+      }
+      b.dwffn = arena.add(v);
+      if (fb) b.dwffn_b = arena.add(vb);
+    }
+    b.pout = pointwise(p + ".ffn.project_out", C, hid, hidS, C, [](int n) { return n; }, "", c.bias, false);
+    return b;
+  }
+
+  std::vector<BlockW> stage(const std::string& n, int cnt, int C, int heads) {
+    std::vector<BlockW> v;
+    for (int i = 0; i < cnt; ++i) v.push_back(block(n + "." + std::to_string(i), C, heads));
+    return v;
+  }
+};
+
+// ----------------------------------------------------------------------------- workspace plan
+struct View {
+  float* p;
+  int ld;
+};
+
+struct Plan {
+  size_t total = 0;
+  size_t catL1, catL2, catL3, lat, dec3, dec2, out4, refo, cenb, srs;
+  size_t qkv, vbuf, fpre, fg, stats, part, red, Mp;
+  size_t take(size_t floats) {
+    size_t off = total;
+    total += (floats * 4 + 255) / 256 * 256;
+    return off;
+  }
+};
+
+static int nslots_for(int HW) {
+  const int steps = (HW + 63) / 64;
+  int n = (steps + 15) / 16;
+  return std::max(1, std::min(64, n));
+}
+
+static Plan make_plan(const kdlae_t_handle* h, int B, int H, int W) {
+  const kdlae_t_config& c = h->cfg;
+  const long long d = c.dim;
+  const long long P1 = (long long)B * H * W, P2 = P1 / 4, P3 = P1 / 16, P4 = P1 / 64, Psr = 4 * P1;
+  Plan pl;
+  pl.catL1 = pl.take(P1 * 2 * d);
+  pl.catL2 = pl.take(P2 * 4 * d);
+  pl.catL3 = pl.take(P3 * 8 * d);
+  pl.lat = pl.take(P4 * 8 * d);
+  pl.dec3 = pl.take(P3 * 4 * d);
+  pl.dec2 = pl.take(P2 * 2 * d);
+  pl.out4 = pl.take(P1 * 4);
+  pl.refo = pl.take(P1 * 2 * d);
+  pl.cenb = c.static_train ? pl.take(P1 * 2 * d) : 0;
+  pl.srs = c.static_train ? pl.take(Psr * d) : 0;
+  // per-block scratch: max over every stage that runs
+  long long mq = 0, mv = 0, mfp = 0, mfg = 0, mst = 0, mpart = 0, mred = 0, mM = 0;
+  auto acc = [&](const std::vector<BlockW>& st, long long P, int HW) {
+    for (const BlockW& b : st) {
+      const int CT = b.Ch / 16;
+      const long long slot = (long long)CT * CT * 256 + 2 * b.Ch;
+      mq = std::max(mq, P * 3 * b.C);
+      mv = std::max(mv, P * b.C);
+      mfp = std::max(mfp, P * 2 * b.hidS);
+      mfg = std::max(mfg, P * b.hidS);
+      mst = std::max(mst, P * 2);
+      mpart = std::max(mpart, (long long)B * b.heads * nslots_for(HW) * slot);
+      mred = std::max(mred, (long long)B * b.heads * slot);
+      mM = std::max(mM, (long long)B * b.C * b.C);
+    }
+  };
+  const int HW1 = H * W;
+  acc(h->enc1, P1, HW1);
+  acc(h->enc2, P2, HW1 / 4);
+  acc(h->enc3, P3, HW1 / 16);
+  acc(h->latent, P4, HW1 / 64);
+  acc(h->dec3, P3, HW1 / 16);
+  acc(h->dec2, P2, HW1 / 4);
+  acc(h->dec1, P1, HW1);
+  acc(h->refinement, P1, HW1);
+  acc(h->refinement_out, P1, HW1);
+  acc(h->enhance, Psr, HW1 * 4);
+  pl.qkv = pl.take(mq);
+  pl.vbuf = pl.take(mv);
+  pl.fpre = pl.take(mfp);
+  pl.fg = pl.take(mfg);
+  pl.stats = pl.take(mst);
+  pl.part = pl.take(mpart);
+  pl.red = pl.take(mred);
+  pl.Mp = pl.take(mM);
+  return pl;
+}
+
+// ----------------------------------------------------------------------------- forward
+struct Fwd {
+  kdlae_t_handle* h;
+  hipStream_t s;
+  char* ws;
+  Plan pl;
+  int B;
+
+  float* buf(size_t off) { return reinterpret_cast<float*>(ws + off); }
+
+  bool probing(int cls, int C) const {
+    return h->probe_class == cls && (h->probe_level == 0 || h->probe_level == C);
+  }
+  int probe_begin(int cls, int C) {
+    if (!probing(cls, C)) return KDLAE_OK;
+    if (h->ev_used + 2 > h->ev.size()) {
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        h->ev.push_back(e);
+      }
+    }
+    HIPCHK(hipEventRecord(h->ev[h->ev_used], s));
+    return KDLAE_OK;
+  }
+  int probe_end(int cls, int C, double bytes, double flops) {
+    if (!probing(cls, C)) return KDLAE_OK;
+    HIPCHK(hipEventRecord(h->ev[h->ev_used + 1], s));
+    h->ev_used += 2;
+    h->probe_bytes += bytes;
+    h->probe_flops += flops;
+    h->probe_launches += 1;
+    return KDLAE_OK;
+  }
+
+  // GEMM launch on views
+  int gemm(const Gemm& g, const float* W, long long w_img_stride, View in, int Hh, int Ww, View out,
+           int out_mode, const float* R, int ldr, int ln, int ln_C, int probeC) {
+    const int HW = Hh * Ww;
+    const long long lim = 1LL << 31;
+    const int ldmax = std::max({in.ld, out.ld, ldr});
+    if ((long long)HW * ldmax >= lim) return fail(KDLAE_EINVAL_SHAPE, "image too large for 32-bit in-image offsets");
+    GemmParams p{};
+    p.A = in.p;
+    p.lda = in.ld;
+    p.cg_per_tap = g.cg_per_tap;
+    p.kgroups = g.kgroups;
+    p.ksize = g.ksize;
+    p.dil = 1;
+    p.Wp = W;
+    p.w_img_stride = w_img_stride;
+    p.ntiles = g.ntiles;
+    p.N = g.N;
+    p.bias = h->P(g.bias);
+    p.out = out.p;
+    p.ldo = out.ld;
+    p.R = R;
+    p.ldr = ldr;
+    p.ln = ln;
+    p.ln_C = ln_C;
+    p.relu = 0;
+    p.Bn = B;
+    p.H = Hh;
+    p.W = Ww;
+    p.out_mode = out_mode;
+    p.tiles_per_img = (int)ceil_div(HW, kGemmRows);
+    p.total_tiles = B * p.tiles_per_img;
+    const int nch = (int)ceil_div(g.ntiles, g.NT);
+    p.kchunks = (int)ceil_div(g.kgroups, g.KG);
+    p.stats = nullptr;
+    if (ln && (p.kchunks > 1 || g.kgroups * 16 != ln_C)) {
+      HIPCHK(launch_ln_stats(in.p, in.ld, ln_C, (long long)B * HW, buf(pl.stats), s));
+      p.stats = buf(pl.stats);
+    }
+    int gx = (int)std::min<long long>(p.total_tiles, std::max(1, 1024 / nch));
+    p.tiles_per_block = (int)ceil_div(p.total_tiles, gx);
+    gx = (int)ceil_div(p.total_tiles, p.tiles_per_block);
+    int rc = probe_begin(1, probeC);
+    if (rc) return rc;
+    HIPCHK(launch_gemm(p, g.NT, g.KG, gx, s));
+    const double P = (double)B * HW;
+    const double kin = g.ksize == 3 ? g.k_true / 9.0 : g.k_true;
+    const double bytes = 4.0 * (P * kin + P * g.n_true * (R ? 2.0 : 1.0) + (double)g.n_true * g.k_true);
+    return probe_end(1, probeC, bytes, 2.0 * P * g.n_true * g.k_true);
+  }
+
+  int block(const BlockW& b, View x, int Hh, int Ww) {
+    const int HW = Hh * Ww;
+    const int ln = h->cfg.layernorm_biasfree ? 1 : 2;
+    const long long P = (long long)B * HW;
+    int rc;
+    // --- attention
+    View qkv{buf(pl.qkv), 3 * b.C};
+    rc = gemm(b.qkv, h->P(b.qkv.w), 0, x, Hh, Ww, qkv, 0, nullptr, 0, ln, b.C, b.C);
+    if (rc) return rc;
+    GramParams gp{};
+    gp.qkv = qkv.p;
+    gp.ld = qkv.ld;
+    gp.wdw = h->P(b.dwqkv);
+    gp.bdw = h->P(b.dwqkv_b);
+    gp.v_out = buf(pl.vbuf);
+    gp.ldv = b.C;
+    gp.partial = buf(pl.part);
+    gp.C = b.C;
+    gp.heads = b.heads;
+    gp.Ch = b.Ch;
+    gp.Bn = B;
+    gp.H = Hh;
+    gp.W = Ww;
+    gp.nslots = nslots_for(HW);
+    const int CT = b.Ch / 16;
+    gp.slot_floats = CT * CT * 256 + 2 * b.Ch;
+    if ((rc = probe_begin(2, b.C))) return rc;
+    HIPCHK(launch_dwconv_gram(gp, s));
+    if ((rc = probe_end(2, b.C, 4.0 * P * 4 * b.C, 2.0 * P * (27.0 * b.C + (double)b.C * b.Ch)))) return rc;
+    HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
+    HIPCHK(launch_attn_fold(buf(pl.red), gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
+    rc = gemm(b.proj_gemm, buf(pl.Mp), (long long)b.C * b.C, View{buf(pl.vbuf), b.C}, Hh, Ww, x, 0, x.p, x.ld, 0,
+              0, b.C);
+    if (rc) return rc;
+    // --- feed-forward
+    View fpre{buf(pl.fpre), 2 * b.hidS};
+    rc = gemm(b.pin, h->P(b.pin.w), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
+    if (rc) return rc;
+    GateParams ga{};
+    ga.x = fpre.p;
+    ga.ld = fpre.ld;
+    ga.hidS = b.hidS;
+    ga.w = h->P(b.dwffn);
+    ga.b = h->P(b.dwffn_b);
+    ga.out = buf(pl.fg);
+    ga.ldo = b.hidS;
+    ga.Bn = B;
+    ga.H = Hh;
+    ga.W = Ww;
+    if ((rc = probe_begin(3, b.C))) return rc;
+    HIPCHK(launch_dwconv_gate(ga, s));
+    if ((rc = probe_end(3, b.C, 4.0 * P * 3 * b.hid, 2.0 * P * 18.0 * b.hid))) return rc;
+    return gemm(b.pout, h->P(b.pout.w), 0, View{buf(pl.fg), b.hidS}, Hh, Ww, x, 0, x.p, x.ld, 0, 0, b.C);
+  }
+
+  int stage(const std::vector<BlockW>& st, View x, int Hh, int Ww) {
+    for (const BlockW& b : st) {
+      int rc = block(b, x, Hh, Ww);
+      if (rc) return rc;
+    }
+    return KDLAE_OK;
+  }
+
+  int small_in(const SmallW& w, const float* in, long long sb, long long sc, long long sy, long long sx, int Hh,
+               int Ww, View out, int dil) {
+    SmallInParams p{};
+    p.in = in;
+    p.sb = sb;
+    p.sc = sc;
+    p.sy = sy;
+    p.sx = sx;
+    p.Cin = w.Cin;
+    p.Cout = w.Cout;
+    p.dil = dil;
+    p.w = h->P(w.w);
+    p.bias = h->P(w.bias);
+    p.out = out.p;
+    p.ldo = out.ld;
+    p.Bn = B;
+    p.H = Hh;
+    p.W = Ww;
+    HIPCHK(launch_conv_small_in(p, s));
+    return KDLAE_OK;
+  }
+
+  int small_out(const SmallW& w, View in, int Hh, int Ww, float* out, int nchw, int ldo, const float* res,
+                const float* extra) {
+    SmallOutParams p{};
+    p.in = in.p;
+    p.ld = in.ld;
+    p.Cin = w.Cin;
+    p.Cout = w.Cout;
+    p.w = h->P(w.w);
+    p.bias = h->P(w.bias);
+    p.Bn = B;
+    p.H = Hh;
+    p.W = Ww;
+    p.out = out;
+    p.out_nchw = nchw;
+    p.ldo = ldo;
+    p.res = res;
+    p.extra = extra;
+    HIPCHK(launch_conv_small_out(p, s));
+    return KDLAE_OK;
+  }
+
+  int run(const float* img, const float* rate, int H, int W, float* hq, float* sr) {
+    const kdlae_t_config& c = h->cfg;
+    const int d = c.dim;
+    int rc;
+    const int H2 = H / 2, W2 = W / 2, H3 = H / 4, W3 = W / 4, H4 = H / 8, W4 = W / 8;
+    float* L1 = buf(pl.catL1);
+    float* L2 = buf(pl.catL2);
+    float* L3 = buf(pl.catL3);
+    View e1{L1 + d, 2 * d}, e2{L2 + 2 * d, 4 * d}, e3{L3 + 4 * d, 8 * d}, lat{buf(pl.lat), 8 * d};
+    const long long HW = (long long)H * W;
+    const int ci = c.inp_channels;
+    // patch_embed (:275) from NCHW img into the level-1 concat buffer's second half
+    if ((rc = small_in(h->patch_embed, img, ci * HW, HW, W, 1, H, W, e1, 1))) return rc;
+    if ((rc = stage(h->enc1, e1, H, W))) return rc;
+    if ((rc = gemm(h->down1_2, h->P(h->down1_2.w), 0, e1, H, W, e2, 1, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = stage(h->enc2, e2, H2, W2))) return rc;
+    if ((rc = gemm(h->down2_3, h->P(h->down2_3.w), 0, e2, H2, W2, e3, 1, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = stage(h->enc3, e3, H3, W3))) return rc;
+    if ((rc = gemm(h->down3_4, h->P(h->down3_4.w), 0, e3, H3, W3, lat, 1, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = stage(h->latent, lat, H4, W4))) return rc;
+    // decoder level 3 (:288-291)
+    if ((rc = gemm(h->up4_3, h->P(h->up4_3.w), 0, lat, H4, W4, View{L3, 8 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
+    View d3{buf(pl.dec3), 4 * d};
+    if ((rc = gemm(h->reduce3, h->P(h->reduce3.w), 0, View{L3, 8 * d}, H3, W3, d3, 0, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = stage(h->dec3, d3, H3, W3))) return rc;
+    // decoder level 2 (:293-296)
+    if ((rc = gemm(h->up3_2, h->P(h->up3_2.w), 0, d3, H3, W3, View{L2, 4 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
+    View d2{buf(pl.dec2), 2 * d};
+    if ((rc = gemm(h->reduce2, h->P(h->reduce2.w), 0, View{L2, 4 * d}, H2, W2, d2, 0, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = stage(h->dec2, d2, H2, W2))) return rc;
+    // decoder level 1 + refinement (:298-302), in place on the full 2d-channel concat buffer
+    if ((rc = gemm(h->up2_1, h->P(h->up2_1.w), 0, d2, H2, W2, View{L1, 2 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
+    View d1{L1, 2 * d};
+    if ((rc = stage(h->dec1, d1, H, W))) return rc;
+    if ((rc = stage(h->refinement, d1, H, W))) return rc;
+    const int co = c.out_channels;
+    if (c.params_cat) {
+      // output (:314) + cat denoise_rate (:316) -> output_param dil 2 (:317) -> refinement_out -> output2 + img
+      float* o4 = buf(pl.out4);
+      if ((rc = small_out(h->output, d1, H, W, o4, 0, 4, nullptr, rate))) return rc;
+      View ro{buf(pl.refo), 2 * d};
+      if ((rc = small_in(h->output_param, o4, 4 * HW, 1, 4LL * W, 4, H, W, ro, 2))) return rc;
+      if ((rc = stage(h->refinement_out, ro, H, W))) return rc;
+      if ((rc = small_out(h->output2, ro, H, W, hq, 1, 0, img, nullptr))) return rc;
+    } else {
+      if ((rc = small_out(h->output, d1, H, W, hq, 1, 0, img, nullptr))) return rc;
+    }
+    if (c.static_train) {
+      // sr head on the UNclamped hq (:326-329)
+      View cb{buf(pl.cenb), 2 * d};
+      if ((rc = small_in(h->cen, hq, co * HW, HW, W, 1, H, W, cb, 1))) return rc;
+      View sv{buf(pl.srs), d};
+      if ((rc = gemm(h->upen, h->P(h->upen.w), 0, cb, H, W, sv, 2, nullptr, 0, 0, 0, -1))) return rc;
+      if ((rc = stage(h->enhance, sv, 2 * H, 2 * W))) return rc;
+      if ((rc = small_out(h->outputen, sv, 2 * H, 2 * W, sr, 1, 0, nullptr, nullptr))) return rc;
+    }
+    return KDLAE_OK;
+  }
+};
+
+}  // namespace kdlae
+
+// ============================================================================= C ABI
+extern "C" {
+
+const char* kdlae_last_error(void) { return kdlae::g_err.c_str(); }
+int kdlae_abi_version(void) { return 1; }
+
+int kdlae_t_create(const kdlae_t_config* cfg, int device, kdlae_t_handle** out) {
+  if (!cfg || !out) return fail(KDLAE_ESTATE, "null argument");
+  *out = nullptr;
+  int rc = validate(*cfg);
+  if (rc) return rc;
+  auto* h = new kdlae_t_handle();
+  h->cfg = *cfg;
+  h->device = device;
+  build_keys(h);
+  *out = h;
+  return KDLAE_OK;
+}
+
+int kdlae_t_destroy(kdlae_t_handle* h) {
+  if (!h) return KDLAE_OK;
+  if (h->dev) (void)hipFree(h->dev);
+  for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+  delete h;
+  return KDLAE_OK;
+}
+
+int kdlae_t_num_params(const kdlae_t_handle* h) { return h ? (int)h->keys.size() : 0; }
+
+int kdlae_t_param_info(const kdlae_t_handle* h, int index, const char** name, int64_t* numel) {
+  if (!h || index < 0 || index >= (int)h->keys.size()) return fail(KDLAE_EPARAM, "param index out of range");
+  if (name) *name = h->keys[index].first.c_str();
+  if (numel) *numel = h->keys[index].second;
+  return KDLAE_OK;
+}
+
+int kdlae_t_set_param(kdlae_t_handle* h, const char* name, const float* host_data, int64_t numel) {
+  if (!h || !name || !host_data) return fail(KDLAE_ESTATE, "null argument");
+  auto it = h->key_index.find(name);
+  if (it == h->key_index.end()) return fail(KDLAE_EPARAM, std::string("unexpected key in state_dict: ") + name);
+  if (h->keys[it->second].second != numel)
+    return fail(KDLAE_EPARAM, std::string("size mismatch for ") + name + ": expected " +
+                                  std::to_string(h->keys[it->second].second) + " got " + std::to_string(numel));
+  h->staged[name].assign(host_data, host_data + numel);
+  h->committed = false;
+  return KDLAE_OK;
+}
+
+int kdlae_t_commit_params(kdlae_t_handle* h, void* stream) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  for (auto& kv : h->keys)
+    if (!h->staged.count(kv.first)) return fail(KDLAE_EPARAM, "missing state_dict entry: " + kv.first);
+  HIPCHK(hipSetDevice(h->device));
+  const kdlae_t_config& c = h->cfg;
+  Packer pk{h};
+  const int d = c.dim;
+  const int* nb = c.num_blocks;
+  const int* hd = c.heads;
+  const int nr = c.num_refinement_blocks;
+  h->patch_embed = pk.small("patch_embed.proj", d, c.inp_channels, false);
+  h->enc1 = pk.stage("encoder_level1", nb[0], d, hd[0]);
+  h->down1_2 = pk.conv3("down1_2.body.0", d / 2, d);
+  h->enc2 = pk.stage("encoder_level2", nb[1], 2 * d, hd[1]);
+  h->down2_3 = pk.conv3("down2_3.body.0", d, 2 * d);
+  h->enc3 = pk.stage("encoder_level3", nb[2], 4 * d, hd[2]);
+  h->down3_4 = pk.conv3("down3_4.body.0", 2 * d, 4 * d);
+  h->latent = pk.stage("latent", nb[3], 8 * d, hd[3]);
+  h->up4_3 = pk.conv3("up4_3.body.0", 16 * d, 8 * d);
+  h->reduce3 = pk.pointwise("reduce_chan_level3", 4 * d, 8 * d, 8 * d, 4 * d, [](int n) { return n; }, "", c.bias, false);
+  h->dec3 = pk.stage("decoder_level3", nb[2], 4 * d, hd[2]);
+  h->up3_2 = pk.conv3("up3_2.body.0", 8 * d, 4 * d);
+  h->reduce2 = pk.pointwise("reduce_chan_level2", 2 * d, 4 * d, 4 * d, 2 * d, [](int n) { return n; }, "", c.bias, false);
+  h->dec2 = pk.stage("decoder_level2", nb[1], 2 * d, hd[1]);
+  h->up2_1 = pk.conv3("up2_1.body.0", 4 * d, 2 * d);
+  h->dec1 = pk.stage("decoder_level1", nb[0], 2 * d, hd[0]);
+  h->refinement = pk.stage("refinement", nr, 2 * d, hd[0]);
+  h->output = pk.small("output", c.out_channels, 2 * d, c.bias);
+  h->output_param = pk.small("output_param", 2 * d, c.out_channels + 1, c.bias);
+  h->refinement_out = pk.stage("refinement_out", nr, 2 * d, hd[0]);
+  h->output2 = pk.small("output2", c.out_channels, 2 * d, c.bias);
+  if (c.static_train) {
+    const int hc = 2 * d;
+    h->cen = pk.small("cen", hc, c.out_channels, c.bias);
+    h->upen = pk.conv3("upen.body.0", 2 * hc, hc);
+    h->enhance = pk.stage("enhance", nr, hc / 2, hd[0]);
+    h->outputen = pk.small("outputen", c.out_channels, hc / 2, c.bias);
+  }
+  if (pk.err) return pk.err;
+  if (h->dev) {
+    HIPCHK(hipFree(h->dev));
+    h->dev = nullptr;
+  }
+  const size_t n = std::max<size_t>(pk.arena.h.size(), 64);
+  pk.arena.h.resize(n, 0.f);
+  HIPCHK(hipMalloc(&h->dev, n * sizeof(float)));
+  h->dev_floats = n;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  HIPCHK(hipMemcpyAsync(h->dev, pk.arena.h.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  h->committed = true;
+  return KDLAE_OK;
+}
+
+int64_t kdlae_t_workspace_bytes(const kdlae_t_handle* h, int B, int H, int W) {
+  if (!h || !h->committed) {
+    fail(KDLAE_ESTATE, "workspace_bytes needs committed params");
+    return -1;
+  }
+  if (B <= 0 || H <= 0 || W <= 0 || H % 8 || W % 8) {
+    fail(KDLAE_EINVAL_SHAPE, "B, H, W must be positive with H % 8 == 0 and W % 8 == 0");
+    return -1;
+  }
+  return (int64_t)make_plan(h, B, H, W).total;
+}
+
+int kdlae_t_forward(kdlae_t_handle* h, const float* img, const float* rate, int B, int H, int W, float* hq,
+                    float* sr, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  if (!h->committed) return fail(KDLAE_ESTATE, "forward before kdlae_t_commit_params");
+  if (B <= 0 || H <= 0 || W <= 0 || H % 8 || W % 8)
+    return fail(KDLAE_EINVAL_SHAPE, "KDLAE_teacher needs H % 8 == 0 and W % 8 == 0 (pixel_unshuffle x3, KDLAE_model.py:187)");
+  if (!img || !hq) return fail(KDLAE_ESTATE, "img and hq are required");
+  if (h->cfg.params_cat && !rate) return fail(KDLAE_ESTATE, "denoise_rate is required when params=='cat'");
+  if ((sr != nullptr) != (h->cfg.static_train != 0))
+    return fail(KDLAE_ESTATE, "sr must be non-null iff static=='train'");
+  Fwd f{h, reinterpret_cast<hipStream_t>(stream), reinterpret_cast<char*>(workspace), make_plan(h, B, H, W), B};
+  if ((int64_t)f.pl.total > workspace_bytes) return fail(KDLAE_ESTATE, "workspace too small");
+  HIPCHK(hipSetDevice(h->device));
+  return f.run(img, rate, H, W, hq, sr);
+}
+
+int kdlae_t_probe_arm(kdlae_t_handle* h, int kernel_class, int level_filter) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  h->probe_class = kernel_class;
+  h->probe_level = level_filter;
+  h->ev_used = 0;
+  h->probe_bytes = h->probe_flops = 0;
+  h->probe_launches = 0;
+  return KDLAE_OK;
+}
+
+int kdlae_t_probe_read(kdlae_t_handle* h, double* ms, int64_t* launches, double* bytes, double* flops) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  double tot = 0;
+  for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+    HIPCHK(hipEventSynchronize(h->ev[i + 1]));
+    float m = 0;
+    HIPCHK(hipEventElapsedTime(&m, h->ev[i], h->ev[i + 1]));
+    tot += m;
+  }
+  if (ms) *ms = tot;
+  if (launches) *launches = h->probe_launches;
+  if (bytes) *bytes = h->probe_bytes;
+  if (flops) *flops = h->probe_flops;
+  return KDLAE_OK;
+}
+
+}  // extern "C"

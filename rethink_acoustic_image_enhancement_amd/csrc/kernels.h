@@ -1,0 +1,91 @@
+// Internal launch interface of the KDLAE HIP kernels (gfx950 / CDNA4).
+//
+// Activation layout in HBM: NHWC fp32 "views" — pixel-major, channels contiguous, a view is
+// (base pointer, pixel stride `ld` in floats).  A view may be a channel slice of a wider buffer,
+// which is how torch.cat in the reference (KDLAE_model.py:289,294,299,316) disappears: the
+// producer writes straight into its half of the concatenated buffer.
+//
+// Packed 1x1 / implicit-GEMM weights ("fragment order"): for output tile t (16 channels) and
+// k-group g (16 reduction indices) one 1 KiB record of 64 lanes x float4 holds
+// W[16t + (lane & 15)][16g + 4*(lane >> 4) + e], e = 0..3 — exactly the B operand each lane of
+// v_mfma_f32_16x16x4_f32 consumes over four k-steps, so a wave reads it as one contiguous 1 KiB.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kdlae {
+
+constexpr int kGemmThreads = 512;            // 8 waves
+constexpr int kGemmRT = 2;                   // 16-row subtiles per wave
+constexpr int kGemmRows = 8 * kGemmRT * 16;  // 256 pixels per block tile
+
+struct GemmParams {
+  const float* A;  int lda;        // input view
+  int cg_per_tap;                  // channel groups (of 16) per tap = Cin_pad / 16
+  int kgroups;                     // taps * cg_per_tap
+  int ksize, dil;                  // 1 (pointwise) or 3 (implicit GEMM, zero padding = dil)
+  const float* Wp; long long w_img_stride; int ntiles;
+  int N;                           // output channels stored (padded channels included)
+  const float* bias;               // [ntiles*16] or null
+  float* out; int ldo;
+  const float* R; int ldr;         // residual view (may alias out) or null
+  const float* stats;              // [P][2] = (mean, rstd) or null
+  int ln;                          // 0 none, 1 BiasFree LN on A, 2 WithBias LN on A
+  int ln_C;                        // LN channel count (true C)
+  int relu;                        // apply ReLU after bias/residual
+  int Bn, H, W;                    // geometry of the input grid
+  int out_mode;                    // 0 plain, 1 PixelUnshuffle(2), 2 PixelShuffle(2)
+  int tiles_per_img, total_tiles, tiles_per_block;
+  int kchunks;
+};
+
+struct GramParams {
+  const float* qkv; int ld;        // [P][ld]: q at [0,C), k at [C,2C), v at [2C,3C)
+  const float* wdw;                // [9][3C] tap-major
+  const float* bdw;                // [3C] or null
+  float* v_out; int ldv;
+  float* partial;                  // [B][heads][nslots][slot_floats]
+  int C, heads, Ch;
+  int Bn, H, W;
+  int nslots, slot_floats;
+};
+
+struct GateParams {
+  const float* x; int ld;          // [P][ld]: x1 at [0,hidS), x2 at [hidS, 2 hidS)
+  int hidS;
+  const float* w;                  // [9][2 hidS]
+  const float* b;                  // [2 hidS] or null
+  float* out; int ldo;
+  int Bn, H, W;
+};
+
+struct SmallInParams {             // 3x3 conv with Cin <= 4, Cout % 16 == 0
+  const float* in; long long sb, sc, sy, sx;
+  int Cin, Cout, dil;
+  const float* w; const float* bias;   // w: [Cout][Cin][3][3]
+  float* out; int ldo;
+  int Bn, H, W;
+};
+
+struct SmallOutParams {            // 3x3 conv with Cout <= 4, Cin % 4 == 0
+  const float* in; int ld; int Cin, Cout;
+  const float* w; const float* bias;   // w: [Cout][Cin][3][3]
+  int Bn, H, W;
+  float* out; int out_nchw; int ldo;   // NCHW (ldo unused) or NHWC with pixel stride ldo
+  const float* res;                    // NCHW residual (same shape as out) or null
+  const float* extra;                  // NCHW [B,1,H,W] copied into channel Cout (NHWC mode) or null
+};
+
+hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int grid_x, hipStream_t s);
+bool gemm_has_variant(int NT, int KG, bool conv3);
+hipError_t launch_ln_stats(const float* x, int ld, int C, long long P, float* stats, hipStream_t s);
+hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s);
+hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int heads, int nslots,
+                              int slot_floats, hipStream_t s);
+hipError_t launch_attn_fold(const float* reduced, int slot_floats, const float* proj, const float* temp,
+                            float* Mpacked, int Bn, int C, int heads, hipStream_t s);
+hipError_t launch_dwconv_gate(const GateParams& p, hipStream_t s);
+hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s);
+hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s);
+
+}  // namespace kdlae

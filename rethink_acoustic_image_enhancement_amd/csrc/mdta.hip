@@ -1,0 +1,347 @@
+// MDTA (transposed channel attention) and GDFN (gated dwconv FFN) kernels, NHWC fp32.
+//
+// Reference math (KDLAE/KDLAE_model.py):
+//   Attention.forward :124-145   qkv_dwconv -> chunk(q,k,v) -> per head q^=q/max(|q|_HW,1e-12),
+//                                 k^ likewise -> A = softmax(q^ k^T * temperature) -> A v -> project_out
+//   FeedForward.forward :101-106  dwconv -> chunk(x1,x2) -> gelu_erf(x1) * x2
+//
+// MDTA is restated as three passes so that q and k never touch HBM:
+//   1. dwconv_gram: depthwise 3x3 of q,k,v for a run of pixels, v written out, and per head the
+//      UN-normalised Gram G = q k^T (v_mfma_f32_16x16x4_f32, pixels as the reduction index) and
+//      the squared norms |q_c|^2, |k_c|^2 accumulated -> one partial slot per workgroup.
+//   2. gram_reduce: deterministic fixed-order sum of the slots (no float atomics).
+//   3. attn_fold: A = softmax(G / (max(|q|,eps) max(|k|,eps)) * temp); M = W_proj . blockdiag(A)
+//      written directly in the packed GEMM fragment order, so "A v then project_out" is ONE GEMM
+//      (conv_gemm with per-image weights M and the residual add in its epilogue).
+#include "kernels.h"
+
+namespace kdlae {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// --------------------------------------------------------------------------- LN statistics
+// (mean, rstd) per pixel over C channels (BiasFree/WithBias LN, :50-52 / :67-70), two-pass from
+// registers; one wave per pixel, float4 per lane.  Used when a LN-fused GEMM needs K-chunking.
+__global__ __launch_bounds__(256) void ln_stats_kernel(const float* __restrict__ x, int ld, int C,
+                                                       long long P, float* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const long long wave = (blockIdx.x * 256LL + threadIdx.x) >> 6;
+  const long long nw = (gridDim.x * 256LL) >> 6;
+  const int c4 = C >> 2;
+  for (long long pix = wave; pix < P; pix += nw) {
+    const float* row = x + pix * ld;
+    f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+    if (lane < c4) v0 = *reinterpret_cast<const f32x4*>(row + 4 * lane);
+    if (lane + 64 < c4) v1 = *reinterpret_cast<const f32x4*>(row + 4 * (lane + 64));
+    float s = (v0.x + v0.y + v0.z + v0.w) + (v1.x + v1.y + v1.z + v1.w);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / (float)C;
+    f32x4 d0 = v0 - mean, d1 = v1 - mean;
+    float q = 0.f;
+    if (lane < c4) q += d0.x * d0.x + d0.y * d0.y + d0.z * d0.z + d0.w * d0.w;
+    if (lane + 64 < c4) q += d1.x * d1.x + d1.y * d1.y + d1.z * d1.z + d1.w * d1.w;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+    if (lane == 0) {
+      stats[2 * pix] = mean;
+      stats[2 * pix + 1] = 1.0f / sqrtf(q / (float)C + 1e-5f);
+    }
+  }
+}
+
+hipError_t launch_ln_stats(const float* x, int ld, int C, long long P, float* stats, hipStream_t s) {
+  long long blocks = (P + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(ln_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, ld, C, P, stats);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------- dwconv + Gram
+// grid (nslots, heads, B), 256 threads (4 waves); LDS-staged per 64-pixel step.
+//  phase 1: wave w computes the depthwise 3x3 of q, k, v for the 16-pixel unit 4*step + w:
+//           lane (i = lane & 15, q = lane >> 4) -> channel 16 ct + i at pixels 16u + 4q + s;
+//           v goes to HBM, q and k to LDS [64 px][S] (S = Ch padded to 16 mod 32 -> the MFMA
+//           operand reads below are bank-conflict free), squared norms accumulate in registers.
+//  phase 2: the CT x CT Gram tiles of this head are dealt to the 4 waves; each wave runs
+//           v_mfma_f32_16x16x4_f32 over the 64 staged pixels (16 k-steps) from LDS.
+template <int CT>
+__global__ __launch_bounds__(256) void dwconv_gram_kernel(GramParams p) {
+  constexpr int Ch = CT * 16;
+  constexpr int S = (Ch % 32 == 16) ? Ch : Ch + 16;
+  constexpr int PPW = (CT * CT + 3) / 4;  // Gram tile pairs per wave
+  __shared__ float qs[64 * S];
+  __shared__ float ks[64 * S];
+  __shared__ float nacc[4][4][2 * Ch];  // [wave][lane>>4][q|k channel] running squared norms
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int slot = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int HW = p.H * p.W;
+  const int C = p.C;
+  const float* __restrict__ X = p.qkv + (long long)b * HW * p.ld;
+  float* __restrict__ V = p.v_out + (long long)b * HW * p.ldv;
+
+  const int steps_total = (HW + 63) >> 6;
+  const int st_begin = (int)((long long)steps_total * slot / p.nslots);
+  const int st_end = (int)((long long)steps_total * (slot + 1) / p.nslots);
+
+  // uniform neighbour deltas (in floats) for the 9 taps
+  int dofs[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) dofs[t] = ((t / 3 - 1) * p.W + (t % 3 - 1)) * p.ld;
+
+  f32x4 acc[PPW];
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = li; i < 2 * Ch; i += 16) nacc[wave][lq][i] = 0.f;
+
+  for (int st = st_begin; st < st_end; ++st) {
+    // ---- phase 1: depthwise conv of this wave's unit
+    const int u = st * 4 + wave;
+    int base[4];
+    unsigned okm[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int pix = u * 16 + 4 * lq + s;
+      const int y = pix / p.W, x = pix - (pix / p.W) * p.W;
+      unsigned m = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+        const bool ok = pix < HW && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+        m |= ok ? (1u << t) : 0u;
+      }
+      okm[s] = m;
+      base[s] = (pix < HW ? pix : 0) * p.ld;
+    }
+#pragma unroll 1
+    for (int ct = 0; ct < CT; ++ct) {
+      const int cq = h * Ch + ct * 16 + li;
+      float n2q = 0.f, n2k = 0.f;
+#pragma unroll 1
+      for (int part = 0; part < 3; ++part) {
+        const int c = cq + part * C;
+        float w[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[t] = p.wdw[t * 3 * C + c];
+        const float bias = p.bdw ? p.bdw[c] : 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float a = bias;
+#pragma unroll
+          for (int t = 0; t < 9; ++t) {
+            const bool ok = (okm[s] >> t) & 1u;
+            const float xv = X[(ok ? base[s] + dofs[t] : 0) + c];
+            a = fmaf(ok ? xv : 0.f, w[t], a);
+          }
+          const int pix = u * 16 + 4 * lq + s;
+          const bool valid = pix < HW;
+          a = valid ? a : 0.f;
+          const int lp = wave * 16 + 4 * lq + s;
+          if (part == 0) {
+            qs[lp * S + ct * 16 + li] = a;
+            n2q = fmaf(a, a, n2q);
+          } else if (part == 1) {
+            ks[lp * S + ct * 16 + li] = a;
+            n2k = fmaf(a, a, n2k);
+          } else if (valid) {
+            V[pix * p.ldv + cq] = a;
+          }
+        }
+      }
+      nacc[wave][lq][ct * 16 + li] += n2q;
+      nacc[wave][lq][Ch + ct * 16 + li] += n2k;
+    }
+    __syncthreads();
+    // ---- phase 2: Gram tiles of this wave over the 64 staged pixels
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) {
+      const int pi = wave * PPW + k;
+      if (pi < CT * CT) {
+        const int i = pi / CT, j = pi - (pi / CT) * CT;
+#pragma unroll
+        for (int ks4 = 0; ks4 < 16; ++ks4) {
+          const int lp = ks4 * 4 + lq;
+          acc[k] = mfma4(qs[lp * S + 16 * i + li], ks[lp * S + 16 * j + li], acc[k]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- write this block's slot: Gram tiles in accumulator layout, then norms
+  float* out = p.partial + (((long long)b * p.heads + h) * p.nslots + slot) * p.slot_floats;
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) {
+    const int pi = wave * PPW + k;
+    if (pi < CT * CT) *reinterpret_cast<f32x4*>(out + (pi * 64 + lane) * 4) = acc[k];
+  }
+__syncthreads();
+  for (int idx = threadIdx.x; idx < 2 * Ch; idx += 256) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) t += nacc[w][g][idx];
+    out[CT * CT * 256 + idx] = t;
+  }
+}
+
+hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s) {
+  dim3 grid(p.nslots, p.heads, p.Bn);
+  switch (p.Ch / 16) {
+    case 1: hipLaunchKernelGGL(dwconv_gram_kernel<1>, grid, dim3(256), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(dwconv_gram_kernel<2>, grid, dim3(256), 0, s, p); break;
+    case 3: hipLaunchKernelGGL(dwconv_gram_kernel<3>, grid, dim3(256), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(dwconv_gram_kernel<4>, grid, dim3(256), 0, s, p); break;
+    case 6: hipLaunchKernelGGL(dwconv_gram_kernel<6>, grid, dim3(256), 0, s, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------- slot reduction
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ partial,
+                                                          float* __restrict__ reduced, int nslots,
+                                                          int slot_floats) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const long long bh = blockIdx.y;
+  if (idx >= slot_floats) return;
+  const float* src = partial + bh * nslots * (long long)slot_floats + idx;
+  float s = 0.f;
+  for (int k = 0; k < nslots; ++k) s += src[(long long)k * slot_floats];
+  reduced[bh * slot_floats + idx] = s;
+}
+
+hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int heads, int nslots,
+                              int slot_floats, hipStream_t s) {
+  dim3 grid((slot_floats + 255) / 256, Bn * heads);
+  hipLaunchKernelGGL(gram_reduce_kernel, grid, dim3(256), 0, s, partial, reduced, nslots, slot_floats);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------- softmax + fold
+// grid (C/16, heads, B).  Each block rebuilds A for (b, h) in LDS, then computes 16 rows of
+// M[n][h*Ch + c2] = sum_c1 Wproj[n][h*Ch + c1] * A[c1][c2], stored in fragment order.
+__global__ __launch_bounds__(256) void attn_fold_kernel(const float* __restrict__ reduced, int slot_floats,
+                                                        const float* __restrict__ proj,
+                                                        const float* __restrict__ temp,
+                                                        float* __restrict__ Mp, int C, int heads) {
+  extern __shared__ float sm[];
+  const int Ch = C / heads;
+  const int CT = Ch / 16;
+  float* A = sm;                  // [Ch][Ch + 1]
+  float* nrm = sm + Ch * (Ch + 1);  // [2 Ch]: 1/max(|q|,eps), 1/max(|k|,eps)
+  const int nb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const float* G = reduced + ((long long)b * heads + h) * slot_floats;
+  const int ldA = Ch + 1;
+  // decode the accumulator layout: G[(i*CT + j)*256 + lane*4 + e] = Gram[16i + 4(lane>>4) + e][16j + (lane&15)]
+  for (int idx = threadIdx.x; idx < CT * CT * 256; idx += 256) {
+    const int e = idx & 3, lane = (idx >> 2) & 63, ij = idx >> 8;
+    const int i = ij / CT, j = ij - (ij / CT) * CT;
+    A[(16 * i + 4 * (lane >> 4) + e) * ldA + 16 * j + (lane & 15)] = G[idx];
+  }
+  for (int c = threadIdx.x; c < 2 * Ch; c += 256) {
+    const float n2 = G[CT * CT * 256 + c];
+    nrm[c] = 1.0f / fmaxf(sqrtf(n2), 1e-12f);
+  }
+  __syncthreads();
+  const float tp = temp[h];
+  for (int r = threadIdx.x; r < Ch; r += 256) {
+    float* row = A + r * ldA;
+    const float sq = nrm[r];
+    float mx = -INFINITY;
+    for (int c = 0; c < Ch; ++c) {
+      const float l = (row[c] * sq * nrm[Ch + c]) * tp;
+      row[c] = l;
+      mx = fmaxf(mx, l);
+    }
+    float sum = 0.f;
+    for (int c = 0; c < Ch; ++c) {
+      const float e = expf(row[c] - mx);
+      row[c] = e;
+      sum += e;
+    }
+    const float inv = 1.0f / sum;
+    for (int c = 0; c < Ch; ++c) row[c] *= inv;
+  }
+  __syncthreads();
+  const int kgroups = C / 16;
+  float* Mb = Mp + (long long)b * C * C;
+  for (int idx = threadIdx.x; idx < 16 * Ch; idx += 256) {
+    const int nl = idx / Ch, c2 = idx - (idx / Ch) * Ch;
+    const int n = nb * 16 + nl;
+    const float* wr = proj + (long long)n * C + h * Ch;
+    float s = 0.f;
+    for (int c1 = 0; c1 < Ch; ++c1) s = fmaf(wr[c1], A[c1 * ldA + c2], s);
+    const int k = h * Ch + c2;
+    const int lane = (n & 15) + 16 * ((k & 15) >> 2);
+    Mb[(((long long)(n >> 4) * kgroups + (k >> 4)) * 64 + lane) * 4 + (k & 3)] = s;
+  }
+}
+
+hipError_t launch_attn_fold(const float* reduced, int slot_floats, const float* proj, const float* temp,
+                            float* Mpacked, int Bn, int C, int heads, hipStream_t s) {
+  const int Ch = C / heads;
+  const size_t lds = (size_t)(Ch * (Ch + 1) + 2 * Ch) * sizeof(float);
+  dim3 grid(C / 16, heads, Bn);
+  hipLaunchKernelGGL(attn_fold_kernel, grid, dim3(256), lds, s, reduced, slot_floats, proj, temp, Mpacked,
+                     C, heads);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------- GDFN dwconv + gate
+// out[p][c] = gelu_erf(dw(x1)[p][c]) * dw(x2)[p][c], c < hidS; float4 of channels per thread.
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__global__ __launch_bounds__(256) void dwconv_gate_kernel(GateParams p) {
+  const int HW = p.H * p.W;
+  const int c4n = p.hidS >> 2;
+  const long long total = (long long)p.Bn * HW * c4n;
+  const int two = 2 * p.hidS;
+  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+    const long long pix = idx / c4n;
+    const int c = (int)(idx - pix * c4n) * 4;
+    const int b = (int)(pix / HW);
+    const int pl = (int)(pix - (long long)b * HW);
+    const int y = pl / p.W, x = pl - (pl / p.W) * p.W;
+    const float* X = p.x + (long long)b * HW * p.ld;
+    f32x4 a1 = p.b ? *reinterpret_cast<const f32x4*>(p.b + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 a2 = p.b ? *reinterpret_cast<const f32x4*>(p.b + p.hidS + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      const bool ok = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      const int off = ok ? (yy * p.W + xx) * p.ld + c : c;
+      f32x4 v1 = *reinterpret_cast<const f32x4*>(X + off);
+      f32x4 v2 = *reinterpret_cast<const f32x4*>(X + off + p.hidS);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(p.w + t * two + c);
+      const f32x4 w2 = *reinterpret_cast<const f32x4*>(p.w + t * two + p.hidS + c);
+      const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+      v1 = ok ? v1 : z;
+      v2 = ok ? v2 : z;
+      a1 = v1 * w1 + a1;
+      a2 = v2 * w2 + a2;
+    }
+    f32x4 o;
+    o.x = gelu_erf(a1.x) * a2.x;
+    o.y = gelu_erf(a1.y) * a2.y;
+    o.z = gelu_erf(a1.z) * a2.z;
+    o.w = gelu_erf(a1.w) * a2.w;
+    *reinterpret_cast<f32x4*>(p.out + pix * p.ldo + c) = o;
+  }
+}
+
+hipError_t launch_dwconv_gate(const GateParams& p, hipStream_t s) {
+  const long long total = (long long)p.Bn * p.H * p.W * (p.hidS / 4);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(dwconv_gate_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace kdlae

@@ -1,0 +1,181 @@
+"""Generate golden fixtures from the IMPORTED REFERENCE (build container only).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+* Imports ``KDLAE/KDLAE_model.py`` and ``ASDQE/ASDQE_model.py`` from /root/reference (read
+  only, no bytecode written).  Nothing from the reference is copied into this repository: only
+  the numeric outputs below are saved.
+* Weights: the §8c hash recipe (rethink_acoustic_image_enhancement_amd/hashweights.py).
+* Inputs: hash images (key names stored in the fixture) and, for config 1, the decoded
+  ``Sample/MDD/origin/0001_sort.jpg`` crop stored as uint8.
+* Outputs: fp32 tensors (small shapes) or [::8, ::8] subsamples + float64 channel sums (512^2).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+from rethink_acoustic_image_enhancement_amd.hashweights import (  # noqa: E402
+    hash_images, hash_normal, hash_state_dict)
+
+REF = "/root/reference"
+sys.dont_write_bytecode = True
+
+
+def _import_ref():
+    sys.path.insert(0, os.path.join(REF, "KDLAE"))
+    sys.path.insert(0, os.path.join(REF, "ASDQE"))
+    import ASDQE_model  # noqa: F401
+    import KDLAE_model  # noqa: F401
+    return KDLAE_model, ASDQE_model
+
+
+def _load_hash(model):
+    sd = model.state_dict()
+    vals = hash_state_dict({k: tuple(v.shape) for k, v in sd.items()})
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()}, strict=True)
+    return model.eval()
+
+
+TEACHER_CASES = {
+    # name: (ctor kwargs, img shape, rate spec)
+    "t_full_b2_32": (dict(dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4,
+                          heads=[1, 2, 4, 8], LayerNorm_type="BiasFree", bias=False,
+                          static="train", params="cat"), (2, 3, 32, 32), "const:0.6,0.25"),
+    "t_full_b1_48x80": (dict(dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4,
+                             heads=[1, 2, 4, 8], LayerNorm_type="BiasFree", bias=False,
+                             static="train", params="cat"), (1, 3, 48, 80), "map"),
+    "t_tiny_withbias": (dict(dim=16, num_blocks=[1, 2, 1, 1], num_refinement_blocks=1,
+                             heads=[1, 2, 4, 8], LayerNorm_type="WithBias", bias=True,
+                             static="train", params="cat"), (2, 3, 32, 48), "map"),
+    "t_tiny_nocat_nosr": (dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1,
+                               heads=[1, 1, 2, 2], LayerNorm_type="BiasFree", bias=False,
+                               static="no", params="plus"), (1, 3, 40, 24), "const:0.5"),
+    "t_gray_1ch": (dict(inp_channels=1, out_channels=1, dim=16, num_blocks=[1, 1, 1, 1],
+                        num_refinement_blocks=1, heads=[1, 2, 4, 8],
+                        LayerNorm_type="BiasFree", bias=False, static="train", params="cat"),
+                   (1, 1, 24, 32), "const:0.9"),
+}
+
+
+def make_rate(spec, b, h, w, key):
+    if spec.startswith("const:"):
+        vals = [float(v) for v in spec[6:].split(",")]
+        vals = (vals * b)[:b]
+        return np.stack([np.full((1, h, w), v, np.float32) for v in vals])
+    return hash_images(key, (b, 1, h, w))
+
+
+def teacher_goldens(KM, out):
+    for name, (kw, shape, rspec) in TEACHER_CASES.items():
+        t0 = time.time()
+        m = _load_hash(KM.KDLAE_teacher(**kw))
+        b, c, h, w = shape
+        img = hash_images(f"img:{name}", shape)
+        rate = make_rate(rspec, b, h, w, f"rate:{name}")
+        with torch.no_grad():
+            o = m({"img": torch.from_numpy(img), "denoise_rate": torch.from_numpy(rate)})
+        d = dict(img=img, rate=rate, hq=o["hq"].numpy())
+        if o["sr"] is not None:
+            d["sr"] = o["sr"].numpy()
+        d["cfg"] = np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8)
+        np.savez_compressed(os.path.join(out, f"{name}.npz"), **d)
+        print(name, {k: v.shape for k, v in d.items()}, f"{time.time() - t0:.1f}s")
+
+
+def mdd_input():
+    """Config 1 input: 0001_sort.jpg rows 73:585, reflect-pad width 438 -> 512."""
+    from PIL import Image
+
+    im = np.asarray(Image.open(os.path.join(REF, "Sample/MDD/origin/0001_sort.jpg")).convert("RGB"))
+    crop = im[73:585]                       # [512, 438, 3] uint8
+    assert crop.shape[:2] == (512, 438), crop.shape
+    return crop
+
+
+def teacher_512(KM, out):
+    crop = mdd_input()
+    t = torch.from_numpy(crop.astype(np.float32) / 255.0).permute(2, 0, 1).unsqueeze(0)
+    t = torch.nn.functional.pad(t, (0, 74, 0, 0), mode="reflect")
+    kw = dict(dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4, heads=[1, 2, 4, 8],
+              LayerNorm_type="BiasFree", bias=False, static="train", params="cat")
+    m = _load_hash(KM.KDLAE_teacher(**kw))
+    rate = torch.full((1, 1, 512, 512), 0.6)
+    t0 = time.time()
+    with torch.no_grad():
+        o = m({"img": t, "denoise_rate": rate})
+    dt = time.time() - t0
+    hq, sr = o["hq"], o["sr"]
+    np.savez_compressed(
+        os.path.join(out, "t_mdd_512.npz"),
+        crop_u8=crop[..., 0] if (crop[..., 0] == crop[..., 1]).all() and
+        (crop[..., 0] == crop[..., 2]).all() else crop,
+        hq_sub=hq[:, :, ::8, ::8].numpy(), sr_sub=sr[:, :, ::8, ::8].numpy(),
+        hq_chsum=hq.double().sum(dim=(2, 3)).numpy(), sr_chsum=sr.double().sum(dim=(2, 3)).numpy(),
+        hq_row257=hq[:, :, 257, :].numpy(), sr_row515=sr[:, :, 515, :].numpy(),
+        ref_cpu_seconds=np.array([dt]), threads=np.array([torch.get_num_threads()]),
+        cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8))
+    print("t_mdd_512", f"{dt:.1f}s")
+
+
+STUDENT_CASES = {
+    "s_default_b2": (dict(inp_channels=1, out_channels=1, residual=True, hidden_channels=[16, 32, 64]),
+                     (2, 4, 32, 32)),
+    "s_nores_3lvl": (dict(inp_channels=1, out_channels=1, residual=False, hidden_channels=[8, 16, 16, 32]),
+                     (1, 3, 24, 40)),
+}
+
+
+def student_goldens(KM, out):
+    for name, (kw, shape) in STUDENT_CASES.items():
+        m = _load_hash(KM.KDLAE_student(**kw))
+        x = hash_images(f"frames:{name}", shape)
+        with torch.no_grad():
+            y = m(torch.from_numpy(x)).numpy()
+        np.savez_compressed(os.path.join(out, f"{name}.npz"), x=x, y=y,
+                            cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8))
+        print(name, y.shape)
+
+
+ASDQE_CASES = {
+    "a_b4_64": (dict(in_channels=3, dim=16), (4, 3, 64, 64)),
+    "a_b2_40x56": (dict(in_channels=3, dim=16), (2, 3, 40, 56)),   # exercises pad_to_multiple
+}
+
+
+def asdqe_goldens(AM, out):
+    for name, (kw, shape) in ASDQE_CASES.items():
+        m = _load_hash(AM.DenoiseRatePredictor(**kw))
+        lq = hash_images(f"lq:{name}", shape)
+        gt = np.clip(lq + 0.05 * hash_normal(f"gt:{name}", shape), 0, 1).astype(np.float32)
+        with torch.no_grad():
+            y = m(torch.from_numpy(lq), torch.from_numpy(gt)).numpy()
+        np.savez_compressed(os.path.join(out, f"{name}.npz"), lq=lq, gt=gt, score=y,
+                            cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8))
+        print(name, y.ravel())
+
+
+def main():
+    KM, AM = _import_ref()
+    out = HERE
+    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512"]
+    if "teacher" in which:
+        teacher_goldens(KM, out)
+    if "student" in which:
+        student_goldens(KM, out)
+    if "asdqe" in which:
+        asdqe_goldens(AM, out)
+    if "t512" in which:
+        teacher_512(KM, out)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+"""GPU parity of the HIP KDLAE-T path (through the C ABI) against the oracle and the goldens.
+
+Tolerance: 1e-3 fp32 max-abs on hq and sr (BASELINE.json north_star).  Every test here runs on
+cuda:0 and calls KDLAE_teacher.forward -> libkdlae.so; there is no fallback path to hide behind.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.kdlae_oracle import TeacherCfg, psnr, teacher_forward, teacher_param_shapes
+from rethink_acoustic_image_enhancement_amd.hashweights import hash_images, load_hash_weights
+from rethink_acoustic_image_enhancement_amd.KDLAE_model import KDLAE_teacher
+from tests.util import GOLDEN, hash_sd_for, load_fixture, max_abs, mdd_input_tensor
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+DEV = "cuda:0"
+
+TEACHER = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "t_*.npz"))
+                 if "mdd_512" not in f)
+
+
+def _model(kw):
+    m = KDLAE_teacher(**kw)
+    load_hash_weights(m)
+    return m.to(DEV).eval()
+
+
+def _run(m, img, rate):
+    with torch.no_grad():
+        out = m({"img": img.to(DEV), "denoise_rate": rate.to(DEV)})
+    torch.cuda.synchronize()
+    return {k: (v.cpu() if v is not None else None) for k, v in out.items()}
+
+
+@pytest.mark.parametrize("name", TEACHER)
+def test_golden_fixture(name):
+    d, kw = load_fixture(name)
+    out = _run(_model(kw), torch.from_numpy(d["img"]), torch.from_numpy(d["rate"]))
+    e_hq = max_abs(out["hq"], torch.from_numpy(d["hq"]))
+    assert e_hq <= TOL, f"hq max-abs {e_hq}"
+    if "sr" in d:
+        e_sr = max_abs(out["sr"], torch.from_numpy(d["sr"]))
+        assert e_sr <= TOL, f"sr max-abs {e_sr}"
+    else:
+        assert out["sr"] is None
+
+
+def test_mdd_512_config1():
+    """Config 1: the MDD sample at 512x512 vs the reference's subsampled outputs + channel sums."""
+    d, kw = load_fixture("t_mdd_512")
+    img = mdd_input_tensor(d)
+    out = _run(_model(kw), img, torch.full((1, 1, 512, 512), 0.6))
+    assert max_abs(out["hq"][:, :, ::8, ::8], torch.from_numpy(d["hq_sub"])) <= TOL
+    assert max_abs(out["sr"][:, :, ::8, ::8], torch.from_numpy(d["sr_sub"])) <= TOL
+    assert max_abs(out["hq"][:, :, 257, :], torch.from_numpy(d["hq_row257"])) <= TOL
+    assert max_abs(out["sr"][:, :, 515, :], torch.from_numpy(d["sr_row515"])) <= TOL
+    np.testing.assert_allclose(out["hq"].double().sum(dim=(2, 3)).numpy(), d["hq_chsum"], rtol=2e-5)
+    np.testing.assert_allclose(out["sr"].double().sum(dim=(2, 3)).numpy(), d["sr_chsum"], rtol=2e-5)
+
+
+@pytest.mark.parametrize("kw,shape", [
+    (dict(dim=48, LayerNorm_type="BiasFree", num_blocks=[1, 1, 1, 1], num_refinement_blocks=1), (3, 3, 64, 48)),
+    (dict(dim=32, heads=[1, 1, 2, 4], num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, bias=True), (2, 3, 40, 56)),
+    (dict(dim=48, heads=[1, 2, 2, 4], num_blocks=[1, 1, 1, 2], num_refinement_blocks=2,
+          LayerNorm_type="BiasFree", ffn_expansion_factor=2.0), (1, 3, 72, 32)),
+    (dict(dim=64, heads=[1, 2, 4, 8], num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, params="mul",
+          static="train"), (2, 3, 32, 32)),
+])
+def test_vs_oracle_random_configs(kw, shape):
+    """Seeded hash weights/inputs at sizes the oracle finishes in seconds; every ctor branch."""
+    cfg = TeacherCfg(**kw)
+    sd = hash_sd_for(teacher_param_shapes(cfg))
+    b, c, h, w = shape
+    img = torch.from_numpy(hash_images(f"img{shape}", shape))
+    rate = torch.from_numpy(hash_images(f"rate{shape}", (b, 1, h, w)))
+    ref = teacher_forward(sd, img, rate, cfg)
+    m = KDLAE_teacher(**kw)
+    m.load_state_dict(sd)
+    out = _run(m.to(DEV).eval(), img, rate)
+    assert max_abs(out["hq"], ref["hq"]) <= TOL
+    if ref["sr"] is not None:
+        assert max_abs(out["sr"], ref["sr"]) <= TOL
+        assert psnr(out["sr"], ref["sr"]) >= 60.0
+
+
+def test_batch_invariance_and_determinism():
+    """Size-independent properties: image i of a batch equals the same image alone, bit-exact,
+    and two runs are bit-identical (fixed-order reductions, no float atomics)."""
+    kw = dict(dim=48, LayerNorm_type="BiasFree", num_blocks=[2, 1, 1, 1], num_refinement_blocks=1)
+    m = _model(kw)
+    img = torch.from_numpy(hash_images("binv", (3, 3, 128, 96)))
+    rate = torch.from_numpy(hash_images("binvr", (3, 1, 128, 96)))
+    full = _run(m, img, rate)
+    again = _run(m, img, rate)
+    assert torch.equal(full["hq"], again["hq"]) and torch.equal(full["sr"], again["sr"])
+    one = _run(m, img[1:2], rate[1:2])
+    assert torch.equal(full["hq"][1:2], one["hq"]) and torch.equal(full["sr"][1:2], one["sr"])
+
+
+def test_weight_reload_is_picked_up():
+    kw = dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1)
+    m = _model(kw)
+    img = torch.from_numpy(hash_images("wr", (1, 3, 16, 16)))
+    rate = torch.full((1, 1, 16, 16), 0.5)
+    a = _run(m, img, rate)["hq"]
+    with torch.no_grad():
+        m.output2.weight.mul_(2.0)
+    b = _run(m, img, rate)["hq"]
+    cfg = TeacherCfg(**kw)
+    ref = teacher_forward({k: v.cpu() for k, v in m.state_dict().items()}, img, rate, cfg)
+    assert not torch.equal(a, b)
+    assert max_abs(b, ref["hq"]) <= TOL
+
+
+def test_error_behaviour():
+    m = _model(dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1))
+    with pytest.raises(RuntimeError):
+        m({"img": torch.zeros(1, 3, 20, 24, device=DEV), "denoise_rate": torch.zeros(1, 1, 20, 24, device=DEV)})
+    with pytest.raises(RuntimeError):
+        m({"img": torch.zeros(1, 3, 16, 16), "denoise_rate": torch.zeros(1, 1, 16, 16)})
+    with pytest.raises(KeyError):
+        m({"img": torch.zeros(1, 3, 16, 16, device=DEV)})
+    with pytest.raises(NotImplementedError):
+        KDLAE_teacher(dim=16, dual_pixel_task=True).to(DEV)(
+            {"img": torch.zeros(1, 3, 16, 16, device=DEV), "denoise_rate": torch.zeros(1, 1, 16, 16, device=DEV)})
