@@ -1,0 +1,184 @@
+"""KDLAE-T forward throughput on MI355X (BASELINE.json configs[1] / configs[4]).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = one KDLAE-T forward (static="train": hq + sr, params="cat", BiasFree LN, fp32) of
+16 synthetic 512x512 images per GPU (weak scaling: global batch 16*N, images sharded by rank,
+no data-path collective).  Weights are the deterministic hash recipe (random init of the real
+architecture), inputs are hash-uniform images with per-image constant denoise_rate.
+
+Printed JSON (rank 0): value = images/s over all ranks (max-over-ranks wall time of exactly K
+steps between barriers + device syncs); roofline of the dominant kernel class measured live with
+HIP events around each of its launches inside the timed steps; cpu_baseline = the CPU oracle
+(oracle/kdlae_oracle.py, test infrastructure) on one image of the same workload, whose output also
+gives the PSNR / max-abs of the GPU result (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from rethink_acoustic_image_enhancement_amd import _lib  # noqa: E402
+from rethink_acoustic_image_enhancement_amd.hashweights import hash_images, hash_uniform, load_hash_weights  # noqa: E402
+from rethink_acoustic_image_enhancement_amd.KDLAE_model import KDLAE_teacher  # noqa: E402
+
+METRIC = "images/sec KDLAE-T 1×512×512 fp32 at 1/2/4/8 MI355X; PSNR vs ref"
+KW = dict(inp_channels=3, out_channels=3, dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4,
+          heads=[1, 2, 4, 8], ffn_expansion_factor=2.66, bias=False, LayerNorm_type="BiasFree",
+          dual_pixel_task=False, static="train", params="cat")
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (vector = MFMA f32), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0      # HBM3E spec
+PROBE_CLASSES = {1: "conv_gemm (MFMA f32 1x1 / implicit-GEMM 3x3)", 2: "dwconv_gram (MDTA pass 1)",
+                 3: "dwconv_gate (GDFN)"}
+
+
+def make_inputs(first: int, n: int, H: int, W: int):
+    imgs = np.stack([hash_images(f"img16:{first + i}", (3, H, W)) for i in range(n)])
+    rates = (hash_uniform("rate16", first + n)[first:] + 1.0) * 0.5
+    rate = np.broadcast_to(rates.astype(np.float32)[:, None, None, None], (n, 1, H, W)).copy()
+    return torch.from_numpy(imgs), torch.from_numpy(rate)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--probe", type=int, default=1, help="kernel class for the roofline (0 = off)")
+    ap.add_argument("--probe-level", type=int, default=0, help="channel filter for the probe (0 = all)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    H = W = args.size
+    B = args.batch
+
+    model = KDLAE_teacher(**KW)
+    load_hash_weights(model)
+    model = model.to(dev).eval()
+    img, rate = make_inputs(rank * B, B, H, W)
+    batch = {"img": img.to(dev), "denoise_rate": rate.to(dev)}
+
+    def step():
+        with torch.no_grad():
+            return model(batch)
+
+    eng = model.engine(dev)
+    L = _lib.lib()
+    if args.probe:
+        L.kdlae_t_probe_arm(eng.handle, args.probe, args.probe_level)  # creates the event pool in warmup
+    out = None
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize(dev)
+    if args.probe:
+        L.kdlae_t_probe_arm(eng.handle, args.probe, args.probe_level)
+
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    roof = None
+    if args.probe:
+        import ctypes
+        ms, n, by, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        L.kdlae_t_probe_read(eng.handle, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(by), ctypes.byref(fl))
+        L.kdlae_t_probe_arm(eng.handle, 0, 0)
+        if n.value:
+            sec = ms.value / 1e3
+            if args.probe == 1:
+                ach = fl.value / sec / 1e12
+                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None}
+            else:
+                ach = by.value / sec / 1e9
+                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
+            roof.update({"kernel": PROBE_CLASSES[args.probe], "launches": int(n.value),
+                         "avg_launch_us": round(ms.value * 1e3 / n.value, 2),
+                         "share_of_step": round(ms.value / 1e3 / elapsed, 4),
+                         "algorithmic_bytes_per_launch": by.value / n.value,
+                         "algorithmic_flops_per_launch": fl.value / n.value})
+
+    imgs_total = world * B * args.steps
+    res = {
+        "metric": METRIC, "value": round(imgs_total / elapsed, 3), "unit": "images/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (hash-uniform images, hash weights of the real architecture)",
+        "config": {"workload": f"KDLAE-T forward bs={B}/GPU {H}x{W} fp32 (static=train, params=cat, BiasFree)",
+                   "global_batch": world * B, "per_gpu_batch": B, "H": H, "W": W,
+                   "parallelism": f"dp{world} (batch-sharded, no data-path collective)"},
+        "roofline": roof,
+    }
+    # algorithmic per-image figures of SURVEY.md §8d (KDLAE-T 512^2 static=train)
+    if H == 512 and W == 512:
+        ips = imgs_total / elapsed / world
+        res["per_gpu"] = {"images_per_s": round(ips, 3),
+                          "hbm_roof_frac_survey_def": round(ips * 150.70e9 / 8.0e12, 4),
+                          "fp32_compute_frac": round(ips * 1.9177e12 / 157.3e12, 4)}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"], res["parity"] = cpu_baseline(model, batch, out, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(model, batch, out, threads):
+    """Oracle (torch CPU restatement, test infrastructure) on image 0 of the workload."""
+    from oracle.kdlae_oracle import TeacherCfg, psnr, teacher_forward
+
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    img = batch["img"][:1].cpu()
+    rate = batch["denoise_rate"][:1].cpu()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        ref = teacher_forward(sd, img, rate, TeacherCfg(**KW))
+    dt = time.perf_counter() - t0
+    hq, sr = out["hq"][:1].cpu(), out["sr"][:1].cpu()
+    parity = {"vs": "CPU oracle, image 0", "hq_max_abs": float((hq - ref["hq"]).abs().max()),
+              "sr_max_abs": float((sr - ref["sr"]).abs().max()),
+              "hq_psnr_db": round(psnr(hq, ref["hq"]), 2), "sr_psnr_db": round(psnr(sr, ref["sr"]), 2)}
+    base = {"value": round(1.0 / dt, 5), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"1 image 1x3x{img.shape[-2]}x{img.shape[-1]} (image 0 of the bench batch), "
+                      f"torch-CPU oracle, {threads} threads, {dt:.1f} s"}
+    return base, parity
+
+
+if __name__ == "__main__":
+    main()

@@ -199,16 +199,15 @@ static int validate(const kdlae_t_config& c) {
     if (C % heads) return false;
     const int ch = C / heads;
     if (ch % 16) return false;
-    const int ct = ch / 16;
-    return ct == 1 || ct == 2 || ct == 3 || ct == 4 || ct == 6;
+    return ch / 16 >= 1 && ch / 16 <= 8;
   };
   const int d = c.dim;
   const int levels[4] = {d, 2 * d, 4 * d, 8 * d};
   for (int i = 0; i < 4; ++i)
     if (!head_ok(levels[i], c.heads[i]))
-      return fail(KDLAE_EINVAL_CONFIG, "channels per head must be 16*{1,2,3,4,6} at every level");
+      return fail(KDLAE_EINVAL_CONFIG, "channels per head must be a multiple of 16 in [16, 128] at every level");
   if (!head_ok(2 * d, c.heads[0]))
-    return fail(KDLAE_EINVAL_CONFIG, "channels per head of decoder_level1/refinement must be 16*{1,2,3,4,6}");
+    return fail(KDLAE_EINVAL_CONFIG, "channels per head of decoder_level1/refinement must be a multiple of 16 in [16, 128]");
   if (c.ffn_expansion_factor <= 0) return fail(KDLAE_EINVAL_CONFIG, "bad ffn_expansion_factor");
   return KDLAE_OK;
 }

@@ -198,7 +198,10 @@ hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s) {
     case 2: hipLaunchKernelGGL(dwconv_gram_kernel<2>, grid, dim3(256), 0, s, p); break;
     case 3: hipLaunchKernelGGL(dwconv_gram_kernel<3>, grid, dim3(256), 0, s, p); break;
     case 4: hipLaunchKernelGGL(dwconv_gram_kernel<4>, grid, dim3(256), 0, s, p); break;
+    case 5: hipLaunchKernelGGL(dwconv_gram_kernel<5>, grid, dim3(256), 0, s, p); break;
     case 6: hipLaunchKernelGGL(dwconv_gram_kernel<6>, grid, dim3(256), 0, s, p); break;
+    case 7: hipLaunchKernelGGL(dwconv_gram_kernel<7>, grid, dim3(256), 0, s, p); break;
+    case 8: hipLaunchKernelGGL(dwconv_gram_kernel<8>, grid, dim3(256), 0, s, p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

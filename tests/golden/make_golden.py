@@ -101,29 +101,42 @@ def mdd_input():
     return crop
 
 
-def teacher_512(KM, out):
-    crop = mdd_input()
-    t = torch.from_numpy(crop.astype(np.float32) / 255.0).permute(2, 0, 1).unsqueeze(0)
-    t = torch.nn.functional.pad(t, (0, 74, 0, 0), mode="reflect")
-    kw = dict(dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4, heads=[1, 2, 4, 8],
-              LayerNorm_type="BiasFree", bias=False, static="train", params="cat")
-    m = _load_hash(KM.KDLAE_teacher(**kw))
-    rate = torch.full((1, 1, 512, 512), 0.6)
+def _run512(KM, img, kw, dtype):
+    m = _load_hash(KM.KDLAE_teacher(**kw)).to(dtype)
+    rate = torch.full((1, 1, 512, 512), 0.6, dtype=dtype)
     t0 = time.time()
     with torch.no_grad():
-        o = m({"img": t, "denoise_rate": rate})
-    dt = time.time() - t0
-    hq, sr = o["hq"], o["sr"]
-    np.savez_compressed(
-        os.path.join(out, "t_mdd_512.npz"),
-        crop_u8=crop[..., 0] if (crop[..., 0] == crop[..., 1]).all() and
-        (crop[..., 0] == crop[..., 2]).all() else crop,
-        hq_sub=hq[:, :, ::8, ::8].numpy(), sr_sub=sr[:, :, ::8, ::8].numpy(),
-        hq_chsum=hq.double().sum(dim=(2, 3)).numpy(), sr_chsum=sr.double().sum(dim=(2, 3)).numpy(),
-        hq_row257=hq[:, :, 257, :].numpy(), sr_row515=sr[:, :, 515, :].numpy(),
-        ref_cpu_seconds=np.array([dt]), threads=np.array([torch.get_num_threads()]),
-        cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8))
-    print("t_mdd_512", f"{dt:.1f}s")
+        o = m({"img": img.to(dtype), "denoise_rate": rate})
+    return o["hq"], o["sr"], time.time() - t0
+
+
+def teacher_512(KM, out):
+    """512x512 KDLAE-T goldens: config-1 MDD input and a hash-uniform image, each from the
+    reference in fp32 (the comparison target) AND in fp64 (the conditioning reference: on the MDD
+    sonar image the reference's own fp32 result is ~3e-3 away from fp64)."""
+    kw = dict(dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4, heads=[1, 2, 4, 8],
+              LayerNorm_type="BiasFree", bias=False, static="train", params="cat")
+    crop = mdd_input()
+    mdd = torch.from_numpy(crop.astype(np.float32) / 255.0).permute(2, 0, 1).unsqueeze(0)
+    mdd = torch.nn.functional.pad(mdd, (0, 74, 0, 0), mode="reflect")
+    rnd = torch.from_numpy(hash_images("img:t_rand_512", (1, 3, 512, 512)))
+    for name, img, extra in (("t_mdd_512", mdd, dict(crop_u8=crop[..., 0] if (crop[..., 0] == crop[..., 1]).all()
+                                                     and (crop[..., 0] == crop[..., 2]).all() else crop)),
+                             ("t_rand_512", rnd, dict())):
+        hq, sr, dt = _run512(KM, img, kw, torch.float32)
+        hq64, sr64, dt64 = _run512(KM, img, kw, torch.float64)
+        np.savez_compressed(
+            os.path.join(out, f"{name}.npz"), **extra,
+            hq_sub=hq[:, :, ::8, ::8].numpy(), sr_sub=sr[:, :, ::8, ::8].numpy(),
+            hq64_sub=hq64[:, :, ::8, ::8].numpy(), sr64_sub=sr64[:, :, ::8, ::8].numpy(),
+            hq_chsum=hq.double().sum(dim=(2, 3)).numpy(), sr_chsum=sr.double().sum(dim=(2, 3)).numpy(),
+            hq64_chsum=hq64.sum(dim=(2, 3)).numpy(), sr64_chsum=sr64.sum(dim=(2, 3)).numpy(),
+            hq_row257=hq[:, :, 257, :].numpy(), sr_row515=sr[:, :, 515, :].numpy(),
+            hq64_row257=hq64[:, :, 257, :].numpy(), sr64_row515=sr64[:, :, 515, :].numpy(),
+            ref_cpu_seconds=np.array([dt]), threads=np.array([torch.get_num_threads()]),
+            cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8))
+        e = float((hq[:, :, ::8, ::8].double() - hq64[:, :, ::8, ::8]).abs().max())
+        print(name, f"fp32 {dt:.1f}s fp64 {dt64:.1f}s  ref fp32-vs-fp64 hq_sub max-abs {e:.3e}")
 
 
 STUDENT_CASES = {
