@@ -28,7 +28,11 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int NT, int KG, bool CONV3>
+// OUT: 0 = plain NHWC store (N % 16 == 0), 1 = PixelUnshuffle(2) store, 2 = PixelShuffle(2) store.
+// Operand roles: the MFMA's A operand is the packed weight tile (rows = output channels) and its
+// B operand is the pixel tile, so the accumulator holds D^T: lane (li, lq) owns pixel li and the 4
+// consecutive output channels 4*lq .. 4*lq+3 -> one 16-byte store (and residual load) per tile.
+template <int NT, int KG, bool CONV3, int OUT>
 __global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];  // [NT][KG][64]
   const int tid = threadIdx.x;
@@ -142,69 +146,59 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p
         }
       }
 
-      // ---- MFMA over the chunk: one LDS b128 read of B feeds kGemmRT x 4 MFMAs.
+      // ---- MFMA over the chunk.  Per k-group: NT LDS b128 reads, then the 4 k-steps with the
+      // NT x RT independent accumulators innermost (hides the 40-cycle dependent latency).
       // Tiles / groups past the end were zero-filled in LDS and A, so no per-tile branches.
 #pragma unroll
       for (int g = 0; g < KG; ++g) {
+        f32x4 bw[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const f32x4 bw = wlds[(t * KG + g) * 64 + lane];
+        for (int t = 0; t < NT; ++t) bw[t] = wlds[(t * KG + g) * 64 + lane];
 #pragma unroll
-          for (int r = 0; r < kGemmRT; ++r) {
-            acc[t][r] = mfma4(a[r][g].x, bw.x, acc[t][r]);
-            acc[t][r] = mfma4(a[r][g].y, bw.y, acc[t][r]);
-            acc[t][r] = mfma4(a[r][g].z, bw.z, acc[t][r]);
-            acc[t][r] = mfma4(a[r][g].w, bw.w, acc[t][r]);
-          }
-        }
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < kGemmRT; ++r) acc[t][r] = mfma4(bw[t][s], a[r][g][s], acc[t][r]);
       }
     }
 
-    // ---- epilogue: D[row = 4*lq + e][col = li] of each 16x16 tile
-    float* __restrict__ Ob = p.out;
+    // ---- epilogue: lane (li, lq) holds pixel (row0 + 16 r + li), channels n0 + 4 lq + e
     const float* __restrict__ Rb = p.R ? p.R + (long long)b * HW * p.ldr : nullptr;
-    if (p.out_mode == 0) Ob += (long long)b * HW * p.ldo;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n0 = (nc * NT + t) * 16;
       if (n0 >= p.N) continue;
-      const int n = n0 + li;
-      const bool nv = n < p.N;
-      const float bn = (p.bias && nv) ? p.bias[n] : 0.f;
+      const int nq = n0 + 4 * lq;
+      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + nq) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < kGemmRT; ++r) {
-        const int pl0 = row0 + r * 16 + 4 * lq;
-        float res[4] = {0.f, 0.f, 0.f, 0.f};
-        if (Rb) {
+        const int pl = row0 + r * 16 + li;
+        if (pl >= HW) continue;
+        f32x4 v = acc[t][r] + bias;
+        if (OUT == 0) {
+          if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + pl * p.ldr + nq);
+          if (p.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+          *reinterpret_cast<f32x4*>(p.out + (long long)b * HW * p.ldo + pl * p.ldo + nq) = v;
+        } else {
+          const int y = pl / p.W, x = pl - y * p.W;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const bool ok = nv && pl0 + e < HW;
-            const float rv = Rb[ok ? (pl0 + e) * p.ldr + n : 0];
-            res[e] = ok ? rv : 0.f;
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int pl = pl0 + e;
-          if (pl < HW && nv) {
-            float v = acc[t][r][e] + bn + res[e];
-            if (p.relu) v = fmaxf(v, 0.f);
-            if (p.out_mode == 0) {
-              Ob[pl * p.ldo + n] = v;
+            const int n = nq + e;
+            if (n >= p.N) continue;
+            float val = v[e];
+            if (p.relu) val = fmaxf(val, 0.f);
+            long long dst;
+            int ch;
+            if (OUT == 1) {
+              const int Wo = p.W >> 1, Ho = p.H >> 1;
+              dst = (long long)b * Ho * Wo + (y >> 1) * Wo + (x >> 1);
+              ch = n * 4 + (y & 1) * 2 + (x & 1);
             } else {
-              const int y = pl / p.W, x = pl - y * p.W;
-              long long dst;
-              int ch;
-              if (p.out_mode == 1) {
-                const int Wo = p.W >> 1, Ho = p.H >> 1;
-                dst = (long long)b * Ho * Wo + (y >> 1) * Wo + (x >> 1);
-                ch = n * 4 + (y & 1) * 2 + (x & 1);
-              } else {
-                dst = (long long)b * 4 * HW + (2 * y + ((n >> 1) & 1)) * (2 * p.W) + 2 * x + (n & 1);
-                ch = n >> 2;
-              }
-              Ob[dst * p.ldo + ch] = v;
+              dst = (long long)b * 4 * HW + (2 * y + ((n >> 1) & 1)) * (2 * p.W) + 2 * x + (n & 1);
+              ch = n >> 2;
             }
+            p.out[dst * p.ldo + ch] = val;
           }
         }
       }
@@ -213,39 +207,42 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p
 }
 
 #define KDLAE_GEMM_VARIANTS(X) \
-  X(3, 3, false) X(6, 3, false) X(9, 3, false) X(12, 3, false) \
-  X(3, 6, false) X(6, 6, false) X(9, 6, false) X(12, 6, false) \
-  X(3, 8, false) X(6, 8, false) X(9, 8, false) \
-  X(3, 12, false) X(6, 12, false) \
-  X(3, 16, false) X(6, 16, false) \
-  X(3, 3, true) X(3, 6, true) X(6, 6, true) X(12, 6, true) X(6, 12, true) X(12, 3, true)
+  X(3, 3, false, 0) X(6, 3, false, 0) X(9, 3, false, 0) X(12, 3, false, 0) \
+  X(3, 6, false, 0) X(6, 6, false, 0) X(9, 6, false, 0) X(12, 6, false, 0) \
+  X(3, 8, false, 0) X(6, 8, false, 0) X(9, 8, false, 0) \
+  X(3, 12, false, 0) X(6, 12, false, 0) \
+  X(3, 16, false, 0) X(6, 16, false, 0) \
+  X(3, 3, true, 1) X(3, 6, true, 1) X(6, 6, true, 1) X(6, 12, true, 1) X(12, 3, true, 1) X(12, 6, true, 1) \
+  X(3, 3, true, 2) X(3, 6, true, 2) X(6, 6, true, 2) X(6, 12, true, 2) X(12, 3, true, 2) X(12, 6, true, 2)
 
 bool gemm_has_variant(int NT, int KG, bool conv3) {
-#define X(a, b, c) if (NT == a && KG == b && conv3 == c) return true;
+#define X(a, b, c, o) if (NT == a && KG == b && conv3 == c) return true;
   KDLAE_GEMM_VARIANTS(X)
 #undef X
   return false;
 }
 
-template <int NT, int KG, bool C3>
+template <int NT, int KG, bool C3, int OUT>
 static hipError_t launch_variant(const GemmParams& p, int grid_x, hipStream_t s) {
   const size_t lds = (size_t)NT * KG * 64 * sizeof(f32x4);
   static bool attr_done = false;
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<NT, KG, C3>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<NT, KG, C3, OUT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_done = true;
   }
   const int nchunks = (p.ntiles + NT - 1) / NT;
   dim3 grid(grid_x, nchunks);
-  hipLaunchKernelGGL((conv_gemm_kernel<NT, KG, C3>), grid, dim3(kGemmThreads), lds, s, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<NT, KG, C3, OUT>), grid, dim3(kGemmThreads), lds, s, p);
   return hipGetLastError();
 }
 
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int grid_x, hipStream_t s) {
   const bool c3 = p.ksize == 3;
-#define X(a, b, c) if (NT == a && KG == b && c3 == c) return launch_variant<a, b, c>(p, grid_x, s);
+  if (p.out_mode == 0 && (p.N % 16)) return hipErrorInvalidValue;  // plain stores are whole 16-channel tiles
+#define X(a, b, c, o) \
+  if (NT == a && KG == b && c3 == c && p.out_mode == o) return launch_variant<a, b, c, o>(p, grid_x, s);
   KDLAE_GEMM_VARIANTS(X)
 #undef X
   return hipErrorInvalidValue;

@@ -403,8 +403,16 @@ struct Plan {
   }
 };
 
-static int nslots_for(int HW) {
-  const int steps = (HW + 63) / 64;
+// Partial Gram slots per (image, head).  Row-sweep kernel (W % 16 == 0): strips x row segments,
+// sized for ~2048 workgroups per launch; generic kernel: 64-pixel steps grouped 16 per slot.
+static int nslots_for(int H, int W, int B, int heads) {
+  if (W % 16 == 0) {
+    const int strips = W / 16;
+    long long nseg = (2048 + (long long)strips * B * heads - 1) / ((long long)strips * B * heads);
+    nseg = std::max<long long>(1, std::min<long long>(nseg, (H + 7) / 8));
+    return (int)(strips * nseg);
+  }
+  const int steps = (H * W + 63) / 64;
   int n = (steps + 15) / 16;
   return std::max(1, std::min(64, n));
 }
@@ -426,7 +434,7 @@ static Plan make_plan(const kdlae_t_handle* h, int B, int H, int W) {
   pl.srs = c.static_train ? pl.take(Psr * d) : 0;
   // per-block scratch: max over every stage that runs
   long long mq = 0, mv = 0, mfp = 0, mfg = 0, mst = 0, mpart = 0, mred = 0, mM = 0;
-  auto acc = [&](const std::vector<BlockW>& st, long long P, int HW) {
+  auto acc = [&](const std::vector<BlockW>& st, long long P, int Hh, int Ww) {
     for (const BlockW& b : st) {
       const int CT = b.Ch / 16;
       const long long slot = (long long)CT * CT * 256 + 2 * b.Ch;
@@ -435,22 +443,21 @@ static Plan make_plan(const kdlae_t_handle* h, int B, int H, int W) {
       mfp = std::max(mfp, P * 2 * b.hidS);
       mfg = std::max(mfg, P * b.hidS);
       mst = std::max(mst, P * 2);
-      mpart = std::max(mpart, (long long)B * b.heads * nslots_for(HW) * slot);
+      mpart = std::max(mpart, (long long)B * b.heads * nslots_for(Hh, Ww, B, b.heads) * slot);
       mred = std::max(mred, (long long)B * b.heads * slot);
       mM = std::max(mM, (long long)B * b.C * b.C);
     }
   };
-  const int HW1 = H * W;
-  acc(h->enc1, P1, HW1);
-  acc(h->enc2, P2, HW1 / 4);
-  acc(h->enc3, P3, HW1 / 16);
-  acc(h->latent, P4, HW1 / 64);
-  acc(h->dec3, P3, HW1 / 16);
-  acc(h->dec2, P2, HW1 / 4);
-  acc(h->dec1, P1, HW1);
-  acc(h->refinement, P1, HW1);
-  acc(h->refinement_out, P1, HW1);
-  acc(h->enhance, Psr, HW1 * 4);
+  acc(h->enc1, P1, H, W);
+  acc(h->enc2, P2, H / 2, W / 2);
+  acc(h->enc3, P3, H / 4, W / 4);
+  acc(h->latent, P4, H / 8, W / 8);
+  acc(h->dec3, P3, H / 4, W / 4);
+  acc(h->dec2, P2, H / 2, W / 2);
+  acc(h->dec1, P1, H, W);
+  acc(h->refinement, P1, H, W);
+  acc(h->refinement_out, P1, H, W);
+  acc(h->enhance, Psr, 2 * H, 2 * W);
   pl.qkv = pl.take(mq);
   pl.vbuf = pl.take(mv);
   pl.fpre = pl.take(mfp);
@@ -571,7 +578,7 @@ struct Fwd {
     gp.Bn = B;
     gp.H = Hh;
     gp.W = Ww;
-    gp.nslots = nslots_for(HW);
+    gp.nslots = nslots_for(Hh, Ww, B, b.heads);
     const int CT = b.Ch / 16;
     gp.slot_floats = CT * CT * 256 + 2 * b.Ch;
     if ((rc = probe_begin(2, b.C))) return rc;

@@ -191,17 +191,156 @@ __syncthreads();
   }
 }
 
+// Row-sweep variant (W % 16 == 0): block = (16-column strip, row segment) of one head.
+//  * the 3*CT (part, channel-tile) stencil jobs are dealt to the 4 waves; lane (i, q) of a job
+//    computes channel 16 ct + i at pixels x0 + 4q + s (s = 0..3) and keeps a rolling 3-row x
+//    6-column window, so a new row costs 6 scalar loads per 4 outputs;
+//  * per row, q and k go to LDS [16 px][S], v to HBM; then the CT x CT Gram tiles (dealt to the
+//    waves) take 4 MFMA k-steps over the row's 16 pixels.  One slot per block.
+template <int CT>
+__global__ __launch_bounds__(256) void dwconv_gram_sweep_kernel(GramParams p, int nseg, int seg_rows) {
+  constexpr int Ch = CT * 16;
+  constexpr int S = (Ch % 32 == 16) ? Ch : Ch + 16;
+  constexpr int NJ = 3 * CT;               // stencil jobs
+  constexpr int JPW = (NJ + 3) / 4;        // jobs per wave
+  constexpr int PPW = (CT * CT + 3) / 4;   // Gram tile pairs per wave
+  __shared__ float qs[2][16 * S];
+  __shared__ float ks[2][16 * S];
+  __shared__ float nred[2 * Ch];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int strips = p.W >> 4;
+  const int slot = blockIdx.x;
+  const int strip = slot % strips, seg = slot / strips;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int HW = p.H * p.W;
+  const int C = p.C;
+  const float* __restrict__ X = p.qkv + (long long)b * HW * p.ld;
+  float* __restrict__ V = p.v_out + (long long)b * HW * p.ldv;
+  const int x0 = strip * 16 + 4 * lq;      // this lane's first pixel column
+  const int y0 = seg * seg_rows, y1 = min(y0 + seg_rows, p.H);
+
+  int chan[JPW], part[JPW];
+  float w[JPW][9], bias[JPW], win[JPW][3][6], n2[JPW];
+#pragma unroll
+  for (int j = 0; j < JPW; ++j) {
+    const int jb = wave + 4 * j;
+    const int job = jb < NJ ? jb : 0;
+    part[j] = job / CT;
+    const int ct = job - part[j] * CT;
+    chan[j] = part[j] * C + h * Ch + ct * 16 + li;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) w[j][t] = p.wdw[t * 3 * C + chan[j]];
+    bias[j] = p.bdw ? p.bdw[chan[j]] : 0.f;
+    n2[j] = 0.f;
+  }
+  auto load_row = [&](int yy, int slotr) {
+    const bool oky = (unsigned)yy < (unsigned)p.H;
+#pragma unroll
+    for (int c6 = 0; c6 < 6; ++c6) {
+      const int xx = x0 - 1 + c6;
+      const bool ok = oky && (unsigned)xx < (unsigned)p.W;
+      const int off = ok ? (yy * p.W + xx) * p.ld : 0;
+#pragma unroll
+      for (int j = 0; j < JPW; ++j) {
+        const float v = X[off + chan[j]];
+        win[j][slotr][c6] = ok ? v : 0.f;
+      }
+    }
+  };
+  f32x4 acc[PPW];
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_row(y0 - 1, 0);
+  load_row(y0, 1);
+  int buf = 0;
+  for (int y = y0; y < y1; ++y) {
+    load_row(y + 1, 2);
+#pragma unroll
+    for (int j = 0; j < JPW; ++j) {
+      if (wave + 4 * j < NJ) {
+        const int ct = (wave + 4 * j) % CT;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float a = bias[j];
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) a = fmaf(win[j][r][s + dx], w[j][3 * r + dx], a);
+          const int lp = 4 * lq + s;
+          if (part[j] == 0) {
+            qs[buf][lp * S + ct * 16 + li] = a;
+            n2[j] = fmaf(a, a, n2[j]);
+          } else if (part[j] == 1) {
+            ks[buf][lp * S + ct * 16 + li] = a;
+            n2[j] = fmaf(a, a, n2[j]);
+          } else {
+            V[(y * p.W + x0 + s) * p.ldv + h * Ch + ct * 16 + li] = a;
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c6 = 0; c6 < 6; ++c6) win[j][r][c6] = win[j][r + 1][c6];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) {
+      const int pi = wave * PPW + k;
+      if (pi < CT * CT) {
+        const int i = pi / CT, jj = pi - (pi / CT) * CT;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int lp = 4 * lq + s;
+          acc[k] = mfma4(qs[buf][lp * S + 16 * i + li], ks[buf][lp * S + 16 * jj + li], acc[k]);
+        }
+      }
+    }
+    buf ^= 1;  // double-buffered staging: the next row's writes go to the other buffer
+  }
+
+  float* out = p.partial + (((long long)b * p.heads + h) * p.nslots + slot) * p.slot_floats;
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) {
+    const int pi = wave * PPW + k;
+    if (pi < CT * CT) *reinterpret_cast<f32x4*>(out + (pi * 64 + lane) * 4) = acc[k];
+  }
+#pragma unroll
+  for (int j = 0; j < JPW; ++j) {
+    float t = n2[j];
+    t += __shfl_xor(t, 16);
+    t += __shfl_xor(t, 32);
+    const int jb = wave + 4 * j;
+    if (jb < NJ && part[j] < 2 && lq == 0) nred[part[j] * Ch + (jb % CT) * 16 + li] = t;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 2 * Ch; idx += 256) out[CT * CT * 256 + idx] = nred[idx];
+}
+
+template <int CT>
+static void launch_gram_ct(const GramParams& p, hipStream_t s) {
+  if (p.W % 16 == 0 && p.nslots % (p.W / 16) == 0) {
+    const int nseg = p.nslots / (p.W / 16);
+    const int seg_rows = (p.H + nseg - 1) / nseg;
+    hipLaunchKernelGGL(dwconv_gram_sweep_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(256), 0, s, p, nseg,
+                       seg_rows);
+  } else {
+    hipLaunchKernelGGL(dwconv_gram_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(256), 0, s, p);
+  }
+}
+
 hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s) {
-  dim3 grid(p.nslots, p.heads, p.Bn);
   switch (p.Ch / 16) {
-    case 1: hipLaunchKernelGGL(dwconv_gram_kernel<1>, grid, dim3(256), 0, s, p); break;
-    case 2: hipLaunchKernelGGL(dwconv_gram_kernel<2>, grid, dim3(256), 0, s, p); break;
-    case 3: hipLaunchKernelGGL(dwconv_gram_kernel<3>, grid, dim3(256), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(dwconv_gram_kernel<4>, grid, dim3(256), 0, s, p); break;
-    case 5: hipLaunchKernelGGL(dwconv_gram_kernel<5>, grid, dim3(256), 0, s, p); break;
-    case 6: hipLaunchKernelGGL(dwconv_gram_kernel<6>, grid, dim3(256), 0, s, p); break;
-    case 7: hipLaunchKernelGGL(dwconv_gram_kernel<7>, grid, dim3(256), 0, s, p); break;
-    case 8: hipLaunchKernelGGL(dwconv_gram_kernel<8>, grid, dim3(256), 0, s, p); break;
+    case 1: launch_gram_ct<1>(p, s); break;
+    case 2: launch_gram_ct<2>(p, s); break;
+    case 3: launch_gram_ct<3>(p, s); break;
+    case 4: launch_gram_ct<4>(p, s); break;
+    case 5: launch_gram_ct<5>(p, s); break;
+    case 6: launch_gram_ct<6>(p, s); break;
+    case 7: launch_gram_ct<7>(p, s); break;
+    case 8: launch_gram_ct<8>(p, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -301,48 +440,93 @@ hipError_t launch_attn_fold(const float* reduced, int slot_floats, const float* 
 // out[p][c] = gelu_erf(dw(x1)[p][c]) * dw(x2)[p][c], c < hidS; float4 of channels per thread.
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
+// Vertical sweep: thread = (channel quad c of x1 and the same quad of x2, one column x) walking a
+// segment of rows.  The 3x3 weights of its 8 channels sit in registers for the whole sweep and a
+// rolling 3-row x 3-column window of float4s means each new output row costs 6 float4 loads
+// (3 columns x {x1, x2}); the column neighbours are the adjacent lanes' loads (L1 hits), so HBM
+// sees each input element ~once.  Lanes run along channels -> coalesced 16 B per lane.
+constexpr int kGateRows = 32;
+
 __global__ __launch_bounds__(256) void dwconv_gate_kernel(GateParams p) {
+  const int c4n = p.hidS >> 2;                     // channel quads per half
+  const int cols_per_block = 256 / c4n > 0 ? 256 / c4n : 1;
+  const int tid = threadIdx.x;
+  // block -> (image, row segment, column group, channel-quad group)
+  const int cq_groups = (c4n + 255) / 256;         // >1 only when hidS > 1024
+  const int col_groups = (p.W + cols_per_block - 1) / cols_per_block;
+  const int segs = (p.H + kGateRows - 1) / kGateRows;
+  int bid = blockIdx.x;
+  const int cqg = bid % cq_groups; bid /= cq_groups;
+  const int colg = bid % col_groups; bid /= col_groups;
+  const int seg = bid % segs; bid /= segs;
+  const int b = bid;
+  const int c4 = cqg * 256 + (c4n >= 256 ? tid : tid % c4n);
+  const int x = colg * cols_per_block + (c4n >= 256 ? 0 : tid / c4n);
+  if (b >= p.Bn || c4 >= c4n || x >= p.W) return;
+  if (c4n < 256 && tid >= cols_per_block * c4n) return;
+  const int c = 4 * c4;
   const int HW = p.H * p.W;
-  const int c4n = p.hidS >> 2;
-  const long long total = (long long)p.Bn * HW * c4n;
+  const float* __restrict__ X = p.x + (long long)b * HW * p.ld;
+  float* __restrict__ O = p.out + (long long)b * HW * p.ldo;
   const int two = 2 * p.hidS;
-  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-    const long long pix = idx / c4n;
-    const int c = (int)(idx - pix * c4n) * 4;
-    const int b = (int)(pix / HW);
-    const int pl = (int)(pix - (long long)b * HW);
-    const int y = pl / p.W, x = pl - (pl / p.W) * p.W;
-    const float* X = p.x + (long long)b * HW * p.ld;
-    f32x4 a1 = p.b ? *reinterpret_cast<const f32x4*>(p.b + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 a2 = p.b ? *reinterpret_cast<const f32x4*>(p.b + p.hidS + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 w1[9], w2[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-      const bool ok = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-      const int off = ok ? (yy * p.W + xx) * p.ld + c : c;
-      f32x4 v1 = *reinterpret_cast<const f32x4*>(X + off);
-      f32x4 v2 = *reinterpret_cast<const f32x4*>(X + off + p.hidS);
-      const f32x4 w1 = *reinterpret_cast<const f32x4*>(p.w + t * two + c);
-      const f32x4 w2 = *reinterpret_cast<const f32x4*>(p.w + t * two + p.hidS + c);
-      const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-      v1 = ok ? v1 : z;
-      v2 = ok ? v2 : z;
-      a1 = v1 * w1 + a1;
-      a2 = v2 * w2 + a2;
+  for (int t = 0; t < 9; ++t) {
+    w1[t] = *reinterpret_cast<const f32x4*>(p.w + t * two + c);
+    w2[t] = *reinterpret_cast<const f32x4*>(p.w + t * two + p.hidS + c);
+  }
+  const f32x4 b1 = p.b ? *reinterpret_cast<const f32x4*>(p.b + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 b2 = p.b ? *reinterpret_cast<const f32x4*>(p.b + p.hidS + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool okl = x > 0, okr = x + 1 < p.W;
+  // window rows: [0] = y-1, [1] = y, [2] = y+1; columns: [0] = x-1, [1] = x, [2] = x+1
+  f32x4 r1[3][3], r2[3][3];
+  auto load_row = [&](int yy, f32x4 (&d1)[3], f32x4 (&d2)[3]) {
+    const bool oky = (unsigned)yy < (unsigned)p.H;
+    const int base = (oky ? yy : 0) * p.W;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const bool ok = oky && (j == 0 ? okl : (j == 2 ? okr : true));
+      const int off = (ok ? base + x + j - 1 : 0) * p.ld + c;
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(X + off);
+      const f32x4 v2 = *reinterpret_cast<const f32x4*>(X + off + p.hidS);
+      d1[j] = ok ? v1 : z;
+      d2[j] = ok ? v2 : z;
     }
+  };
+  const int y0 = seg * kGateRows;
+  const int y1 = min(y0 + kGateRows, p.H);
+  load_row(y0 - 1, r1[0], r2[0]);
+  load_row(y0, r1[1], r2[1]);
+  for (int y = y0; y < y1; ++y) {
+    load_row(y + 1, r1[2], r2[2]);
+    f32x4 a1 = b1, a2 = b2;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        a1 = r1[i][j] * w1[3 * i + j] + a1;
+        a2 = r2[i][j] * w2[3 * i + j] + a2;
+      }
     f32x4 o;
     o.x = gelu_erf(a1.x) * a2.x;
     o.y = gelu_erf(a1.y) * a2.y;
     o.z = gelu_erf(a1.z) * a2.z;
     o.w = gelu_erf(a1.w) * a2.w;
-    *reinterpret_cast<f32x4*>(p.out + pix * p.ldo + c) = o;
+    *reinterpret_cast<f32x4*>(O + (y * p.W + x) * p.ldo + c) = o;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      r1[0][j] = r1[1][j]; r2[0][j] = r2[1][j];
+      r1[1][j] = r1[2][j]; r2[1][j] = r2[2][j];
+    }
   }
 }
 
 hipError_t launch_dwconv_gate(const GateParams& p, hipStream_t s) {
-  const long long total = (long long)p.Bn * p.H * p.W * (p.hidS / 4);
-  long long blocks = (total + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
+  const int c4n = p.hidS / 4;
+  const int cols_per_block = 256 / c4n > 0 ? 256 / c4n : 1;
+  const long long blocks = (long long)p.Bn * ((p.H + kGateRows - 1) / kGateRows) *
+                           ((p.W + cols_per_block - 1) / cols_per_block) * ((c4n + 255) / 256);
   hipLaunchKernelGGL(dwconv_gate_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);
   return hipGetLastError();
 }

@@ -20,7 +20,7 @@ TOL = 1e-3
 DEV = "cuda:0"
 
 TEACHER = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "t_*.npz"))
-                 if "mdd_512" not in f)
+                 if "_512" not in f)
 
 
 def _model(kw):

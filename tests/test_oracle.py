@@ -11,7 +11,7 @@ from oracle.kdlae_oracle import (StudentCfg, TeacherCfg, student_forward, studen
 from tests.util import GOLDEN, hash_sd_for, load_fixture, max_abs, mdd_input_tensor
 
 TEACHER = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "t_*.npz"))
-                 if "mdd_512" not in f)
+                 if "_512" not in f)
 STUDENT = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "s_*.npz")))
 
 
