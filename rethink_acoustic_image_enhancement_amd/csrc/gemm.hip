@@ -32,36 +32,239 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // Operand roles: the MFMA's A operand is the packed weight tile (rows = output channels) and its
 // B operand is the pixel tile, so the accumulator holds D^T: lane (li, lq) owns pixel li and the 4
 // consecutive output channels 4*lq .. 4*lq+3 -> one 16-byte store (and residual load) per tile.
-template <int NT, int KG, bool CONV3, int OUT>
+//
+// Two schedules, chosen by the host:
+//  * resident (group_tiles > 0, needs KG == kgroups): the block's whole weight group (grid.y selects the group of
+//    group_tiles output tiles) sits in LDS for the block's lifetime; each wave keeps its A rows
+//    (full K, LN applied) in VGPRs, walks the group's n-chunks of NT tiles, and — with PF — issues
+//    the next tile's A loads before this tile's MFMAs so HBM latency hides under matrix work.
+//  * chunked (group_tiles == 0: deep layers, implicit-GEMM 3x3, odd K): grid.y = n-chunk; the [NT][KG] weight chunk is restaged
+//    per k-chunk and A is reloaded per k-chunk (LN then comes from precomputed row stats).
+
+template <int KG, bool CONV3>
+__device__ __forceinline__ void load_a(const GemmParams& p, const float* __restrict__ Ab, int row0, int kc,
+                                       int li, int lq, int HW, f32x4 (&a)[kGemmRT][KG]) {
+#pragma unroll
+  for (int r = 0; r < kGemmRT; ++r) {
+    const int prow = row0 + r * 16 + li;
+    const bool pv = prow < HW;
+    if (!CONV3) {
+      const int off0 = prow * p.lda + 4 * lq + kc * KG * 16;
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        const bool ok = pv && (kc * KG + g) < p.kgroups;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(Ab + (ok ? off0 + g * 16 : 0));
+        a[r][g] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+      const int py = prow / p.W;
+      const int px = prow - py * p.W;
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        const int gg = kc * KG + g;
+        const int tap = gg / p.cg_per_tap;
+        const int cgi = gg - tap * p.cg_per_tap;
+        const int ty = tap / 3;
+        const int yy = py + (ty - 1) * p.dil;
+        const int xx = px + (tap - 3 * ty - 1) * p.dil;
+        const bool ok = pv && gg < p.kgroups && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+        const int off = (yy * p.W + xx) * p.lda + cgi * 16 + 4 * lq;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(Ab + (ok ? off : 0));
+        a[r][g] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+}
+
+template <int KG>
+__device__ __forceinline__ void apply_ln(const GemmParams& p, int b, int row0, int li, int HW,
+                                         f32x4 (&a)[kGemmRT][KG]) {
+  const float wb = (p.ln == 2) ? 1.f : 0.f;
+#pragma unroll
+  for (int r = 0; r < kGemmRT; ++r) {
+    float mean, rstd;
+    if (p.stats) {
+      const int prow = min(row0 + r * 16 + li, HW - 1);
+      const float2 st = *reinterpret_cast<const float2*>(p.stats + 2 * ((long long)b * HW + prow));
+      mean = st.x;
+      rstd = st.y;
+    } else {
+      // the whole LN row is in registers (host: kchunks == 1, kgroups * 16 == ln_C)
+      float s = 0.f;
+#pragma unroll
+      for (int g = 0; g < KG; ++g) s += (a[r][g].x + a[r][g].y) + (a[r][g].z + a[r][g].w);
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      mean = s / (float)p.ln_C;
+      float v2 = 0.f;
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        const f32x4 d = a[r][g] - mean;
+        const float dd = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        v2 += (g < p.kgroups) ? dd : 0.f;
+      }
+      v2 += __shfl_xor(v2, 16);
+      v2 += __shfl_xor(v2, 32);
+      rstd = 1.0f / sqrtf(v2 / (float)p.ln_C + 1e-5f);
+    }
+    const float sh = mean * wb;
+#pragma unroll
+    for (int g = 0; g < KG; ++g) a[r][g] = (a[r][g] - sh) * rstd;
+  }
+}
+
+// acc[t][r] += W-tile(t) x A(r) over KG k-groups; W tiles at wl[(t * ldk + g) * 64 + lane].
+// Pairs of tiles share a step so 4 independent accumulators interleave (MFMA latency 40 > issue 32).
+template <int NT, int KG>
+__device__ __forceinline__ void mfma_chunk(const f32x4* __restrict__ wl, int ldk, int lane,
+                                           const f32x4 (&a)[kGemmRT][KG], f32x4 (&acc)[NT][kGemmRT]) {
+#pragma unroll
+  for (int g = 0; g < KG; ++g) {
+#pragma unroll
+    for (int t = 0; t < NT; t += 2) {
+      if (t + 1 < NT) {
+        const f32x4 b0 = wl[(t * ldk + g) * 64 + lane];
+        const f32x4 b1 = wl[((t + 1) * ldk + g) * 64 + lane];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int r = 0; r < kGemmRT; ++r) {
+            acc[t][r] = mfma4(b0[s], a[r][g][s], acc[t][r]);
+            acc[t + 1][r] = mfma4(b1[s], a[r][g][s], acc[t + 1][r]);
+          }
+      } else {
+        const f32x4 b0 = wl[(t * ldk + g) * 64 + lane];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int r = 0; r < kGemmRT; ++r) acc[t][r] = mfma4(b0[s], a[r][g][s], acc[t][r]);
+      }
+    }
+  }
+}
+
+template <int NT, int OUT>
+__device__ __forceinline__ void epilogue(const GemmParams& p, int b, int row0, int nt0, int tmax, int li, int lq,
+                                         int HW, f32x4 (&acc)[NT][kGemmRT]) {
+  const float* __restrict__ Rb = p.R ? p.R + (long long)b * HW * p.ldr : nullptr;
+  float* __restrict__ Ob = p.out + (OUT == 0 ? (long long)b * HW * p.ldo : 0);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n0 = (nt0 + t) * 16;
+    if (t >= tmax || n0 >= p.N) continue;
+    const int nq = n0 + 4 * lq;
+    const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + nq) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r) {
+      const int pl = row0 + r * 16 + li;
+      if (pl >= HW) continue;
+      f32x4 v = acc[t][r] + bias;
+      if (OUT == 0) {
+        if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + pl * p.ldr + nq);
+        if (p.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+        *reinterpret_cast<f32x4*>(Ob + pl * p.ldo + nq) = v;
+      } else {
+        const int y = pl / p.W, x = pl - y * p.W;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = nq + e;
+          if (n >= p.N) continue;
+          float val = v[e];
+          if (p.relu) val = fmaxf(val, 0.f);
+          long long dst;
+          int ch;
+          if (OUT == 1) {
+            const int Wo = p.W >> 1, Ho = p.H >> 1;
+            dst = (long long)b * Ho * Wo + (y >> 1) * Wo + (x >> 1);
+            ch = n * 4 + (y & 1) * 2 + (x & 1);
+          } else {
+            dst = (long long)b * 4 * HW + (2 * y + ((n >> 1) & 1)) * (2 * p.W) + 2 * x + (n & 1);
+            ch = n >> 2;
+          }
+          Ob[dst * p.ldo + ch] = val;
+        }
+      }
+    }
+  }
+}
+
+template <int NT, int KG, bool CONV3, int OUT, bool PF>
 __global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];  // [NT][KG][64]
+  extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
-  const int nc = blockIdx.y;
   const int HW = p.H * p.W;
-  const bool resident = (p.kchunks == 1);
-  int staged = -1;
-
   const int t_begin = blockIdx.x * p.tiles_per_block;
   const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
+  if (t_begin >= t_end) return;
 
-  for (int tile = t_begin; tile < t_end; ++tile) {
-    const int b = tile / p.tiles_per_img;
-    const int tin = tile - b * p.tiles_per_img;
-    const int row0 = tin * kGemmRows + wave * (kGemmRT * 16);
-    // uniform per-image bases; per-lane offsets stay 32-bit (HW * ld < 2^31 is checked on host)
-    const float* __restrict__ Ab = p.A + (long long)b * HW * p.lda;
-
-    f32x4 acc[NT][kGemmRT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int kc = 0; kc < p.kchunks; ++kc) {
+  if (p.group_tiles > 0) {
+    // ------------------------------------------------------------------ resident schedule
+    const int g0 = blockIdx.y * p.group_tiles;                       // first output tile of the group
+    const int gtiles = min(p.group_tiles, p.ntiles - g0);
+    int staged = -1;
+    f32x4 a[kGemmRT][KG];
+    [[maybe_unused]] f32x4 an[kGemmRT][KG];
+    if (PF) {
+      const int b = t_begin / p.tiles_per_img;
+      load_a<KG, CONV3>(p, p.A + (long long)b * HW * p.lda,
+                        (t_begin - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16), 0, li, lq, HW, an);
+    }
+    for (int tile = t_begin; tile < t_end; ++tile) {
+      const int b = tile / p.tiles_per_img;
+      const int row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
       const int wkey = p.w_img_stride ? b : 0;
-      if (!resident || staged != wkey) {
+      if (staged != wkey) {
+        __syncthreads();
+        const f32x4* wbase = reinterpret_cast<const f32x4*>(p.Wp + (long long)wkey * p.w_img_stride +
+                                                            (long long)g0 * p.kgroups * 256);
+        const int n4 = gtiles * p.kgroups * 64;
+        const int n4pad = ((gtiles + NT - 1) / NT) * NT * p.kgroups * 64;  // partial last chunk reads zeros
+        for (int idx = tid; idx < n4pad; idx += kGemmThreads)
+          wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+        __syncthreads();
+        staged = wkey;
+      }
+      if (PF) {
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r)
+#pragma unroll
+          for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
+        if (tile + 1 < t_end) {
+          const int bn = (tile + 1) / p.tiles_per_img;
+          load_a<KG, CONV3>(p, p.A + (long long)bn * HW * p.lda,
+                            (tile + 1 - bn * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16), 0, li, lq,
+                            HW, an);
+        }
+      } else {
+        load_a<KG, CONV3>(p, p.A + (long long)b * HW * p.lda, row0, 0, li, lq, HW, a);
+      }
+      if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
+      for (int c0 = 0; c0 < gtiles; c0 += NT) {
+        f32x4 acc[NT][kGemmRT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mfma_chunk<NT, KG>(wlds + (size_t)c0 * p.kgroups * 64, p.kgroups, lane, a, acc);
+        epilogue<NT, OUT>(p, b, row0, g0 + c0, gtiles - c0, li, lq, HW, acc);
+      }
+    }
+  } else {
+    // ------------------------------------------------------------------ chunked schedule
+    const int nc = blockIdx.y;
+    for (int tile = t_begin; tile < t_end; ++tile) {
+      const int b = tile / p.tiles_per_img;
+      const int row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
+      const float* __restrict__ Ab = p.A + (long long)b * HW * p.lda;
+      f32x4 acc[NT][kGemmRT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kc = 0; kc < p.kchunks; ++kc) {
+        const int wkey = p.w_img_stride ? b : 0;
         __syncthreads();
         const float* wbase = p.Wp + (long long)wkey * p.w_img_stride;
         for (int idx = tid; idx < NT * KG * 64; idx += kGemmThreads) {
@@ -75,174 +278,64 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p
           wlds[idx] = v;
         }
         __syncthreads();
-        staged = wkey;
+        f32x4 a[kGemmRT][KG];
+        load_a<KG, CONV3>(p, Ab, row0, kc, li, lq, HW, a);
+        if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
+        mfma_chunk<NT, KG>(wlds, KG, lane, a, acc);
       }
-
-      // ---- A rows for this k-chunk: unconditional loads from clamped offsets, then select
-      f32x4 a[kGemmRT][KG];
-#pragma unroll
-      for (int r = 0; r < kGemmRT; ++r) {
-        const int prow = row0 + r * 16 + li;
-        const bool pv = prow < HW;
-        if (!CONV3) {
-          const int off0 = prow * p.lda + 4 * lq + kc * KG * 16;
-#pragma unroll
-          for (int g = 0; g < KG; ++g) {
-            const bool ok = pv && (kc * KG + g) < p.kgroups;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(Ab + (ok ? off0 + g * 16 : 0));
-            a[r][g] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-        } else {
-          const int py = prow / p.W;
-          const int px = prow - py * p.W;
-#pragma unroll
-          for (int g = 0; g < KG; ++g) {
-            const int gg = kc * KG + g;
-            const int tap = gg / p.cg_per_tap;
-            const int cgi = gg - tap * p.cg_per_tap;
-            const int ty = tap / 3;
-            const int yy = py + (ty - 1) * p.dil;
-            const int xx = px + (tap - 3 * ty - 1) * p.dil;
-            const bool ok = pv && gg < p.kgroups && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-            const int off = (yy * p.W + xx) * p.lda + cgi * 16 + 4 * lq;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(Ab + (ok ? off : 0));
-            a[r][g] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
-      }
-
-      if (p.ln) {
-        const float wb = (p.ln == 2) ? 1.f : 0.f;
-#pragma unroll
-        for (int r = 0; r < kGemmRT; ++r) {
-          float mean, rstd;
-          if (p.stats) {
-            const int prow = min(row0 + r * 16 + li, HW - 1);
-            const float2 st = *reinterpret_cast<const float2*>(p.stats + 2 * ((long long)b * HW + prow));
-            mean = st.x;
-            rstd = st.y;
-          } else {
-            // the whole LN row is in this k-chunk (host: kchunks == 1, kgroups * 16 == ln_C)
-            float s = 0.f;
-#pragma unroll
-            for (int g = 0; g < KG; ++g) s += (a[r][g].x + a[r][g].y) + (a[r][g].z + a[r][g].w);
-            s += __shfl_xor(s, 16);
-            s += __shfl_xor(s, 32);
-            mean = s / (float)p.ln_C;
-            float v2 = 0.f;
-#pragma unroll
-            for (int g = 0; g < KG; ++g) {
-              const f32x4 d = a[r][g] - mean;
-              const float dd = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
-              v2 += (g < p.kgroups) ? dd : 0.f;
-            }
-            v2 += __shfl_xor(v2, 16);
-            v2 += __shfl_xor(v2, 32);
-            rstd = 1.0f / sqrtf(v2 / (float)p.ln_C + 1e-5f);
-          }
-          const float sh = mean * wb;
-#pragma unroll
-          for (int g = 0; g < KG; ++g) a[r][g] = (a[r][g] - sh) * rstd;
-        }
-      }
-
-      // ---- MFMA over the chunk.  Per k-group: NT LDS b128 reads, then the 4 k-steps with the
-      // NT x RT independent accumulators innermost (hides the 40-cycle dependent latency).
-      // Tiles / groups past the end were zero-filled in LDS and A, so no per-tile branches.
-#pragma unroll
-      for (int g = 0; g < KG; ++g) {
-        f32x4 bw[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) bw[t] = wlds[(t * KG + g) * 64 + lane];
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int r = 0; r < kGemmRT; ++r) acc[t][r] = mfma4(bw[t][s], a[r][g][s], acc[t][r]);
-      }
-    }
-
-    // ---- epilogue: lane (li, lq) holds pixel (row0 + 16 r + li), channels n0 + 4 lq + e
-    const float* __restrict__ Rb = p.R ? p.R + (long long)b * HW * p.ldr : nullptr;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int n0 = (nc * NT + t) * 16;
-      if (n0 >= p.N) continue;
-      const int nq = n0 + 4 * lq;
-      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + nq) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < kGemmRT; ++r) {
-        const int pl = row0 + r * 16 + li;
-        if (pl >= HW) continue;
-        f32x4 v = acc[t][r] + bias;
-        if (OUT == 0) {
-          if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + pl * p.ldr + nq);
-          if (p.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
-          *reinterpret_cast<f32x4*>(p.out + (long long)b * HW * p.ldo + pl * p.ldo + nq) = v;
-        } else {
-          const int y = pl / p.W, x = pl - y * p.W;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int n = nq + e;
-            if (n >= p.N) continue;
-            float val = v[e];
-            if (p.relu) val = fmaxf(val, 0.f);
-            long long dst;
-            int ch;
-            if (OUT == 1) {
-              const int Wo = p.W >> 1, Ho = p.H >> 1;
-              dst = (long long)b * Ho * Wo + (y >> 1) * Wo + (x >> 1);
-              ch = n * 4 + (y & 1) * 2 + (x & 1);
-            } else {
-              dst = (long long)b * 4 * HW + (2 * y + ((n >> 1) & 1)) * (2 * p.W) + 2 * x + (n & 1);
-              ch = n >> 2;
-            }
-            p.out[dst * p.ldo + ch] = val;
-          }
-        }
-      }
+      epilogue<NT, OUT>(p, b, row0, nc * NT, NT, li, lq, HW, acc);
     }
   }
 }
 
+// (NT, KG, CONV3, OUT, PF).  Resident variants need KG == kgroups exactly; chunked ones any KG.
 #define KDLAE_GEMM_VARIANTS(X) \
-  X(3, 3, false, 0) X(6, 3, false, 0) X(9, 3, false, 0) X(12, 3, false, 0) \
-  X(3, 6, false, 0) X(6, 6, false, 0) X(9, 6, false, 0) X(12, 6, false, 0) \
-  X(3, 8, false, 0) X(6, 8, false, 0) X(9, 8, false, 0) \
-  X(3, 12, false, 0) X(6, 12, false, 0) \
-  X(3, 16, false, 0) X(6, 16, false, 0) \
-  X(3, 3, true, 1) X(3, 6, true, 1) X(6, 6, true, 1) X(6, 12, true, 1) X(12, 3, true, 1) X(12, 6, true, 1) \
-  X(3, 3, true, 2) X(3, 6, true, 2) X(6, 6, true, 2) X(6, 12, true, 2) X(12, 3, true, 2) X(12, 6, true, 2)
+  X(9, 3, false, 0, true) X(8, 3, false, 0, true) X(3, 3, false, 0, true) X(6, 3, false, 0, true) \
+  X(9, 6, false, 0, true) X(8, 6, false, 0, true) X(6, 6, false, 0, true) X(3, 6, false, 0, true) \
+  X(3, 8, false, 0, true) X(6, 8, false, 0, true) \
+  X(9, 12, false, 0, false) X(8, 12, false, 0, false) X(6, 12, false, 0, false) X(3, 12, false, 0, false) \
+  X(6, 16, false, 0, false) X(3, 16, false, 0, false) \
+  X(3, 3, true, 1, false) X(3, 6, true, 1, false) X(6, 6, true, 1, false) X(6, 12, true, 1, false) \
+  X(12, 3, true, 1, false) X(12, 6, true, 1, false) \
+  X(3, 3, true, 2, false) X(3, 6, true, 2, false) X(6, 6, true, 2, false) X(6, 12, true, 2, false) \
+  X(12, 3, true, 2, false) X(12, 6, true, 2, false)
 
 bool gemm_has_variant(int NT, int KG, bool conv3) {
-#define X(a, b, c, o) if (NT == a && KG == b && conv3 == c) return true;
+#define X(a, b, c, o, f) if (NT == a && KG == b && conv3 == c) return true;
   KDLAE_GEMM_VARIANTS(X)
 #undef X
   return false;
 }
 
-template <int NT, int KG, bool C3, int OUT>
-static hipError_t launch_variant(const GemmParams& p, int grid_x, hipStream_t s) {
-  const size_t lds = (size_t)NT * KG * 64 * sizeof(f32x4);
-  static bool attr_done = false;
-  if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<NT, KG, C3, OUT>),
+template <int NT, int KG, bool C3, int OUT, bool PF>
+static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
+  static size_t attr_lds = 0;
+  if (lds > attr_lds) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<NT, KG, C3, OUT, PF>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attr_done = true;
+    attr_lds = lds;
   }
-  const int nchunks = (p.ntiles + NT - 1) / NT;
-  dim3 grid(grid_x, nchunks);
-  hipLaunchKernelGGL((conv_gemm_kernel<NT, KG, C3, OUT>), grid, dim3(kGemmThreads), lds, s, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<NT, KG, C3, OUT, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
   return hipGetLastError();
 }
 
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int grid_x, hipStream_t s) {
   const bool c3 = p.ksize == 3;
   if (p.out_mode == 0 && (p.N % 16)) return hipErrorInvalidValue;  // plain stores are whole 16-channel tiles
-#define X(a, b, c, o) \
-  if (NT == a && KG == b && c3 == c && p.out_mode == o) return launch_variant<a, b, c, o>(p, grid_x, s);
+  int grid_y;
+  size_t lds;
+  if (p.group_tiles > 0) {
+    if (p.kgroups != KG || p.kchunks != 1) return hipErrorInvalidValue;
+    grid_y = (p.ntiles + p.group_tiles - 1) / p.group_tiles;
+    lds = (size_t)((p.group_tiles + NT - 1) / NT) * NT * p.kgroups * 1024;
+  } else {
+    grid_y = (p.ntiles + NT - 1) / NT;
+    lds = (size_t)NT * KG * 1024;
+  }
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+#define X(a, b, c, o, f) \
+  if (NT == a && KG == b && c3 == c && p.out_mode == o) return launch_variant<a, b, c, o, f>(p, grid_x, grid_y, lds, s);
   KDLAE_GEMM_VARIANTS(X)
 #undef X
   return hipErrorInvalidValue;

@@ -44,7 +44,7 @@ static constexpr size_t kNone = (size_t)-1;
 struct Gemm {
   size_t w = kNone, bias = kNone;  // offsets (floats) into the device weight arena
   int ntiles = 0, kgroups = 0, N = 0, K = 0, ksize = 1, cg_per_tap = 0;
-  int NT = 0, KG = 0;
+  int NT = 0, KG = 0, group_tiles = 0;
   int n_true = 0, k_true = 0;  // un-padded sizes (FLOP accounting)
 };
 struct SmallW {
@@ -58,18 +58,45 @@ struct BlockW {
   size_t dwffn = kNone, dwffn_b = kNone;
 };
 
-static void choose_variant(Gemm& g, bool prefer_single_k) {
-  static const int nts[] = {3, 6, 9, 12};
+// Tile-shape selection.  Resident schedule when a variant with KG == kgroups exists: the weights
+// are split into groups that fit the LDS budget (one group per grid.y), and NT (accumulator tiles
+// per pass) minimises padding inside a group.  Otherwise the chunked schedule over (NT, KG).
+static constexpr int kLdsBudgetKB = 152;
+
+static void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
+  static const int nts[] = {3, 6, 8, 9, 12};
   static const int kgs[] = {3, 6, 8, 12, 16};
+  g.group_tiles = 0;
+  if (g.ksize == 1) {
+    int best_nt = 0;
+    double best = 1e30;
+    const int budget = std::max(1, kLdsBudgetKB / g.kgroups);
+    const int ngroups = (int)ceil_div(g.ntiles, budget);
+    const int gt = (int)ceil_div(g.ntiles, ngroups);
+    for (int nt : nts) {
+      if (!gemm_has_variant(nt, g.kgroups, false)) continue;
+      const long long padded = ceil_div(gt, nt) * nt;
+      if (padded * g.kgroups > kLdsBudgetKB + 8) continue;
+      const double cost = (double)padded / gt + 0.01 * (12 - nt);
+      if (cost < best) {
+        best = cost;
+        best_nt = nt;
+      }
+    }
+    if (best_nt) {
+      g.NT = best_nt;
+      g.KG = g.kgroups;
+      g.group_tiles = gt;
+      return;
+    }
+  }
   double best = 1e30;
   for (int nt : nts)
     for (int kg : kgs) {
       if (!gemm_has_variant(nt, kg, g.ksize == 3)) continue;
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
-      double cost = waste * (1.0 + 0.12 * (nch - 1)) * (kch > 1 ? 1.08 : 1.0);
-      if (prefer_single_k && kch > 1) cost *= 1.3;
-      cost *= 1.0 + 0.002 * (nt * kg > 96 ? nt * kg - 96 : 0);  // big LDS chunks lower occupancy
+      double cost = waste * (1.0 + 0.05 * (nch - 1));
       if (cost < best - 1e-9) {
         best = cost;
         g.NT = nt;
@@ -536,14 +563,15 @@ struct Fwd {
     p.out_mode = out_mode;
     p.tiles_per_img = (int)ceil_div(HW, kGemmRows);
     p.total_tiles = B * p.tiles_per_img;
-    const int nch = (int)ceil_div(g.ntiles, g.NT);
-    p.kchunks = (int)ceil_div(g.kgroups, g.KG);
+    p.kchunks = g.group_tiles ? 1 : (int)ceil_div(g.kgroups, g.KG);
+    p.group_tiles = g.group_tiles;
     p.stats = nullptr;
     if (ln && (p.kchunks > 1 || g.kgroups * 16 != ln_C)) {
       HIPCHK(launch_ln_stats(in.p, in.ld, ln_C, (long long)B * HW, buf(pl.stats), s));
       p.stats = buf(pl.stats);
     }
-    int gx = (int)std::min<long long>(p.total_tiles, std::max(1, 1024 / nch));
+    const int gy = g.group_tiles ? (int)ceil_div(g.ntiles, g.group_tiles) : (int)ceil_div(g.ntiles, g.NT);
+    int gx = (int)std::min<long long>(p.total_tiles, std::max<long long>(1, ceil_div(g.group_tiles ? 512 : 1024, gy)));
     p.tiles_per_block = (int)ceil_div(p.total_tiles, gx);
     gx = (int)ceil_div(p.total_tiles, p.tiles_per_block);
     int rc = probe_begin(1, probeC);

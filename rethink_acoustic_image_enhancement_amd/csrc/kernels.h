@@ -37,6 +37,7 @@ struct GemmParams {
   int out_mode;                    // 0 plain, 1 PixelUnshuffle(2), 2 PixelShuffle(2)
   int tiles_per_img, total_tiles, tiles_per_block;
   int kchunks;
+  int group_tiles;                 // resident schedule: output tiles whose weights one block keeps in LDS
 };
 
 struct GramParams {
