@@ -96,7 +96,8 @@ static void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
       if (!gemm_has_variant(nt, kg, g.ksize == 3)) continue;
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
-      double cost = waste * (1.0 + 0.05 * (nch - 1));
+      // every k-chunk restages weights behind two barriers; every n-chunk re-reads A
+      double cost = waste * (1.0 + 0.04 * (nch - 1) + 0.08 * (kch - 1));
       if (cost < best - 1e-9) {
         best = cost;
         g.NT = nt;

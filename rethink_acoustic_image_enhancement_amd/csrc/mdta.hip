@@ -197,13 +197,20 @@ __syncthreads();
 //    6-column window, so a new row costs 6 scalar loads per 4 outputs;
 //  * per row, q and k go to LDS [16 px][S], v to HBM; then the CT x CT Gram tiles (dealt to the
 //    waves) take 4 MFMA k-steps over the row's 16 pixels.  One slot per block.
+// waves per block for the sweep kernel: balances the 3*CT stencil jobs and CT^2 Gram tiles while
+// keeping per-wave VGPRs low enough for >= 2 waves per SIMD
+__host__ __device__ constexpr int gram_waves(int ct) {
+  return ct == 1 ? 3 : ct == 2 ? 6 : ct == 3 ? 9 : ct == 4 ? 12 : ct == 5 ? 15 : ct == 6 ? 9 : ct == 7 ? 7 : 12;
+}
+
 template <int CT>
-__global__ __launch_bounds__(256) void dwconv_gram_sweep_kernel(GramParams p, int nseg, int seg_rows) {
+__global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(GramParams p, int nseg, int seg_rows) {
+  constexpr int NW = gram_waves(CT);
   constexpr int Ch = CT * 16;
   constexpr int S = (Ch % 32 == 16) ? Ch : Ch + 16;
   constexpr int NJ = 3 * CT;               // stencil jobs
-  constexpr int JPW = (NJ + 3) / 4;        // jobs per wave
-  constexpr int PPW = (CT * CT + 3) / 4;   // Gram tile pairs per wave
+  constexpr int JPW = (NJ + NW - 1) / NW;  // jobs per wave
+  constexpr int PPW = (CT * CT + NW - 1) / NW;   // Gram tile pairs per wave
   __shared__ float qs[2][16 * S];
   __shared__ float ks[2][16 * S];
   __shared__ float nred[2 * Ch];
@@ -224,7 +231,7 @@ __global__ __launch_bounds__(256) void dwconv_gram_sweep_kernel(GramParams p, in
   float w[JPW][9], bias[JPW], win[JPW][3][6], n2[JPW];
 #pragma unroll
   for (int j = 0; j < JPW; ++j) {
-    const int jb = wave + 4 * j;
+    const int jb = wave + NW * j;
     const int job = jb < NJ ? jb : 0;
     part[j] = job / CT;
     const int ct = job - part[j] * CT;
@@ -259,8 +266,8 @@ __global__ __launch_bounds__(256) void dwconv_gram_sweep_kernel(GramParams p, in
     load_row(y + 1, 2);
 #pragma unroll
     for (int j = 0; j < JPW; ++j) {
-      if (wave + 4 * j < NJ) {
-        const int ct = (wave + 4 * j) % CT;
+      if (wave + NW * j < NJ) {
+        const int ct = (wave + NW * j) % CT;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           float a = bias[j];
@@ -312,11 +319,11 @@ __global__ __launch_bounds__(256) void dwconv_gram_sweep_kernel(GramParams p, in
     float t = n2[j];
     t += __shfl_xor(t, 16);
     t += __shfl_xor(t, 32);
-    const int jb = wave + 4 * j;
+    const int jb = wave + NW * j;
     if (jb < NJ && part[j] < 2 && lq == 0) nred[part[j] * Ch + (jb % CT) * 16 + li] = t;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < 2 * Ch; idx += 256) out[CT * CT * 256 + idx] = nred[idx];
+  for (int idx = threadIdx.x; idx < 2 * Ch; idx += 64 * NW) out[CT * CT * 256 + idx] = nred[idx];
 }
 
 template <int CT>
@@ -324,8 +331,8 @@ static void launch_gram_ct(const GramParams& p, hipStream_t s) {
   if (p.W % 16 == 0 && p.nslots % (p.W / 16) == 0) {
     const int nseg = p.nslots / (p.W / 16);
     const int seg_rows = (p.H + nseg - 1) / nseg;
-    hipLaunchKernelGGL(dwconv_gram_sweep_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(256), 0, s, p, nseg,
-                       seg_rows);
+    hipLaunchKernelGGL(dwconv_gram_sweep_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(64 * gram_waves(CT)), 0, s,
+                       p, nseg, seg_rows);
   } else {
     hipLaunchKernelGGL(dwconv_gram_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(256), 0, s, p);
   }
@@ -448,10 +455,10 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + e
 constexpr int kGateRows = 32;
 
 __global__ __launch_bounds__(256) void dwconv_gate_kernel(GateParams p) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 wsh[];  // [9][2][256 quads] of this block's channels
   const int c4n = p.hidS >> 2;                     // channel quads per half
   const int cols_per_block = 256 / c4n > 0 ? 256 / c4n : 1;
   const int tid = threadIdx.x;
-  // block -> (image, row segment, column group, channel-quad group)
   const int cq_groups = (c4n + 255) / 256;         // >1 only when hidS > 1024
   const int col_groups = (p.W + cols_per_block - 1) / cols_per_block;
   const int segs = (p.H + kGateRows - 1) / kGateRows;
@@ -460,27 +467,29 @@ __global__ __launch_bounds__(256) void dwconv_gate_kernel(GateParams p) {
   const int colg = bid % col_groups; bid /= col_groups;
   const int seg = bid % segs; bid /= segs;
   const int b = bid;
-  const int c4 = cqg * 256 + (c4n >= 256 ? tid : tid % c4n);
+  const int nq = min(256, c4n - cqg * 256);        // channel quads handled by this block
+  const int two = 2 * p.hidS;
+  for (int i = tid; i < 9 * 2 * nq; i += 256) {
+    const int t = i / (2 * nq), rem = i - t * 2 * nq, half = rem / nq, q = rem - half * nq;
+    wsh[(t * 2 + half) * 256 + q] =
+        *reinterpret_cast<const f32x4*>(p.w + t * two + half * p.hidS + 4 * (cqg * 256 + q));
+  }
+  __syncthreads();
+  const int ql = c4n >= 256 ? tid : tid % c4n;
+  const int c4 = cqg * 256 + ql;
   const int x = colg * cols_per_block + (c4n >= 256 ? 0 : tid / c4n);
-  if (b >= p.Bn || c4 >= c4n || x >= p.W) return;
+  if (b >= p.Bn || ql >= nq || x >= p.W) return;
   if (c4n < 256 && tid >= cols_per_block * c4n) return;
   const int c = 4 * c4;
   const int HW = p.H * p.W;
   const float* __restrict__ X = p.x + (long long)b * HW * p.ld;
   float* __restrict__ O = p.out + (long long)b * HW * p.ldo;
-  const int two = 2 * p.hidS;
-  f32x4 w1[9], w2[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    w1[t] = *reinterpret_cast<const f32x4*>(p.w + t * two + c);
-    w2[t] = *reinterpret_cast<const f32x4*>(p.w + t * two + p.hidS + c);
-  }
   const f32x4 b1 = p.b ? *reinterpret_cast<const f32x4*>(p.b + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 b2 = p.b ? *reinterpret_cast<const f32x4*>(p.b + p.hidS + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool okl = x > 0, okr = x + 1 < p.W;
-  // window rows: [0] = y-1, [1] = y, [2] = y+1; columns: [0] = x-1, [1] = x, [2] = x+1
-  f32x4 r1[3][3], r2[3][3];
+  // window rows: [0] = y-1, [1] = y, [2] = y+1 (all landed); nx = row y+2 (in flight)
+  f32x4 r1[3][3], r2[3][3], n1[3], n2[3];
   auto load_row = [&](int yy, f32x4 (&d1)[3], f32x4 (&d2)[3]) {
     const bool oky = (unsigned)yy < (unsigned)p.H;
     const int base = (oky ? yy : 0) * p.W;
@@ -498,16 +507,20 @@ __global__ __launch_bounds__(256) void dwconv_gate_kernel(GateParams p) {
   const int y1 = min(y0 + kGateRows, p.H);
   load_row(y0 - 1, r1[0], r2[0]);
   load_row(y0, r1[1], r2[1]);
+  load_row(y0 + 1, r1[2], r2[2]);
   for (int y = y0; y < y1; ++y) {
-    load_row(y + 1, r1[2], r2[2]);
+    load_row(y + 2, n1, n2);  // prefetch; consumed next iteration
+    asm volatile("" ::: "memory");  // keep the weight reads in LDS (no hoisting into 72 VGPRs)
     f32x4 a1 = b1, a2 = b2;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 3; ++i) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        a1 = r1[i][j] * w1[3 * i + j] + a1;
-        a2 = r2[i][j] * w2[3 * i + j] + a2;
+        a1 = r1[i][j] * wsh[((3 * i + j) * 2 + 0) * 256 + ql] + a1;
+        a2 = r2[i][j] * wsh[((3 * i + j) * 2 + 1) * 256 + ql] + a2;
       }
+      __builtin_amdgcn_sched_barrier(0);  // at most one window row of weights live at a time
+    }
     f32x4 o;
     o.x = gelu_erf(a1.x) * a2.x;
     o.y = gelu_erf(a1.y) * a2.y;
@@ -518,6 +531,7 @@ __global__ __launch_bounds__(256) void dwconv_gate_kernel(GateParams p) {
     for (int j = 0; j < 3; ++j) {
       r1[0][j] = r1[1][j]; r2[0][j] = r2[1][j];
       r1[1][j] = r1[2][j]; r2[1][j] = r2[2][j];
+      r1[2][j] = n1[j];    r2[2][j] = n2[j];
     }
   }
 }
@@ -527,7 +541,8 @@ hipError_t launch_dwconv_gate(const GateParams& p, hipStream_t s) {
   const int cols_per_block = 256 / c4n > 0 ? 256 / c4n : 1;
   const long long blocks = (long long)p.Bn * ((p.H + kGateRows - 1) / kGateRows) *
                            ((p.W + cols_per_block - 1) / cols_per_block) * ((c4n + 255) / 256);
-  hipLaunchKernelGGL(dwconv_gate_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  const size_t lds = (size_t)9 * 2 * 256 * sizeof(f32x4);
+  hipLaunchKernelGGL(dwconv_gate_kernel, dim3((unsigned)blocks), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
