@@ -72,7 +72,9 @@ hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// thread = pixel; weights transposed in LDS to [tap][ci][4] so every read is a broadcast float4
+// 4 lanes per pixel, each owning a quarter of the input channels (coalesced 16 B per lane along
+// channels); weights transposed in LDS to [tap][ci][4 outputs]; partial sums combined with two
+// butterfly shuffles.  A wave covers 16 pixels.
 __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
   extern __shared__ __attribute__((aligned(16))) float wso[];  // [9][Cin][4]
   const int nw = 9 * p.Cin * 4;
@@ -83,22 +85,34 @@ __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
   __syncthreads();
   const int HW = p.H * p.W;
   const long long P = (long long)p.Bn * HW;
-  for (long long pix = blockIdx.x * 256LL + threadIdx.x; pix < P; pix += (long long)gridDim.x * 256) {
-    const int b = (int)(pix / HW);
-    const int pl = (int)(pix - (long long)b * HW);
+  const int cs = threadIdx.x & 3;
+  const int cq = p.Cin >> 2;  // channels per lane (multiple of 4)
+  for (long long pix = (blockIdx.x * 256LL + threadIdx.x) >> 2; pix < P + 0; pix += (long long)gridDim.x * 64) {
+    const bool pv = pix < P;
+    const long long pc = pv ? pix : 0;
+    const int b = (int)(pc / HW);
+    const int pl = (int)(pc - (long long)b * HW);
     const int y = pl / p.W, x = pl - (pl / p.W) * p.W;
-    const float* Xb = p.in + (long long)b * HW * p.ld;
+    const float* Xb = p.in + (long long)b * HW * p.ld + cs * cq;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t < 9; ++t) {
       const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-      if ((unsigned)yy >= (unsigned)p.H || (unsigned)xx >= (unsigned)p.W) continue;
-      const float* xr = Xb + (yy * p.W + xx) * p.ld;
-      const f32x4* wt = reinterpret_cast<const f32x4*>(wso + t * p.Cin * 4);
-      for (int c = 0; c < p.Cin; c += 4) {
+      const bool ok = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      const float* xr = Xb + (ok ? (yy * p.W + xx) * p.ld : 0);
+      const f32x4* wt = reinterpret_cast<const f32x4*>(wso + (t * p.Cin + cs * cq) * 4);
+      f32x4 part = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < cq; c += 4) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(xr + c);
-        acc += v.x * wt[c] + v.y * wt[c + 1] + v.z * wt[c + 2] + v.w * wt[c + 3];
+        part += v.x * wt[c] + v.y * wt[c + 1] + v.z * wt[c + 2] + v.w * wt[c + 3];
       }
+      acc += ok ? part : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[e] += __shfl_xor(acc[e], 1);
+      acc[e] += __shfl_xor(acc[e], 2);
+    }
+    if (!pv || cs != 0) continue;
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
       if (o >= p.Cout) break;
@@ -116,8 +130,9 @@ __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
 }
 
 hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s) {
+  if (p.Cin % 16) return hipErrorInvalidValue;
   const long long P = (long long)p.Bn * p.H * p.W;
-  long long blocks = (P + 255) / 256;
+  long long blocks = (P + 63) / 64;
   if (blocks > 16384) blocks = 16384;
   const size_t lds = (size_t)9 * p.Cin * 4 * sizeof(float);
   hipLaunchKernelGGL(conv_small_out_kernel, dim3((unsigned)blocks), dim3(256), lds, s, p);

@@ -97,7 +97,7 @@ static void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
       // every k-chunk restages weights behind two barriers; every n-chunk re-reads A
-      double cost = waste * (1.0 + 0.04 * (nch - 1) + 0.08 * (kch - 1));
+      double cost = waste * (1.0 + 0.04 * (nch - 1) + (g.ksize == 3 ? 0.0 : 0.08 * (kch - 1)));
       if (cost < best - 1e-9) {
         best = cost;
         g.NT = nt;
