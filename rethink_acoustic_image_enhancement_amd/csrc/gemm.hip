@@ -114,31 +114,39 @@ __device__ __forceinline__ void apply_ln(const GemmParams& p, int b, int row0, i
 }
 
 // acc[t][r] += W-tile(t) x A(r) over KG k-groups; W tiles at wl[(t * ldk + g) * 64 + lane].
-// Pairs of tiles share a step so 4 independent accumulators interleave (MFMA latency 40 > issue 32).
+// Work is walked in units of two tiles (4 independent accumulators per k-step: MFMA latency 40 >
+// issue 32) and the B fragments of the NEXT unit (possibly of the next k-group) are read from LDS
+// before the current unit's 16 MFMAs, so LDS latency hides under ~512 cycles of matrix work even
+// at two waves per SIMD.
 template <int NT, int KG>
 __device__ __forceinline__ void mfma_chunk(const f32x4* __restrict__ wl, int ldk, int lane,
                                            const f32x4 (&a)[kGemmRT][KG], f32x4 (&acc)[NT][kGemmRT]) {
+  constexpr int NU = (NT + 1) / 2;  // units per k-group
+  f32x4 c0 = wl[(0 * ldk + 0) * 64 + lane];
+  f32x4 c1 = NT > 1 ? wl[(1 * ldk + 0) * 64 + lane] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int g = 0; g < KG; ++g) {
 #pragma unroll
-    for (int t = 0; t < NT; t += 2) {
-      if (t + 1 < NT) {
-        const f32x4 b0 = wl[(t * ldk + g) * 64 + lane];
-        const f32x4 b1 = wl[((t + 1) * ldk + g) * 64 + lane];
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int r = 0; r < kGemmRT; ++r) {
-            acc[t][r] = mfma4(b0[s], a[r][g][s], acc[t][r]);
-            acc[t + 1][r] = mfma4(b1[s], a[r][g][s], acc[t + 1][r]);
-          }
-      } else {
-        const f32x4 b0 = wl[(t * ldk + g) * 64 + lane];
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int r = 0; r < kGemmRT; ++r) acc[t][r] = mfma4(b0[s], a[r][g][s], acc[t][r]);
+    for (int u = 0; u < NU; ++u) {
+      const int t = 2 * u;
+      // prefetch the next unit
+      const int nu = (u + 1 < NU) ? u + 1 : 0;
+      const int ng = (u + 1 < NU) ? g : g + 1;
+      const int nt = 2 * nu;
+      f32x4 n0 = c0, n1 = c1;
+      if (ng < KG) {
+        n0 = wl[(nt * ldk + ng) * 64 + lane];
+        if (nt + 1 < NT) n1 = wl[((nt + 1) * ldk + ng) * 64 + lane];
       }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) {
+          acc[t][r] = mfma4(c0[s], a[r][g][s], acc[t][r]);
+          if (t + 1 < NT) acc[t + 1][r] = mfma4(c1[s], a[r][g][s], acc[t + 1][r]);
+        }
+      c0 = n0;
+      c1 = n1;
     }
   }
 }

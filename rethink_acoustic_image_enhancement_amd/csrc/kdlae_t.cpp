@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -139,6 +141,8 @@ struct kdlae_t_handle {
   size_t ev_used = 0;
   double probe_bytes = 0, probe_flops = 0;
   long long probe_launches = 0;
+  struct ProbeRec { std::string tag; double bytes, flops; };
+  std::vector<ProbeRec> probe_recs;
 
   const float* P(size_t off) const { return off == kNone ? nullptr : dev + off; }
 };
@@ -522,6 +526,7 @@ struct Fwd {
     HIPCHK(hipEventRecord(h->ev[h->ev_used], s));
     return KDLAE_OK;
   }
+  std::string tag;  // layer label of the launch being probed (per-launch dump)
   int probe_end(int cls, int C, double bytes, double flops) {
     if (!probing(cls, C)) return KDLAE_OK;
     HIPCHK(hipEventRecord(h->ev[h->ev_used + 1], s));
@@ -529,6 +534,7 @@ struct Fwd {
     h->probe_bytes += bytes;
     h->probe_flops += flops;
     h->probe_launches += 1;
+    h->probe_recs.push_back({tag, bytes, flops});
     return KDLAE_OK;
   }
 
@@ -577,6 +583,10 @@ struct Fwd {
     gx = (int)ceil_div(p.total_tiles, p.tiles_per_block);
     int rc = probe_begin(1, probeC);
     if (rc) return rc;
+    if (h->probe_class == 1)
+      tag = "gemm C" + std::to_string(probeC) + " HW" + std::to_string(HW) + " N" + std::to_string(g.n_true) + " K" +
+            std::to_string(g.k_true) + " k" + std::to_string(g.ksize) + " v" + std::to_string(g.NT) + "x" +
+            std::to_string(g.KG) + (g.group_tiles ? "r" : "c") + (ln ? " ln" : "") + (R ? " res" : "");
     HIPCHK(launch_gemm(p, g.NT, g.KG, gx, s));
     const double P = (double)B * HW;
     const double kin = g.ksize == 3 ? g.k_true / 9.0 : g.k_true;
@@ -611,6 +621,7 @@ struct Fwd {
     const int CT = b.Ch / 16;
     gp.slot_floats = CT * CT * 256 + 2 * b.Ch;
     if ((rc = probe_begin(2, b.C))) return rc;
+    tag = "gram C" + std::to_string(b.C) + " Ch" + std::to_string(b.Ch) + " HW" + std::to_string(HW);
     HIPCHK(launch_dwconv_gram(gp, s));
     if ((rc = probe_end(2, b.C, 4.0 * P * 4 * b.C, 2.0 * P * (27.0 * b.C + (double)b.C * b.Ch)))) return rc;
     HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
@@ -634,6 +645,7 @@ struct Fwd {
     ga.H = Hh;
     ga.W = Ww;
     if ((rc = probe_begin(3, b.C))) return rc;
+    tag = "gate C" + std::to_string(b.C) + " hid" + std::to_string(b.hid) + " HW" + std::to_string(HW);
     HIPCHK(launch_dwconv_gate(ga, s));
     if ((rc = probe_end(3, b.C, 4.0 * P * 3 * b.hid, 2.0 * P * 18.0 * b.hid))) return rc;
     return gemm(b.pout, h->P(b.pout.w), 0, View{buf(pl.fg), b.hidS}, Hh, Ww, x, 0, x.p, x.ld, 0, 0, b.C);
@@ -890,18 +902,27 @@ int kdlae_t_probe_arm(kdlae_t_handle* h, int kernel_class, int level_filter) {
   h->ev_used = 0;
   h->probe_bytes = h->probe_flops = 0;
   h->probe_launches = 0;
+  h->probe_recs.clear();
   return KDLAE_OK;
 }
 
 int kdlae_t_probe_read(kdlae_t_handle* h, double* ms, int64_t* launches, double* bytes, double* flops) {
   if (!h) return fail(KDLAE_ESTATE, "null handle");
   double tot = 0;
+  const char* dump = getenv("KDLAE_PROBE_DUMP");  // optional per-launch CSV (tag, ms, bytes, flops)
+  FILE* f = dump ? fopen(dump, "w") : nullptr;
+  if (f) fprintf(f, "tag,ms,bytes,flops\n");
   for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
     HIPCHK(hipEventSynchronize(h->ev[i + 1]));
     float m = 0;
     HIPCHK(hipEventElapsedTime(&m, h->ev[i], h->ev[i + 1]));
     tot += m;
+    if (f && i / 2 < h->probe_recs.size()) {
+      const auto& r = h->probe_recs[i / 2];
+      fprintf(f, "%s,%.6f,%.0f,%.0f\n", r.tag.c_str(), m, r.bytes, r.flops);
+    }
   }
+  if (f) fclose(f);
   if (ms) *ms = tot;
   if (launches) *launches = h->probe_launches;
   if (bytes) *bytes = h->probe_bytes;
