@@ -196,8 +196,10 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int b, int row0, i
   }
 }
 
-template <int NT, int KG, bool CONV3, int OUT, bool PF>
-__global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p) {
+// WPE = waves per SIMD the register budget must allow: 2 (<= 256 VGPRs, one 8-wave block per CU)
+// or 4 (<= 128 VGPRs, two blocks per CU: more latency hiding for the store-heavy small-K shapes).
+template <int NT, int KG, bool CONV3, int OUT, bool PF, int WPE, bool RES>
+__global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p
   const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
   if (t_begin >= t_end) return;
 
-  if (p.group_tiles > 0) {
+  if constexpr (RES) {
     // ------------------------------------------------------------------ resident schedule
     const int g0 = blockIdx.y * p.group_tiles;                       // first output tile of the group
     const int gtiles = min(p.group_tiles, p.ntiles - g0);
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p
       }
     }
   } else {
-    // ------------------------------------------------------------------ chunked schedule
+    // ------------------------------------------------------------------ chunked schedule (RES == false)
     const int nc = blockIdx.y;
     for (int tile = t_begin; tile < t_end; ++tile) {
       const int b = tile / p.tiles_per_img;
@@ -296,44 +298,51 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_gemm_kernel(GemmParams p
   }
 }
 
-// (NT, KG, CONV3, OUT, PF).  Resident variants need KG == kgroups exactly; chunked ones any KG.
+// (NT, KG, CONV3, OUT, PF, WPE, RES).  Resident variants need KG == kgroups exactly.
 #define KDLAE_GEMM_VARIANTS(X) \
-  X(9, 3, false, 0, true) X(8, 3, false, 0, true) X(3, 3, false, 0, true) X(6, 3, false, 0, true) \
-  X(9, 6, false, 0, true) X(8, 6, false, 0, true) X(6, 6, false, 0, true) X(3, 6, false, 0, true) \
-  X(3, 8, false, 0, true) X(6, 8, false, 0, true) \
-  X(9, 12, false, 0, false) X(8, 12, false, 0, false) X(6, 12, false, 0, false) X(3, 12, false, 0, false) \
-  X(6, 16, false, 0, false) X(3, 16, false, 0, false) \
-  X(3, 3, true, 1, false) X(3, 6, true, 1, false) X(6, 6, true, 1, false) X(6, 12, true, 1, false) \
-  X(12, 3, true, 1, false) X(12, 6, true, 1, false) \
-  X(3, 3, true, 2, false) X(3, 6, true, 2, false) X(6, 6, true, 2, false) X(6, 12, true, 2, false) \
-  X(12, 3, true, 2, false) X(12, 6, true, 2, false)
+  X(9, 3, false, 0, true, 2, true) X(8, 3, false, 0, true, 2, true) X(3, 3, false, 0, true, 2, true) \
+  X(6, 3, false, 0, true, 2, true) X(9, 6, false, 0, true, 2, true) X(8, 6, false, 0, true, 2, true) \
+  X(6, 6, false, 0, true, 2, true) X(3, 6, false, 0, true, 2, true) X(3, 8, false, 0, true, 2, true) \
+  X(6, 8, false, 0, true, 2, true) X(6, 12, false, 0, false, 2, true) X(8, 12, false, 0, false, 2, true) \
+  X(3, 12, false, 0, false, 2, true) X(6, 16, false, 0, false, 2, true) X(3, 16, false, 0, false, 2, true) \
+  X(4, 3, false, 0, true, 4, true) X(3, 3, false, 0, true, 4, true) \
+  X(3, 3, false, 0, false, 2, false) X(6, 6, false, 0, false, 2, false) X(9, 12, false, 0, false, 2, false) \
+  X(8, 12, false, 0, false, 2, false) X(6, 12, false, 0, false, 2, false) X(3, 12, false, 0, false, 2, false) \
+  X(6, 16, false, 0, false, 2, false) X(3, 16, false, 0, false, 2, false) \
+  X(3, 3, true, 1, false, 2, false) X(3, 6, true, 1, false, 2, false) X(6, 6, true, 1, false, 2, false) \
+  X(6, 12, true, 1, false, 2, false) X(12, 3, true, 1, false, 2, false) X(12, 6, true, 1, false, 2, false) \
+  X(3, 3, true, 2, false, 2, false) X(3, 6, true, 2, false, 2, false) X(6, 6, true, 2, false, 2, false) \
+  X(6, 12, true, 2, false, 2, false) X(12, 3, true, 2, false, 2, false) X(12, 6, true, 2, false, 2, false)
 
-bool gemm_has_variant(int NT, int KG, bool conv3) {
-#define X(a, b, c, o, f) if (NT == a && KG == b && conv3 == c) return true;
+bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident) {
+#define X(a, b, c, o, f, w, r) if (NT == a && KG == b && conv3 == c && wpe == w && resident == r) return true;
   KDLAE_GEMM_VARIANTS(X)
 #undef X
   return false;
 }
 
-template <int NT, int KG, bool C3, int OUT, bool PF>
+template <int NT, int KG, bool C3, int OUT, bool PF, int WPE, bool RES>
 static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
   static size_t attr_lds = 0;
   if (lds > attr_lds) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<NT, KG, C3, OUT, PF>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv_gemm_kernel<NT, KG, C3, OUT, PF, WPE, RES>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_lds = lds;
   }
-  hipLaunchKernelGGL((conv_gemm_kernel<NT, KG, C3, OUT, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<NT, KG, C3, OUT, PF, WPE, RES>), dim3(grid_x, grid_y), dim3(kGemmThreads),
+                     lds, s, p);
   return hipGetLastError();
 }
 
-hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int grid_x, hipStream_t s) {
+hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s) {
   const bool c3 = p.ksize == 3;
+  const bool res = p.group_tiles > 0;
   if (p.out_mode == 0 && (p.N % 16)) return hipErrorInvalidValue;  // plain stores are whole 16-channel tiles
   int grid_y;
   size_t lds;
-  if (p.group_tiles > 0) {
+  if (res) {
     if (p.kgroups != KG || p.kchunks != 1) return hipErrorInvalidValue;
     grid_y = (p.ntiles + p.group_tiles - 1) / p.group_tiles;
     lds = (size_t)((p.group_tiles + NT - 1) / NT) * NT * p.kgroups * 1024;
@@ -342,8 +351,9 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int grid_x, hipStrea
     lds = (size_t)NT * KG * 1024;
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-#define X(a, b, c, o, f) \
-  if (NT == a && KG == b && c3 == c && p.out_mode == o) return launch_variant<a, b, c, o, f>(p, grid_x, grid_y, lds, s);
+#define X(a, b, c, o, f, w, r)                                                                 \
+  if (NT == a && KG == b && c3 == c && p.out_mode == o && wpe == w && res == r)                \
+    return launch_variant<a, b, c, o, f, w, r>(p, grid_x, grid_y, lds, s);
   KDLAE_GEMM_VARIANTS(X)
 #undef X
   return hipErrorInvalidValue;

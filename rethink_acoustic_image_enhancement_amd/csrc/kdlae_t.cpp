@@ -46,7 +46,7 @@ static constexpr size_t kNone = (size_t)-1;
 struct Gemm {
   size_t w = kNone, bias = kNone;  // offsets (floats) into the device weight arena
   int ntiles = 0, kgroups = 0, N = 0, K = 0, ksize = 1, cg_per_tap = 0;
-  int NT = 0, KG = 0, group_tiles = 0;
+  int NT = 0, KG = 0, group_tiles = 0, WPE = 2;
   int n_true = 0, k_true = 0;  // un-padded sizes (FLOP accounting)
 };
 struct SmallW {
@@ -65,37 +65,59 @@ struct BlockW {
 // per pass) minimises padding inside a group.  Otherwise the chunked schedule over (NT, KG).
 static constexpr int kLdsBudgetKB = 152;
 
+// KDLAE_GEMM_WPE=2|4 forces one occupancy class where a variant exists (A/B measurement hook).
+static int forced_wpe() {
+  static int v = [] {
+    const char* e = getenv("KDLAE_GEMM_WPE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
-  static const int nts[] = {3, 6, 8, 9, 12};
+  static const int nts[] = {3, 4, 6, 8, 9, 12};
   static const int kgs[] = {3, 6, 8, 12, 16};
   g.group_tiles = 0;
+  g.WPE = 2;
   if (g.ksize == 1) {
-    int best_nt = 0;
+    int best_nt = 0, best_w = 2;
     double best = 1e30;
-    const int budget = std::max(1, kLdsBudgetKB / g.kgroups);
-    const int ngroups = (int)ceil_div(g.ntiles, budget);
-    const int gt = (int)ceil_div(g.ntiles, ngroups);
-    for (int nt : nts) {
-      if (!gemm_has_variant(nt, g.kgroups, false)) continue;
-      const long long padded = ceil_div(gt, nt) * nt;
-      if (padded * g.kgroups > kLdsBudgetKB + 8) continue;
-      const double cost = (double)padded / gt + 0.01 * (12 - nt);
-      if (cost < best) {
-        best = cost;
-        best_nt = nt;
+    for (int w : {2, 4}) {
+      if (forced_wpe() && forced_wpe() != w) continue;
+      // two resident blocks per CU at 4 waves/SIMD -> half the LDS budget each
+      const int budget_kb = w == 4 ? 76 : kLdsBudgetKB;
+      const int budget = std::max(1, budget_kb / g.kgroups);
+      const int ngroups = (int)ceil_div(g.ntiles, budget);
+      const int gt = (int)ceil_div(g.ntiles, ngroups);
+      for (int nt : nts) {
+        if (!gemm_has_variant(nt, g.kgroups, false, w, true)) continue;
+        const long long padded = ceil_div(gt, nt) * nt;
+        if (padded * g.kgroups > budget_kb + 8) continue;
+        // default policy: 4 waves/SIMD only for the store-heavy K <= 48 shapes
+        double cost = (double)padded / gt + 0.01 * (12 - nt) + (ngroups - 1) * 0.05;
+        if (!forced_wpe() && w == 4 && g.kgroups > 3) cost += 1.0;
+        if (!forced_wpe() && w == 2 && g.kgroups <= 3) cost += 0.5;
+        if (cost < best) {
+          best = cost;
+          best_nt = nt;
+          best_w = w;
+        }
       }
     }
     if (best_nt) {
+      const int budget_kb = best_w == 4 ? 76 : kLdsBudgetKB;
+      const int budget = std::max(1, budget_kb / g.kgroups);
       g.NT = best_nt;
       g.KG = g.kgroups;
-      g.group_tiles = gt;
+      g.WPE = best_w;
+      g.group_tiles = (int)ceil_div(g.ntiles, ceil_div(g.ntiles, budget));
       return;
     }
   }
   double best = 1e30;
   for (int nt : nts)
     for (int kg : kgs) {
-      if (!gemm_has_variant(nt, kg, g.ksize == 3)) continue;
+      if (!gemm_has_variant(nt, kg, g.ksize == 3, 2, false)) continue;
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
       // every k-chunk restages weights behind two barriers; every n-chunk re-reads A
@@ -578,7 +600,8 @@ struct Fwd {
       p.stats = buf(pl.stats);
     }
     const int gy = g.group_tiles ? (int)ceil_div(g.ntiles, g.group_tiles) : (int)ceil_div(g.ntiles, g.NT);
-    int gx = (int)std::min<long long>(p.total_tiles, std::max<long long>(1, ceil_div(g.group_tiles ? 512 : 1024, gy)));
+    int gx = (int)std::min<long long>(p.total_tiles,
+                                      std::max<long long>(1, ceil_div(g.group_tiles ? 256 * g.WPE : 1024, gy)));
     p.tiles_per_block = (int)ceil_div(p.total_tiles, gx);
     gx = (int)ceil_div(p.total_tiles, p.tiles_per_block);
     int rc = probe_begin(1, probeC);
@@ -586,8 +609,9 @@ struct Fwd {
     if (h->probe_class == 1)
       tag = "gemm C" + std::to_string(probeC) + " HW" + std::to_string(HW) + " N" + std::to_string(g.n_true) + " K" +
             std::to_string(g.k_true) + " k" + std::to_string(g.ksize) + " v" + std::to_string(g.NT) + "x" +
-            std::to_string(g.KG) + (g.group_tiles ? "r" : "c") + (ln ? " ln" : "") + (R ? " res" : "");
-    HIPCHK(launch_gemm(p, g.NT, g.KG, gx, s));
+            std::to_string(g.KG) + (g.group_tiles ? "r" : "c") + "w" + std::to_string(g.WPE) + (ln ? " ln" : "") +
+            (R ? " res" : "");
+    HIPCHK(launch_gemm(p, g.NT, g.KG, g.WPE, gx, s));
     const double P = (double)B * HW;
     const double kin = g.ksize == 3 ? g.k_true / 9.0 : g.k_true;
     const double bytes = 4.0 * (P * kin + P * g.n_true * (R ? 2.0 : 1.0) + (double)g.n_true * g.k_true);

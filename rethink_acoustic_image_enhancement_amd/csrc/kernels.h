@@ -77,8 +77,8 @@ struct SmallOutParams {            // 3x3 conv with Cout <= 4, Cin % 4 == 0
   const float* extra;                  // NCHW [B,1,H,W] copied into channel Cout (NHWC mode) or null
 };
 
-hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int grid_x, hipStream_t s);
-bool gemm_has_variant(int NT, int KG, bool conv3);
+hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s);
+bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident);
 hipError_t launch_ln_stats(const float* x, int ld, int C, long long P, float* stats, hipStream_t s);
 hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s);
 hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int heads, int nslots,
