@@ -228,7 +228,7 @@ __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(
   const int y0 = seg * seg_rows, y1 = min(y0 + seg_rows, p.H);
 
   int chan[JPW], part[JPW];
-  float w[JPW][9], bias[JPW], win[JPW][3][6], n2[JPW];
+  float w[JPW][9], bias[JPW], win[JPW][3][6], nxt[JPW][6], n2[JPW];
 #pragma unroll
   for (int j = 0; j < JPW; ++j) {
     const int jb = wave + NW * j;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(
     bias[j] = p.bdw ? p.bdw[chan[j]] : 0.f;
     n2[j] = 0.f;
   }
-  auto load_row = [&](int yy, int slotr) {
+  auto load_row = [&](int yy) {  // -> nxt
     const bool oky = (unsigned)yy < (unsigned)p.H;
 #pragma unroll
     for (int c6 = 0; c6 < 6; ++c6) {
@@ -251,19 +251,31 @@ __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(
 #pragma unroll
       for (int j = 0; j < JPW; ++j) {
         const float v = X[off + chan[j]];
-        win[j][slotr][c6] = ok ? v : 0.f;
+        nxt[j][c6] = ok ? v : 0.f;
       }
     }
+  };
+  auto put_row = [&](int slotr) {
+#pragma unroll
+    for (int j = 0; j < JPW; ++j)
+#pragma unroll
+      for (int c6 = 0; c6 < 6; ++c6) win[j][slotr][c6] = nxt[j][c6];
   };
   f32x4 acc[PPW];
 #pragma unroll
   for (int k = 0; k < PPW; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_row(y0 - 1, 0);
-  load_row(y0, 1);
+  // rolling window rows y-1, y, y+1 in win[.][0..2]; row y+2 is prefetched into nxt while row y
+  // is computed, so one memory latency overlaps a row of work instead of stalling every row
+  load_row(y0 - 1);
+  put_row(0);
+  load_row(y0);
+  put_row(1);
+  load_row(y0 + 1);
+  put_row(2);
   int buf = 0;
   for (int y = y0; y < y1; ++y) {
-    load_row(y + 1, 2);
+    load_row(y + 2);
 #pragma unroll
     for (int j = 0; j < JPW; ++j) {
       if (wave + NW * j < NJ) {
@@ -292,6 +304,7 @@ __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(
 #pragma unroll
         for (int c6 = 0; c6 < 6; ++c6) win[j][r][c6] = win[j][r + 1][c6];
     }
+    put_row(2);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {

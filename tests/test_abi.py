@@ -1,0 +1,100 @@
+"""C ABI of libkdlae.so: loads without a GPU, exports every symbol include/kdlae.h declares, and
+its host-side logic (key enumeration, config validation, strict state_dict staging) mirrors the
+reference module.  No call here touches the GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from rethink_acoustic_image_enhancement_amd import _lib
+from rethink_acoustic_image_enhancement_amd.KDLAE_model import KDLAE_teacher
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "kdlae.h")).read()
+    return sorted(set(re.findall(r"\b(kdlae_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    declared = header_symbols()
+    assert len(declared) >= 12
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(declared) == set(_lib.EXPORTS)
+    assert L.kdlae_abi_version() == 1
+
+
+def _create(m):
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    rc = L.kdlae_t_create(ctypes.byref(m._c_config()), 0, ctypes.byref(h))
+    return rc, h
+
+
+@pytest.mark.parametrize("kw", [dict(LayerNorm_type="BiasFree"), dict(), dict(bias=True, static="no", params="plus"),
+                                dict(dim=16, inp_channels=1, out_channels=1, num_blocks=[1, 2, 1, 1])])
+def test_param_enumeration_matches_module_state_dict(kw):
+    m = KDLAE_teacher(**kw)
+    rc, h = _create(m)
+    assert rc == 0
+    L = _lib.lib()
+    sd = m.state_dict()
+    n = L.kdlae_t_num_params(h)
+    assert n == len(sd)
+    for i, (k, v) in enumerate(sd.items()):
+        name, numel = ctypes.c_char_p(), ctypes.c_int64()
+        assert L.kdlae_t_param_info(h, i, ctypes.byref(name), ctypes.byref(numel)) == 0
+        assert name.value.decode() == k and numel.value == v.numel()
+    L.kdlae_t_destroy(h)
+
+
+def test_config_validation_errors():
+    rc, h = _create(KDLAE_teacher(dim=16, dual_pixel_task=True))
+    assert rc == 5 and "NameError" in _lib.last_error()
+    rc, h = _create(KDLAE_teacher(dim=20, heads=[1, 1, 1, 1]))
+    assert rc == 2
+    rc, h = _create(KDLAE_teacher(dim=48, heads=[1, 2, 4, 5]))
+    assert rc == 2
+    rc, h = _create(KDLAE_teacher(inp_channels=3, out_channels=1, dim=16))
+    assert rc == 2
+
+
+def test_strict_state_dict_staging():
+    m = KDLAE_teacher(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1)
+    rc, h = _create(m)
+    assert rc == 0
+    L = _lib.lib()
+    t = torch.zeros(16)
+    ptr = ctypes.c_void_p(t.data_ptr())
+    assert L.kdlae_t_set_param(h, b"not.a.key", ptr, 16) == 4
+    assert "unexpected key" in _lib.last_error()
+    assert L.kdlae_t_set_param(h, b"encoder_level1.0.norm1.body.weight", ptr, 15) == 4
+    assert "size mismatch" in _lib.last_error()
+    assert L.kdlae_t_set_param(h, b"encoder_level1.0.norm1.body.weight", ptr, 16) == 0
+    # commit with missing entries fails before any device work
+    assert L.kdlae_t_commit_params(h, None) == 4 and "missing" in _lib.last_error()
+    # forward before commit and workspace query before commit are state errors
+    assert L.kdlae_t_workspace_bytes(h, 1, 16, 16) == -1
+    assert L.kdlae_t_forward(h, None, None, 1, 16, 16, None, None, None, 0, None) == 6
+    L.kdlae_t_destroy(h)
+
+
+def test_module_is_drop_in_for_reference_checkpoints():
+    """strict load of a {'params': sd} checkpoint written by the module itself (BasicSR layout)."""
+    kw = dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, LayerNorm_type="BiasFree")
+    m = KDLAE_teacher(**kw)
+    ck = {"params": m.state_dict()}
+    KDLAE_teacher(**kw).load_state_dict(ck["params"], strict=True)
+    with pytest.raises(RuntimeError):  # static="train" checkpoint into static="no" fails strict load
+        KDLAE_teacher(static="no", **kw).load_state_dict(ck["params"], strict=True)
+
+
+def test_cpu_tensors_fail_loudly():
+    m = KDLAE_teacher(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m({"img": torch.zeros(1, 3, 16, 16), "denoise_rate": torch.zeros(1, 1, 16, 16)})
