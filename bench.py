@@ -125,6 +125,9 @@ def main():
                 ach = by.value / sec / 1e9
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
+            tr = pmc_traffic(args.probe)
+            if tr is not None:
+                roof["traffic"], roof["traffic_source"] = tr
             roof.update({"kernel": PROBE_CLASSES[args.probe], "launches": int(n.value),
                          "avg_launch_us": round(ms.value * 1e3 / n.value, 2),
                          "share_of_step": round(ms.value / 1e3 / elapsed, 4),
@@ -155,6 +158,21 @@ def main():
         print(json.dumps(res), flush=True)
     if distributed:
         dist.destroy_process_group()
+
+
+def pmc_traffic(cls):
+    """HBM bytes per launch of a kernel class from the committed rocprofv3 PMC summary
+    (profiles/*pmc_traffic*.json, produced by tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    c = d.get("classes", {}).get(str(cls))
+    if not c:
+        return None
+    return c["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(model, batch, out, threads):

@@ -475,7 +475,12 @@ __global__ __launch_bounds__(256) void dwconv_gate_kernel(GateParams p) {
   const int cq_groups = (c4n + 255) / 256;         // >1 only when hidS > 1024
   const int col_groups = (p.W + cols_per_block - 1) / cols_per_block;
   const int segs = (p.H + kGateRows - 1) / kGateRows;
-  int bid = blockIdx.x;
+  // XCD-aware remap (blocks b and b+8 share an XCD's L2): consecutive logical blocks — adjacent
+  // column groups whose halo columns overlap — land on the same XCD.  Grid is padded to 8k.
+  const int nb = p.Bn * segs * col_groups * cq_groups;
+  const int per = (int)(gridDim.x >> 3);
+  int bid = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (bid >= nb) return;
   const int cqg = bid % cq_groups; bid /= cq_groups;
   const int colg = bid % col_groups; bid /= col_groups;
   const int seg = bid % segs; bid /= segs;
@@ -552,8 +557,9 @@ __global__ __launch_bounds__(256) void dwconv_gate_kernel(GateParams p) {
 hipError_t launch_dwconv_gate(const GateParams& p, hipStream_t s) {
   const int c4n = p.hidS / 4;
   const int cols_per_block = 256 / c4n > 0 ? 256 / c4n : 1;
-  const long long blocks = (long long)p.Bn * ((p.H + kGateRows - 1) / kGateRows) *
-                           ((p.W + cols_per_block - 1) / cols_per_block) * ((c4n + 255) / 256);
+  long long blocks = (long long)p.Bn * ((p.H + kGateRows - 1) / kGateRows) *
+                     ((p.W + cols_per_block - 1) / cols_per_block) * ((c4n + 255) / 256);
+  blocks = (blocks + 7) / 8 * 8;  // XCD remap needs a multiple of 8
   const size_t lds = (size_t)9 * 2 * 256 * sizeof(f32x4);
   hipLaunchKernelGGL(dwconv_gate_kernel, dim3((unsigned)blocks), dim3(256), lds, s, p);
   return hipGetLastError();
