@@ -57,18 +57,25 @@ __device__ __forceinline__ void load_a(const GemmParams& p, const float* __restr
         a[r][g] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     } else {
-      const int py = prow / p.W;
-      const int px = prow - py * p.W;
+      // pixel -> (frame, y, x); taps are (dt, dy, dx) for Conv3d (kt = 3) or (dy, dx) for 2-D
+      const int fhw = p.H * p.W;
+      const int pt = prow / fhw;
+      const int rem = prow - pt * fhw;
+      const int py = rem / p.W;
+      const int px = rem - py * p.W;
 #pragma unroll
       for (int g = 0; g < KG; ++g) {
         const int gg = kc * KG + g;
         const int tap = gg / p.cg_per_tap;
         const int cgi = gg - tap * p.cg_per_tap;
-        const int ty = tap / 3;
+        const int t9 = p.kt == 3 ? tap - (tap / 9) * 9 : tap;
+        const int tt = p.kt == 3 ? pt + tap / 9 - 1 : pt;
+        const int ty = t9 / 3;
         const int yy = py + (ty - 1) * p.dil;
-        const int xx = px + (tap - 3 * ty - 1) * p.dil;
-        const bool ok = pv && gg < p.kgroups && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-        const int off = (yy * p.W + xx) * p.lda + cgi * 16 + 4 * lq;
+        const int xx = px + (t9 - 3 * ty - 1) * p.dil;
+        const bool ok = pv && gg < p.kgroups && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W &&
+                        (unsigned)tt < (unsigned)p.F;
+        const int off = ((tt * p.H + yy) * p.W + xx) * p.lda + cgi * 16 + 4 * lq;
         const f32x4 v = *reinterpret_cast<const f32x4*>(Ab + (ok ? off : 0));
         a[r][g] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -172,23 +179,27 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int b, int row0, i
         if (p.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
         *reinterpret_cast<f32x4*>(Ob + pl * p.ldo + nq) = v;
       } else {
-        const int y = pl / p.W, x = pl - y * p.W;
+        const int fhw = p.H * p.W;
+        const int t = pl / fhw;
+        const int rem = pl - t * fhw;
+        const int y = rem / p.W, x = rem - y * p.W;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int n = nq + e;
           if (n >= p.N) continue;
           float val = v[e];
-          if (p.relu) val = fmaxf(val, 0.f);
           long long dst;
           int ch;
           if (OUT == 1) {
             const int Wo = p.W >> 1, Ho = p.H >> 1;
-            dst = (long long)b * Ho * Wo + (y >> 1) * Wo + (x >> 1);
+            dst = ((long long)b * p.F + t) * Ho * Wo + (y >> 1) * Wo + (x >> 1);
             ch = n * 4 + (y & 1) * 2 + (x & 1);
           } else {
-            dst = (long long)b * 4 * HW + (2 * y + ((n >> 1) & 1)) * (2 * p.W) + 2 * x + (n & 1);
+            dst = ((long long)b * p.F + t) * 4 * fhw + (2 * y + ((n >> 1) & 1)) * (2 * p.W) + 2 * x + (n & 1);
             ch = n >> 2;
           }
+          if (p.R) val += p.R[dst * p.ldr + ch];  // residual in the OUTPUT geometry (ConvTranspose3d + skip)
+          if (p.relu) val = fmaxf(val, 0.f);
           Ob[dst * p.ldo + ch] = val;
         }
       }
@@ -204,7 +215,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
-  const int HW = p.H * p.W;
+  const int HW = p.F * p.H * p.W;  // pixels per image (x frames for 3-D sequences)
   const int t_begin = blockIdx.x * p.tiles_per_block;
   const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
   if (t_begin >= t_end) return;
@@ -312,7 +323,11 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
   X(3, 3, true, 1, false, 2, false) X(3, 6, true, 1, false, 2, false) X(6, 6, true, 1, false, 2, false) \
   X(6, 12, true, 1, false, 2, false) X(12, 3, true, 1, false, 2, false) X(12, 6, true, 1, false, 2, false) \
   X(3, 3, true, 2, false, 2, false) X(3, 6, true, 2, false, 2, false) X(6, 6, true, 2, false, 2, false) \
-  X(6, 12, true, 2, false, 2, false) X(12, 3, true, 2, false, 2, false) X(12, 6, true, 2, false, 2, false)
+  X(6, 12, true, 2, false, 2, false) X(12, 3, true, 2, false, 2, false) X(12, 6, true, 2, false, 2, false) \
+  X(1, 9, true, 0, false, 2, false) X(2, 9, true, 0, false, 2, false) X(4, 9, true, 0, false, 2, false) \
+  X(8, 6, true, 0, false, 2, false) X(4, 6, true, 0, false, 2, false) X(2, 6, true, 0, false, 2, false) \
+  X(1, 3, false, 0, false, 2, false) X(3, 4, false, 0, false, 2, false) X(4, 4, false, 2, false, 2, false) \
+  X(8, 4, false, 2, false, 2, false) X(4, 2, false, 2, false, 2, false) X(3, 3, false, 2, false, 2, false)
 
 bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident) {
 #define X(a, b, c, o, f, w, r) if (NT == a && KG == b && conv3 == c && wpe == w && resident == r) return true;

@@ -21,123 +21,15 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/kdlae.h"
-#include "kernels.h"
+#include "runtime.h"
 
 namespace kdlae {
 
-thread_local std::string g_err;
-int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
-
-#define HIPCHK(x)                                                                          \
-  do {                                                                                     \
-    hipError_t e_ = (x);                                                                   \
-    if (e_ != hipSuccess) return fail(KDLAE_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
-static inline int ru16(int x) { return (x + 15) / 16 * 16; }
-static inline long long ceil_div(long long a, long long b) { return (a + b - 1) / b; }
-static constexpr size_t kNone = (size_t)-1;
-
-// ----------------------------------------------------------------------------- packed weights
-struct Gemm {
-  size_t w = kNone, bias = kNone;  // offsets (floats) into the device weight arena
-  int ntiles = 0, kgroups = 0, N = 0, K = 0, ksize = 1, cg_per_tap = 0;
-  int NT = 0, KG = 0, group_tiles = 0, WPE = 2;
-  int n_true = 0, k_true = 0;  // un-padded sizes (FLOP accounting)
-};
-struct SmallW {
-  size_t w = kNone, bias = kNone;
-  int Cout = 0, Cin = 0;
-};
 struct BlockW {
   int C = 0, heads = 0, Ch = 0, hid = 0, hidS = 0;
   Gemm qkv, pin, pout, proj_gemm;  // proj_gemm: geometry of the per-image M GEMM
   size_t dwqkv = kNone, dwqkv_b = kNone, proj = kNone, proj_b = kNone, temp = kNone;
   size_t dwffn = kNone, dwffn_b = kNone;
-};
-
-// Tile-shape selection.  Resident schedule when a variant with KG == kgroups exists: the weights
-// are split into groups that fit the LDS budget (one group per grid.y), and NT (accumulator tiles
-// per pass) minimises padding inside a group.  Otherwise the chunked schedule over (NT, KG).
-static constexpr int kLdsBudgetKB = 152;
-
-// KDLAE_GEMM_WPE=2|4 forces one occupancy class where a variant exists (A/B measurement hook).
-static int forced_wpe() {
-  static int v = [] {
-    const char* e = getenv("KDLAE_GEMM_WPE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-static void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
-  static const int nts[] = {3, 4, 6, 8, 9, 12};
-  static const int kgs[] = {3, 6, 8, 12, 16};
-  g.group_tiles = 0;
-  g.WPE = 2;
-  if (g.ksize == 1) {
-    int best_nt = 0, best_w = 2;
-    double best = 1e30;
-    for (int w : {2, 4}) {
-      if (forced_wpe() && forced_wpe() != w) continue;
-      // two resident blocks per CU at 4 waves/SIMD -> half the LDS budget each
-      const int budget_kb = w == 4 ? 76 : kLdsBudgetKB;
-      const int budget = std::max(1, budget_kb / g.kgroups);
-      const int ngroups = (int)ceil_div(g.ntiles, budget);
-      const int gt = (int)ceil_div(g.ntiles, ngroups);
-      for (int nt : nts) {
-        if (!gemm_has_variant(nt, g.kgroups, false, w, true)) continue;
-        const long long padded = ceil_div(gt, nt) * nt;
-        if (padded * g.kgroups > budget_kb + 8) continue;
-        // default policy: 4 waves/SIMD only for the store-heavy K <= 48 shapes
-        double cost = (double)padded / gt + 0.01 * (12 - nt) + (ngroups - 1) * 0.05;
-        if (!forced_wpe() && w == 4 && g.kgroups > 3) cost += 1.0;
-        if (!forced_wpe() && w == 2 && g.kgroups <= 3) cost += 0.5;
-        if (cost < best) {
-          best = cost;
-          best_nt = nt;
-          best_w = w;
-        }
-      }
-    }
-    if (best_nt) {
-      const int budget_kb = best_w == 4 ? 76 : kLdsBudgetKB;
-      const int budget = std::max(1, budget_kb / g.kgroups);
-      g.NT = best_nt;
-      g.KG = g.kgroups;
-      g.WPE = best_w;
-      g.group_tiles = (int)ceil_div(g.ntiles, ceil_div(g.ntiles, budget));
-      return;
-    }
-  }
-  double best = 1e30;
-  for (int nt : nts)
-    for (int kg : kgs) {
-      if (!gemm_has_variant(nt, kg, g.ksize == 3, 2, false)) continue;
-      const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
-      const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
-      // every k-chunk restages weights behind two barriers; every n-chunk re-reads A
-      double cost = waste * (1.0 + 0.04 * (nch - 1) + (g.ksize == 3 ? 0.0 : 0.08 * (kch - 1)));
-      if (cost < best - 1e-9) {
-        best = cost;
-        g.NT = nt;
-        g.KG = kg;
-      }
-    }
-}
-
-struct Arena {
-  std::vector<float> h;
-  size_t add(const std::vector<float>& v) {
-    size_t off = (h.size() + 63) / 64 * 64;
-    h.resize(off + v.size());
-    std::copy(v.begin(), v.end(), h.begin() + off);
-    return off;
-  }
 };
 
 }  // namespace kdlae
@@ -441,11 +333,6 @@ struct Packer {
 };
 
 // ----------------------------------------------------------------------------- workspace plan
-struct View {
-  float* p;
-  int ld;
-};
-
 struct Plan {
   size_t total = 0;
   size_t catL1, catL2, catL3, lat, dec3, dec2, out4, refo, cenb, srs;
@@ -560,50 +447,27 @@ struct Fwd {
     return KDLAE_OK;
   }
 
-  // GEMM launch on views
+  // GEMM launch on views (probe-wrapped)
   int gemm(const Gemm& g, const float* W, long long w_img_stride, View in, int Hh, int Ww, View out,
            int out_mode, const float* R, int ldr, int ln, int ln_C, int probeC) {
     const int HW = Hh * Ww;
-    const long long lim = 1LL << 31;
-    const int ldmax = std::max({in.ld, out.ld, ldr});
-    if ((long long)HW * ldmax >= lim) return fail(KDLAE_EINVAL_SHAPE, "image too large for 32-bit in-image offsets");
-    GemmParams p{};
-    p.A = in.p;
-    p.lda = in.ld;
-    p.cg_per_tap = g.cg_per_tap;
-    p.kgroups = g.kgroups;
-    p.ksize = g.ksize;
-    p.dil = 1;
-    p.Wp = W;
-    p.w_img_stride = w_img_stride;
-    p.ntiles = g.ntiles;
-    p.N = g.N;
-    p.bias = h->P(g.bias);
-    p.out = out.p;
-    p.ldo = out.ld;
-    p.R = R;
-    p.ldr = ldr;
-    p.ln = ln;
-    p.ln_C = ln_C;
-    p.relu = 0;
-    p.Bn = B;
-    p.H = Hh;
-    p.W = Ww;
-    p.out_mode = out_mode;
-    p.tiles_per_img = (int)ceil_div(HW, kGemmRows);
-    p.total_tiles = B * p.tiles_per_img;
-    p.kchunks = g.group_tiles ? 1 : (int)ceil_div(g.kgroups, g.KG);
-    p.group_tiles = g.group_tiles;
-    p.stats = nullptr;
-    if (ln && (p.kchunks > 1 || g.kgroups * 16 != ln_C)) {
-      HIPCHK(launch_ln_stats(in.p, in.ld, ln_C, (long long)B * HW, buf(pl.stats), s));
-      p.stats = buf(pl.stats);
-    }
-    const int gy = g.group_tiles ? (int)ceil_div(g.ntiles, g.group_tiles) : (int)ceil_div(g.ntiles, g.NT);
-    int gx = (int)std::min<long long>(p.total_tiles,
-                                      std::max<long long>(1, ceil_div(g.group_tiles ? 256 * g.WPE : 1024, gy)));
-    p.tiles_per_block = (int)ceil_div(p.total_tiles, gx);
-    gx = (int)ceil_div(p.total_tiles, p.tiles_per_block);
+    GemmCall c;
+    c.g = &g;
+    c.W = W;
+    c.w_img_stride = w_img_stride;
+    c.bias = h->P(g.bias);
+    c.in = in;
+    c.out = out;
+    c.B = B;
+    c.F = 1;
+    c.H = Hh;
+    c.Wd = Ww;
+    c.out_mode = out_mode;
+    c.R = R;
+    c.ldr = ldr;
+    c.ln = ln;
+    c.ln_C = ln_C;
+    c.stats_buf = buf(pl.stats);
     int rc = probe_begin(1, probeC);
     if (rc) return rc;
     if (h->probe_class == 1)
@@ -611,7 +475,7 @@ struct Fwd {
             std::to_string(g.k_true) + " k" + std::to_string(g.ksize) + " v" + std::to_string(g.NT) + "x" +
             std::to_string(g.KG) + (g.group_tiles ? "r" : "c") + "w" + std::to_string(g.WPE) + (ln ? " ln" : "") +
             (R ? " res" : "");
-    HIPCHK(launch_gemm(p, g.NT, g.KG, g.WPE, gx, s));
+    if ((rc = run_gemm(c, s))) return rc;
     const double P = (double)B * HW;
     const double kin = g.ksize == 3 ? g.k_true / 9.0 : g.k_true;
     const double bytes = 4.0 * (P * kin + P * g.n_true * (R ? 2.0 : 1.0) + (double)g.n_true * g.k_true);

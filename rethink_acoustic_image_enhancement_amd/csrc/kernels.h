@@ -38,6 +38,7 @@ struct GemmParams {
   int tiles_per_img, total_tiles, tiles_per_block;
   int kchunks;
   int group_tiles;                 // resident schedule: output tiles whose weights one block keeps in LDS
+  int F, kt;                       // frames per sequence (1 for 2-D) and temporal taps (1, or 3 for Conv3d)
 };
 
 struct GramParams {

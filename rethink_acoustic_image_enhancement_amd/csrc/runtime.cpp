@@ -1,0 +1,185 @@
+// Shared host runtime (see runtime.h).
+#include "runtime.h"
+
+#include <cstdio>
+#include <cstdlib>
+
+namespace kdlae {
+
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+// Tile-shape selection.  Resident schedule when a variant with KG == kgroups exists: the weights
+// are split into groups that fit the LDS budget (one group per grid.y), and NT (accumulator tiles
+// per pass) minimises padding inside a group.  Otherwise the chunked schedule over (NT, KG).
+static constexpr int kLdsBudgetKB = 152;
+
+// KDLAE_GEMM_WPE=2|4 forces one occupancy class where a variant exists (A/B measurement hook).
+static int forced_wpe() {
+  static int v = [] {
+    const char* e = getenv("KDLAE_GEMM_WPE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
+  static const int nts[] = {3, 4, 6, 8, 9, 12};
+  static const int kgs[] = {3, 6, 8, 12, 16};
+  g.group_tiles = 0;
+  g.WPE = 2;
+  if (g.ksize == 1) {
+    int best_nt = 0, best_w = 2;
+    double best = 1e30;
+    for (int w : {2, 4}) {
+      if (forced_wpe() && forced_wpe() != w) continue;
+      // two resident blocks per CU at 4 waves/SIMD -> half the LDS budget each
+      const int budget_kb = w == 4 ? 76 : kLdsBudgetKB;
+      const int budget = std::max(1, budget_kb / g.kgroups);
+      const int ngroups = (int)ceil_div(g.ntiles, budget);
+      const int gt = (int)ceil_div(g.ntiles, ngroups);
+      for (int nt : nts) {
+        if (!gemm_has_variant(nt, g.kgroups, false, w, true)) continue;
+        const long long padded = ceil_div(gt, nt) * nt;
+        if (padded * g.kgroups > budget_kb + 8) continue;
+        // default policy: 4 waves/SIMD only for the store-heavy K <= 48 shapes
+        double cost = (double)padded / gt + 0.01 * (12 - nt) + (ngroups - 1) * 0.05;
+        if (!forced_wpe() && w == 4 && g.kgroups > 3) cost += 1.0;
+        if (!forced_wpe() && w == 2 && g.kgroups <= 3) cost += 0.5;
+        if (cost < best) {
+          best = cost;
+          best_nt = nt;
+          best_w = w;
+        }
+      }
+    }
+    if (best_nt) {
+      const int budget_kb = best_w == 4 ? 76 : kLdsBudgetKB;
+      const int budget = std::max(1, budget_kb / g.kgroups);
+      g.NT = best_nt;
+      g.KG = g.kgroups;
+      g.WPE = best_w;
+      g.group_tiles = (int)ceil_div(g.ntiles, ceil_div(g.ntiles, budget));
+      return;
+    }
+  }
+  double best = 1e30;
+  for (int nt : nts)
+    for (int kg : kgs) {
+      if (!gemm_has_variant(nt, kg, g.ksize == 3, 2, false)) continue;
+      const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
+      const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
+      // every k-chunk restages weights behind two barriers; every n-chunk re-reads A
+      double cost = waste * (1.0 + 0.04 * (nch - 1) + (g.ksize == 3 ? 0.0 : 0.08 * (kch - 1)));
+      if (cost < best - 1e-9) {
+        best = cost;
+        g.NT = nt;
+        g.KG = kg;
+      }
+    }
+}
+
+
+int ParamStore::set(const char* name, const float* data, int64_t numel) {
+  auto it = index.find(name);
+  if (it == index.end()) return fail(KDLAE_EPARAM, std::string("unexpected key in state_dict: ") + name);
+  if (keys[it->second].second != numel)
+    return fail(KDLAE_EPARAM, std::string("size mismatch for ") + name + ": expected " +
+                                  std::to_string(keys[it->second].second) + " got " + std::to_string(numel));
+  staged[name].assign(data, data + numel);
+  return KDLAE_OK;
+}
+
+int ParamStore::info(int i, const char** name, int64_t* numel) const {
+  if (i < 0 || i >= (int)keys.size()) return fail(KDLAE_EPARAM, "param index out of range");
+  if (name) *name = keys[i].first.c_str();
+  if (numel) *numel = keys[i].second;
+  return KDLAE_OK;
+}
+
+int ParamStore::check_complete() const {
+  for (auto& kv : keys)
+    if (!staged.count(kv.first)) return fail(KDLAE_EPARAM, "missing state_dict entry: " + kv.first);
+  return KDLAE_OK;
+}
+
+const std::vector<float>* ParamStore::get(const std::string& k, int* err) const {
+  auto it = staged.find(k);
+  if (it == staged.end()) {
+    if (err && *err == KDLAE_OK) *err = fail(KDLAE_EPARAM, "missing state_dict entry: " + k);
+    return nullptr;
+  }
+  return &it->second;
+}
+
+int DeviceWeights::upload(Arena& a, hipStream_t s) {
+  release();
+  const size_t m = std::max<size_t>(a.h.size(), 64);
+  a.h.resize(m, 0.f);
+  HIPCHK(hipMalloc(&dev, m * sizeof(float)));
+  n = m;
+  HIPCHK(hipMemcpyAsync(dev, a.h.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return KDLAE_OK;
+}
+
+void DeviceWeights::release() {
+  if (dev) (void)hipFree(dev);
+  dev = nullptr;
+  n = 0;
+}
+
+int run_gemm(const GemmCall& c, hipStream_t s) {
+  const Gemm& g = *c.g;
+  const long long HW = (long long)c.F * c.H * c.Wd;
+  const int ldmax = std::max({c.in.ld, c.out.ld, c.ldr});
+  if (HW * ldmax * (c.out_mode == 2 ? 4 : 1) >= (1LL << 31))
+    return fail(KDLAE_EINVAL_SHAPE, "image too large for 32-bit in-image offsets");
+  GemmParams p{};
+  p.A = c.in.p;
+  p.lda = c.in.ld;
+  p.cg_per_tap = g.cg_per_tap;
+  p.kgroups = g.kgroups;
+  p.ksize = g.ksize;
+  p.dil = 1;
+  p.Wp = c.W;
+  p.w_img_stride = c.w_img_stride;
+  p.ntiles = g.ntiles;
+  p.N = g.N;
+  p.bias = c.bias;
+  p.out = c.out.p;
+  p.ldo = c.out.ld;
+  p.R = c.R;
+  p.ldr = c.ldr;
+  p.ln = c.ln;
+  p.ln_C = c.ln_C;
+  p.relu = c.relu;
+  p.Bn = c.B;
+  p.H = c.H;
+  p.W = c.Wd;
+  p.F = c.F;
+  p.kt = g.kt;
+  p.out_mode = c.out_mode;
+  p.tiles_per_img = (int)ceil_div(HW, kGemmRows);
+  p.total_tiles = c.B * p.tiles_per_img;
+  p.kchunks = g.group_tiles ? 1 : (int)ceil_div(g.kgroups, g.KG);
+  p.group_tiles = g.group_tiles;
+  p.stats = nullptr;
+  if (c.ln && (p.kchunks > 1 || g.kgroups * 16 != c.ln_C)) {
+    if (!c.stats_buf) return fail(KDLAE_ESTATE, "LN GEMM needs a stats buffer");
+    HIPCHK(launch_ln_stats(c.in.p, c.in.ld, c.ln_C, (long long)c.B * HW, c.stats_buf, s));
+    p.stats = c.stats_buf;
+  }
+  const int gy = g.group_tiles ? (int)ceil_div(g.ntiles, g.group_tiles) : (int)ceil_div(g.ntiles, g.NT);
+  int gx = (int)std::min<long long>(p.total_tiles,
+                                    std::max<long long>(1, ceil_div(g.group_tiles ? 256 * g.WPE : 1024, gy)));
+  p.tiles_per_block = (int)ceil_div(p.total_tiles, gx);
+  gx = (int)ceil_div(p.total_tiles, p.tiles_per_block);
+  HIPCHK(launch_gemm(p, g.NT, g.KG, g.WPE, gx, s));
+  return KDLAE_OK;
+}
+
+}  // namespace kdlae
