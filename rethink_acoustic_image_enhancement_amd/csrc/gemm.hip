@@ -329,8 +329,9 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
   X(1, 3, false, 0, false, 2, false) X(3, 4, false, 0, false, 2, false) X(4, 4, false, 2, false, 2, false) \
   X(8, 4, false, 2, false, 2, false) X(4, 2, false, 2, false, 2, false) X(3, 3, false, 2, false, 2, false)
 
-bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident) {
-#define X(a, b, c, o, f, w, r) if (NT == a && KG == b && conv3 == c && wpe == w && resident == r) return true;
+bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident, int out_mode) {
+#define X(a, b, c, o, f, w, r) \
+  if (NT == a && KG == b && conv3 == c && wpe == w && resident == r && out_mode == o) return true;
   KDLAE_GEMM_VARIANTS(X)
 #undef X
   return false;

@@ -230,8 +230,9 @@ struct Packer {
   }
 
   // 3x3 conv [Cout][Cin][3][3] as implicit GEMM, k = tap * Cin + c (Cin % 16 == 0)
-  Gemm conv3(const std::string& name, int Cout, int Cin) {
+  Gemm conv3(const std::string& name, int Cout, int Cin, int out_mode) {
     Gemm g;
+    g.out_mode = out_mode;
     const std::vector<float>* W = get(name + ".weight");
     if (err) return g;
     g.ksize = 3;
@@ -713,19 +714,19 @@ int kdlae_t_commit_params(kdlae_t_handle* h, void* stream) {
   const int nr = c.num_refinement_blocks;
   h->patch_embed = pk.small("patch_embed.proj", d, c.inp_channels, false);
   h->enc1 = pk.stage("encoder_level1", nb[0], d, hd[0]);
-  h->down1_2 = pk.conv3("down1_2.body.0", d / 2, d);
+  h->down1_2 = pk.conv3("down1_2.body.0", d / 2, d, 1);
   h->enc2 = pk.stage("encoder_level2", nb[1], 2 * d, hd[1]);
-  h->down2_3 = pk.conv3("down2_3.body.0", d, 2 * d);
+  h->down2_3 = pk.conv3("down2_3.body.0", d, 2 * d, 1);
   h->enc3 = pk.stage("encoder_level3", nb[2], 4 * d, hd[2]);
-  h->down3_4 = pk.conv3("down3_4.body.0", 2 * d, 4 * d);
+  h->down3_4 = pk.conv3("down3_4.body.0", 2 * d, 4 * d, 1);
   h->latent = pk.stage("latent", nb[3], 8 * d, hd[3]);
-  h->up4_3 = pk.conv3("up4_3.body.0", 16 * d, 8 * d);
+  h->up4_3 = pk.conv3("up4_3.body.0", 16 * d, 8 * d, 2);
   h->reduce3 = pk.pointwise("reduce_chan_level3", 4 * d, 8 * d, 8 * d, 4 * d, [](int n) { return n; }, "", c.bias, false);
   h->dec3 = pk.stage("decoder_level3", nb[2], 4 * d, hd[2]);
-  h->up3_2 = pk.conv3("up3_2.body.0", 8 * d, 4 * d);
+  h->up3_2 = pk.conv3("up3_2.body.0", 8 * d, 4 * d, 2);
   h->reduce2 = pk.pointwise("reduce_chan_level2", 2 * d, 4 * d, 4 * d, 2 * d, [](int n) { return n; }, "", c.bias, false);
   h->dec2 = pk.stage("decoder_level2", nb[1], 2 * d, hd[1]);
-  h->up2_1 = pk.conv3("up2_1.body.0", 4 * d, 2 * d);
+  h->up2_1 = pk.conv3("up2_1.body.0", 4 * d, 2 * d, 2);
   h->dec1 = pk.stage("decoder_level1", nb[0], 2 * d, hd[0]);
   h->refinement = pk.stage("refinement", nr, 2 * d, hd[0]);
   h->output = pk.small("output", c.out_channels, 2 * d, c.bias);
@@ -735,7 +736,7 @@ int kdlae_t_commit_params(kdlae_t_handle* h, void* stream) {
   if (c.static_train) {
     const int hc = 2 * d;
     h->cen = pk.small("cen", hc, c.out_channels, c.bias);
-    h->upen = pk.conv3("upen.body.0", 2 * hc, hc);
+    h->upen = pk.conv3("upen.body.0", 2 * hc, hc, 2);
     h->enhance = pk.stage("enhance", nr, hc / 2, hd[0]);
     h->outputen = pk.small("outputen", c.out_channels, hc / 2, c.bias);
   }

@@ -79,7 +79,7 @@ struct SmallOutParams {            // 3x3 conv with Cout <= 4, Cin % 4 == 0
 };
 
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s);
-bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident);
+bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident, int out_mode);
 hipError_t launch_ln_stats(const float* x, int ld, int C, long long P, float* stats, hipStream_t s);
 hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s);
 hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int heads, int nslots,

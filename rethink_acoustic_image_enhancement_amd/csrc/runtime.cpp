@@ -27,8 +27,8 @@ static int forced_wpe() {
 }
 
 void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
-  static const int nts[] = {3, 4, 6, 8, 9, 12};
-  static const int kgs[] = {3, 6, 8, 12, 16};
+  static const int nts[] = {1, 2, 3, 4, 6, 8, 9, 12};
+  static const int kgs[] = {2, 3, 4, 6, 8, 9, 12, 16};
   g.group_tiles = 0;
   g.WPE = 2;
   if (g.ksize == 1) {
@@ -42,7 +42,7 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
       const int ngroups = (int)ceil_div(g.ntiles, budget);
       const int gt = (int)ceil_div(g.ntiles, ngroups);
       for (int nt : nts) {
-        if (!gemm_has_variant(nt, g.kgroups, false, w, true)) continue;
+        if (!gemm_has_variant(nt, g.kgroups, false, w, true, g.out_mode)) continue;
         const long long padded = ceil_div(gt, nt) * nt;
         if (padded * g.kgroups > budget_kb + 8) continue;
         // default policy: 4 waves/SIMD only for the store-heavy K <= 48 shapes
@@ -69,7 +69,7 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
   double best = 1e30;
   for (int nt : nts)
     for (int kg : kgs) {
-      if (!gemm_has_variant(nt, kg, g.ksize == 3, 2, false)) continue;
+      if (!gemm_has_variant(nt, kg, g.ksize == 3, 2, false, g.out_mode)) continue;
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
       // every k-chunk restages weights behind two barriers; every n-chunk re-reads A

@@ -32,6 +32,7 @@ constexpr size_t kNone = (size_t)-1;
 struct Gemm {
   size_t w = kNone, bias = kNone;
   int ntiles = 0, kgroups = 0, N = 0, K = 0, ksize = 1, cg_per_tap = 0, kt = 1;
+  int out_mode = 0;  // store map the variant must support (0 plain, 1 unshuffle, 2 shuffle)
   int NT = 0, KG = 0, group_tiles = 0, WPE = 2;
   int n_true = 0, k_true = 0;  // un-padded sizes (FLOP accounting)
 };
