@@ -94,6 +94,40 @@ int kdlae_t_forward(kdlae_t_handle* h, const float* img, const float* rate, int 
 int kdlae_t_probe_arm(kdlae_t_handle* h, int kernel_class, int level_filter);
 int kdlae_t_probe_read(kdlae_t_handle* h, double* ms, int64_t* launches, double* bytes, double* flops);
 
+/* ------------------------------------------------------------------ KDLAE-S
+ * Ctor kwargs of KDLAE_student (KDLAE/KDLAE_model.py:340-384): a 3-D U-Net over a burst of frames.
+ * hidden_channels has num_hidden entries (default [8, 16, 16, 32]); levels = num_hidden - 1.
+ * The HIP path supports inp_channels == out_channels == 1 (forward unsqueezes a [B,F,H,W] input,
+ * :397) and kernel_size == 3.
+ */
+typedef struct kdlae_s_config {
+  int inp_channels;
+  int out_channels;
+  int residual;
+  int num_hidden;
+  int hidden_channels[8];
+  int kernel_size;
+} kdlae_s_config;
+
+typedef struct kdlae_s_handle kdlae_s_handle;
+
+/* replaces KDLAE_student.__init__ (KDLAE_model.py:341-384). */
+int kdlae_s_create(const kdlae_s_config* cfg, int device, kdlae_s_handle** out);
+int kdlae_s_destroy(kdlae_s_handle* h);
+/* state_dict surface: encoders.{i}.{0,2}, st_fusion.{0,2}, upconv_layers.{j}, decoders.{j}.{0,2},
+ * out_conv (same semantics as the kdlae_t_* calls). */
+int kdlae_s_num_params(const kdlae_s_handle* h);
+int kdlae_s_param_info(const kdlae_s_handle* h, int index, const char** name, int64_t* numel);
+int kdlae_s_set_param(kdlae_s_handle* h, const char* name, const float* host_data, int64_t numel);
+int kdlae_s_commit_params(kdlae_s_handle* h, void* stream);
+int64_t kdlae_s_workspace_bytes(const kdlae_s_handle* h, int B, int F, int H, int W);
+/* replaces KDLAE_student.forward (KDLAE_model.py:395-431):
+ *   x   [B, F, H, W]  (F = frames, the burst axis)
+ *   out [B, F, H, W]  (= out_conv(...) + x when residual, squeezed)
+ * H and W must be divisible by 2^levels (else KDLAE_EINVAL_SHAPE). */
+int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int W, float* out,
+                    void* workspace, int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

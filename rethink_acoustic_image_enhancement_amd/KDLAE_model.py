@@ -111,17 +111,21 @@ def _stage(n, dim, heads, ffn, bias, ln):
 
 
 class _Engine:
-    """One C-ABI handle per (module, device); re-packs weights when any parameter changes."""
+    """One C-ABI handle per (module, device); re-packs weights when any parameter changes.
 
-    def __init__(self, cfg: _lib.TConfig, device_index: int):
+    ``prefix`` selects the handle family: ``kdlae_t`` (teacher) or ``kdlae_s`` (student)."""
+
+    def __init__(self, cfg, device_index: int, prefix: str = "kdlae_t"):
         L = _lib.lib()
         h = ctypes.c_void_p()
-        _lib.check(L.kdlae_t_create(ctypes.byref(cfg), device_index, ctypes.byref(h)), "kdlae_t_create")
+        self.prefix = prefix
+        _lib.check(getattr(L, prefix + "_create")(ctypes.byref(cfg), device_index, ctypes.byref(h)),
+                   prefix + "_create")
         self.handle = h
         self.device_index = device_index
         self.signature = None
         self.ws = None
-        self._fin = weakref.finalize(self, L.kdlae_t_destroy, h)
+        self._fin = weakref.finalize(self, getattr(L, prefix + "_destroy"), h)
 
     def sync_params(self, module: nn.Module, stream) -> None:
         params = list(module.parameters())
@@ -131,9 +135,11 @@ class _Engine:
         L = _lib.lib()
         for name, t in module.state_dict().items():
             host = t.detach().to("cpu", torch.float32).contiguous()
-            _lib.check(L.kdlae_t_set_param(self.handle, name.encode(), ctypes.c_void_p(host.data_ptr()),
-                                           host.numel()), f"load {name}")
-        _lib.check(L.kdlae_t_commit_params(self.handle, ctypes.c_void_p(stream)), "kdlae_t_commit_params")
+            _lib.check(getattr(L, self.prefix + "_set_param")(self.handle, name.encode(),
+                                                              ctypes.c_void_p(host.data_ptr()), host.numel()),
+                       f"load {name}")
+        _lib.check(getattr(L, self.prefix + "_commit_params")(self.handle, ctypes.c_void_p(stream)),
+                   self.prefix + "_commit_params")
         self.signature = sig
 
     def workspace(self, nbytes: int, device) -> torch.Tensor:
@@ -262,3 +268,93 @@ class KDLAE_teacher(nn.Module):
 
 # BasicSR registers the same network under this name (Train/basicsr/models/archs/restormer_arch.py:566)
 RestormerSuperResolutionParam2 = KDLAE_teacher
+
+
+def _conv_block3d(cin, cout, k, pad):
+    """KDLAE_student._create_conv_block (KDLAE_model.py:386-393): Conv3d, ReLU, Conv3d, ReLU."""
+    return nn.Sequential(nn.Conv3d(cin, cout, kernel_size=k, padding=pad), nn.ReLU(inplace=True),
+                         nn.Conv3d(cout, cout, kernel_size=k, padding=pad), nn.ReLU(inplace=True))
+
+
+class KDLAE_student(nn.Module):
+    """KDLAE-S (KDLAE/KDLAE_model.py:340-431): multi-frame 3-D U-Net, forward on the HIP path.
+
+    ``forward(x [B, F, H, W]) -> [B, F, H, W]`` with H and W divisible by 2**(len(hidden_channels)-1).
+    """
+
+    def __init__(self, inp_channels=1, out_channels=1, residual=False, hidden_channels=[16, 32, 64], kernel_size=3):
+        super().__init__()
+        self.residual = residual
+        self.num_levels = len(hidden_channels) - 1
+        hc = list(hidden_channels)
+        pad = kernel_size // 2
+        self._cfg = dict(inp_channels=inp_channels, out_channels=out_channels, residual=residual,
+                         hidden_channels=hc, kernel_size=kernel_size)
+        self.encoders = nn.ModuleList()
+        self.pooling_layers = nn.ModuleList()
+        cin = inp_channels
+        for i in range(self.num_levels):
+            self.encoders.append(_conv_block3d(cin, hc[i], kernel_size, pad))
+            self.pooling_layers.append(nn.MaxPool3d(kernel_size=(1, 2, 2)))
+            cin = hc[i]
+        self.st_fusion = _conv_block3d(cin, hc[-1], kernel_size, pad)
+        self.upconv_layers = nn.ModuleList()
+        self.decoders = nn.ModuleList()
+        for i in range(self.num_levels - 1, -1, -1):
+            cu = hc[-1] if i == self.num_levels - 1 else hc[i + 1]
+            self.upconv_layers.append(nn.ConvTranspose3d(cu, hc[i], kernel_size=(1, 2, 2), stride=(1, 2, 2)))
+            self.decoders.append(_conv_block3d(hc[i], hc[i], kernel_size, pad))
+        self.out_conv = nn.Conv3d(hc[0], out_channels, kernel_size=(1, 1, 1))
+        self._engines = {}
+        self._warned_grad = False
+
+    def _c_config(self) -> _lib.SConfig:
+        c = self._cfg
+        cfg = _lib.SConfig()
+        cfg.inp_channels, cfg.out_channels = c["inp_channels"], c["out_channels"]
+        cfg.residual = int(bool(c["residual"]))
+        if not 2 <= len(c["hidden_channels"]) <= 8:
+            raise RuntimeError("KDLAE_student (MI355X build) supports 2..8 hidden_channels entries")
+        cfg.num_hidden = len(c["hidden_channels"])
+        for i, v in enumerate(c["hidden_channels"]):
+            cfg.hidden_channels[i] = int(v)
+        cfg.kernel_size = c["kernel_size"]
+        return cfg
+
+    def engine(self, device: torch.device) -> _Engine:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        eng = self._engines.get(idx)
+        if eng is None:
+            eng = _Engine(self._c_config(), idx, "kdlae_s")
+            self._engines[idx] = eng
+        return eng
+
+    def forward(self, x):
+        if x.device.type != "cuda":
+            raise RuntimeError("KDLAE_student (MI355X build) runs on ROCm devices only; there is no CPU fallback")
+        if x.dim() != 4:
+            raise RuntimeError(f"expected x [B,F,H,W], got {tuple(x.shape)}")
+        B, Fr, H, W = x.shape
+        m = 1 << self.num_levels
+        if H % m or W % m:
+            raise RuntimeError(f"KDLAE_student needs H and W divisible by {m}, got {H}x{W}")
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            if not self._warned_grad:
+                warnings.warn("KDLAE_student HIP forward is inference-only: outputs carry no autograd graph")
+                self._warned_grad = True
+        dev = x.device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        eng = self.engine(dev)
+        eng.sync_params(self, stream)
+        x_c = x.detach().to(torch.float32).contiguous()
+        out = torch.empty((B, Fr, H, W), device=dev, dtype=torch.float32)
+        L = _lib.lib()
+        nbytes = L.kdlae_s_workspace_bytes(eng.handle, B, Fr, H, W)
+        if nbytes < 0:
+            _lib.check(1, "kdlae_s_workspace_bytes")
+        ws = eng.workspace(nbytes, dev)
+        rc = L.kdlae_s_forward(eng.handle, ctypes.c_void_p(x_c.data_ptr()), B, Fr, H, W,
+                               ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                               ctypes.c_void_p(stream))
+        _lib.check(rc, "kdlae_s_forward")
+        return out

@@ -24,6 +24,8 @@ EXPORTS = (
     "kdlae_t_create", "kdlae_t_destroy", "kdlae_t_num_params", "kdlae_t_param_info",
     "kdlae_t_set_param", "kdlae_t_commit_params", "kdlae_t_workspace_bytes", "kdlae_t_forward",
     "kdlae_t_probe_arm", "kdlae_t_probe_read",
+    "kdlae_s_create", "kdlae_s_destroy", "kdlae_s_num_params", "kdlae_s_param_info",
+    "kdlae_s_set_param", "kdlae_s_commit_params", "kdlae_s_workspace_bytes", "kdlae_s_forward",
 )
 
 
@@ -35,6 +37,15 @@ class TConfig(ctypes.Structure):
         ("num_blocks", c_int * 4), ("num_refinement_blocks", c_int), ("heads", c_int * 4),
         ("ffn_expansion_factor", c_double), ("bias", c_int), ("layernorm_biasfree", c_int),
         ("dual_pixel_task", c_int), ("static_train", c_int), ("params_cat", c_int),
+    ]
+
+
+class SConfig(ctypes.Structure):
+    """kdlae_s_config (include/kdlae.h) = KDLAE_student ctor kwargs (KDLAE_model.py:341-342)."""
+
+    _fields_ = [
+        ("inp_channels", c_int), ("out_channels", c_int), ("residual", c_int), ("num_hidden", c_int),
+        ("hidden_channels", c_int * 8), ("kernel_size", c_int),
     ]
 
 
@@ -66,8 +77,18 @@ def lib() -> ctypes.CDLL:
     L.kdlae_t_probe_arm.argtypes = [c_void_p, c_int, c_int]
     L.kdlae_t_probe_read.argtypes = [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int64),
                                      ctypes.POINTER(c_double), ctypes.POINTER(c_double)]
+    L.kdlae_s_create.argtypes = [ctypes.POINTER(SConfig), c_int, ctypes.POINTER(c_void_p)]
+    L.kdlae_s_destroy.argtypes = [c_void_p]
+    L.kdlae_s_num_params.argtypes = [c_void_p]
+    L.kdlae_s_param_info.argtypes = [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]
+    L.kdlae_s_set_param.argtypes = [c_void_p, c_char_p, c_void_p, c_int64]
+    L.kdlae_s_commit_params.argtypes = [c_void_p, c_void_p]
+    L.kdlae_s_workspace_bytes.argtypes = [c_void_p, c_int, c_int, c_int, c_int]
+    L.kdlae_s_workspace_bytes.restype = c_int64
+    L.kdlae_s_forward.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64,
+                                  c_void_p]
     for name in EXPORTS:
-        if name not in ("kdlae_last_error", "kdlae_abi_version", "kdlae_t_workspace_bytes"):
+        if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes")):
             getattr(L, name).restype = c_int
     _lib = L
     return L

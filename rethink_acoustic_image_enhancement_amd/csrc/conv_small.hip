@@ -15,15 +15,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // thread = (16-channel output group, pixel); all lanes of a wave share the group -> LDS broadcast
 __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
-  extern __shared__ float wsm[];  // [Cout][36] (ci-major, zero for ci >= Cin) then bias[Cout]
+  extern __shared__ float wsm[];  // [Cout][36] (ci-major then taps, zero past Cin*kt*9) then bias[Cout]
+  const int taps = 9 * p.kt;
   const int nw = p.Cout * 36;
   for (int i = threadIdx.x; i < nw; i += 256) {
     const int co = i / 36, k = i - (i / 36) * 36;
-    wsm[i] = (k / 9) < p.Cin ? p.w[co * p.Cin * 9 + k] : 0.f;
+    wsm[i] = k < p.Cin * taps ? p.w[co * p.Cin * taps + k] : 0.f;
   }
   for (int i = threadIdx.x; i < p.Cout; i += 256) wsm[nw + i] = p.bias ? p.bias[i] : 0.f;
   __syncthreads();
-  const int HW = p.H * p.W;
+  const int fhw = p.H * p.W;
+  const int HW = p.F * fhw;
   const long long P = (long long)p.Bn * HW;
   const int ngroups = p.Cout / 16;
   const long long total = P * ngroups;
@@ -32,18 +34,21 @@ __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
     const long long pix = idx - (long long)og * P;
     const int b = (int)(pix / HW);
     const int pl = (int)(pix - (long long)b * HW);
-    const int y = pl / p.W, x = pl - (pl / p.W) * p.W;
+    const int t0 = pl / fhw;
+    const int rem = pl - t0 * fhw;
+    const int y = rem / p.W, x = rem - (rem / p.W) * p.W;
     float in[36];
 #pragma unroll
-    for (int ci = 0; ci < 4; ++ci) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y + (t / 3 - 1) * p.dil, xx = x + (t % 3 - 1) * p.dil;
-        const bool ok = ci < p.Cin && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-        const long long off = ok ? b * p.sb + ci * p.sc + yy * p.sy + xx * p.sx : 0;
-        const float v = p.in[off];
-        in[ci * 9 + t] = ok ? v : 0.f;
-      }
+    for (int k = 0; k < 36; ++k) {
+      const int ci = k / taps, tap = k - (k / taps) * taps;  // taps = 9 (2-D) or 27 (3-D)
+      const int t9 = tap % 9;
+      const int tt = t0 + (p.kt == 3 ? tap / 9 - 1 : 0);
+      const int yy = y + (t9 / 3 - 1) * p.dil, xx = x + (t9 % 3 - 1) * p.dil;
+      const bool ok = ci < p.Cin && (unsigned)tt < (unsigned)p.F && (unsigned)yy < (unsigned)p.H &&
+                      (unsigned)xx < (unsigned)p.W;
+      const long long off = ok ? b * p.sb + ci * p.sc + tt * p.st + yy * p.sy + xx * p.sx : 0;
+      const float v = p.in[off];
+      in[k] = ok ? v : 0.f;
     }
     float* o = p.out + pix * p.ldo + og * 16;
 #pragma unroll
@@ -56,7 +61,7 @@ __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
         float a = wsm[nw + co];
 #pragma unroll
         for (int k = 0; k < 36; ++k) a = fmaf(in[k], wr[k], a);
-        r[e] = a;
+        r[e] = p.relu ? fmaxf(a, 0.f) : a;
       }
       *reinterpret_cast<f32x4*>(o + j4 * 4) = r;
     }
@@ -64,7 +69,8 @@ __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
 }
 
 hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s) {
-  const long long total = (long long)p.Bn * p.H * p.W * (p.Cout / 16);
+  if (p.Cin * 9 * p.kt > 36 || p.Cout % 16) return hipErrorInvalidValue;
+  const long long total = (long long)p.Bn * p.F * p.H * p.W * (p.Cout / 16);
   long long blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   const size_t lds = (size_t)(p.Cout * 36 + p.Cout) * sizeof(float);
@@ -76,14 +82,16 @@ hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s) {
 // channels); weights transposed in LDS to [tap][ci][4 outputs]; partial sums combined with two
 // butterfly shuffles.  A wave covers 16 pixels.
 __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
-  extern __shared__ __attribute__((aligned(16))) float wso[];  // [9][Cin][4]
-  const int nw = 9 * p.Cin * 4;
+  extern __shared__ __attribute__((aligned(16))) float wso[];  // [taps][Cin][4]
+  const int taps = p.ks * p.ks;
+  const int nw = taps * p.Cin * 4;
   for (int i = threadIdx.x; i < nw; i += 256) {
     const int o = i & 3, ci = (i >> 2) % p.Cin, t = (i >> 2) / p.Cin;
-    wso[i] = o < p.Cout ? p.w[(o * p.Cin + ci) * 9 + t] : 0.f;
+    wso[i] = o < p.Cout ? p.w[(o * p.Cin + ci) * taps + t] : 0.f;
   }
   __syncthreads();
-  const int HW = p.H * p.W;
+  const int fhw = p.H * p.W;
+  const int HW = p.F * fhw;
   const long long P = (long long)p.Bn * HW;
   const int cs = threadIdx.x & 3;
   const int cq = p.Cin >> 2;  // channels per lane (multiple of 4)
@@ -92,11 +100,13 @@ __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
     const long long pc = pv ? pix : 0;
     const int b = (int)(pc / HW);
     const int pl = (int)(pc - (long long)b * HW);
-    const int y = pl / p.W, x = pl - (pl / p.W) * p.W;
-    const float* Xb = p.in + (long long)b * HW * p.ld + cs * cq;
+    const int tf = pl / fhw;
+    const int rem = pl - tf * fhw;
+    const int y = rem / p.W, x = rem - (rem / p.W) * p.W;
+    const float* Xb = p.in + ((long long)b * HW + (long long)tf * fhw) * p.ld + cs * cq;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < 9; ++t) {
-      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+    for (int t = 0; t < taps; ++t) {
+      const int yy = p.ks == 3 ? y + t / 3 - 1 : y, xx = p.ks == 3 ? x + t % 3 - 1 : x;
       const bool ok = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
       const float* xr = Xb + (ok ? (yy * p.W + xx) * p.ld : 0);
       const f32x4* wt = reinterpret_cast<const f32x4*>(wso + (t * p.Cin + cs * cq) * 4);
@@ -130,12 +140,49 @@ __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
 }
 
 hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s) {
-  if (p.Cin % 16) return hipErrorInvalidValue;
-  const long long P = (long long)p.Bn * p.H * p.W;
+  if (p.Cin % 16 || (p.ks != 1 && p.ks != 3)) return hipErrorInvalidValue;
+  const long long P = (long long)p.Bn * p.F * p.H * p.W;
   long long blocks = (P + 63) / 64;
   if (blocks > 16384) blocks = 16384;
-  const size_t lds = (size_t)9 * p.Cin * 4 * sizeof(float);
+  const size_t lds = (size_t)p.ks * p.ks * p.Cin * 4 * sizeof(float);
   hipLaunchKernelGGL(conv_small_out_kernel, dim3((unsigned)blocks), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+// MaxPool (1,2,2) (KDLAE_model.py:366) / MaxPool2d(2) (ASDQE_model.py:41), NHWC float4 per thread.
+__global__ __launch_bounds__(256) void maxpool2_kernel(const float* __restrict__ in, int ldi, float* __restrict__ out,
+                                                       int ldo, int C, long long nframes, int H, int W) {
+  const int Ho = H >> 1, Wo = W >> 1, c4n = C >> 2;
+  const long long total = nframes * Ho * Wo * c4n;
+  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+    const int c = (int)(idx % c4n) * 4;
+    long long r = idx / c4n;
+    const int xo = (int)(r % Wo);
+    r /= Wo;
+    const int yo = (int)(r % Ho);
+    const long long f = r / Ho;
+    const float* base = in + ((f * H + 2 * yo) * W + 2 * xo) * (long long)ldi + c;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(base);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(base + ldi);
+    const f32x4 d = *reinterpret_cast<const f32x4*>(base + (long long)W * ldi);
+    const f32x4 e = *reinterpret_cast<const f32x4*>(base + (long long)W * ldi + ldi);
+    f32x4 m;
+    m.x = fmaxf(fmaxf(a.x, b.x), fmaxf(d.x, e.x));
+    m.y = fmaxf(fmaxf(a.y, b.y), fmaxf(d.y, e.y));
+    m.z = fmaxf(fmaxf(a.z, b.z), fmaxf(d.z, e.z));
+    m.w = fmaxf(fmaxf(a.w, b.w), fmaxf(d.w, e.w));
+    *reinterpret_cast<f32x4*>(out + ((f * Ho + yo) * Wo + xo) * (long long)ldo + c) = m;
+  }
+}
+
+hipError_t launch_maxpool2(const float* in, int ldi, float* out, int ldo, int C, long long nframes, int H, int W,
+                           hipStream_t s) {
+  if (C % 4) return hipErrorInvalidValue;
+  const long long total = nframes * (H / 2) * (W / 2) * (C / 4);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(maxpool2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, ldi, out, ldo, C, nframes, H, W);
   return hipGetLastError();
 }
 

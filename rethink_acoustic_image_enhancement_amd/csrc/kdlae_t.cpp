@@ -566,6 +566,10 @@ struct Fwd {
     p.Bn = B;
     p.H = Hh;
     p.W = Ww;
+    p.F = 1;
+    p.kt = 1;
+    p.st = 0;
+    p.relu = 0;
     HIPCHK(launch_conv_small_in(p, s));
     return KDLAE_OK;
   }
@@ -582,6 +586,8 @@ struct Fwd {
     p.Bn = B;
     p.H = Hh;
     p.W = Ww;
+    p.F = 1;
+    p.ks = 3;
     p.out = out;
     p.out_nchw = nchw;
     p.ldo = ldo;

@@ -61,18 +61,21 @@ struct GateParams {
   int Bn, H, W;
 };
 
-struct SmallInParams {             // 3x3 conv with Cin <= 4, Cout % 16 == 0
+struct SmallInParams {             // 3x3 (kt=1) or 3x3x3 (kt=3) conv, Cin * 9 * kt <= 36, Cout % 16 == 0
   const float* in; long long sb, sc, sy, sx;
   int Cin, Cout, dil;
-  const float* w; const float* bias;   // w: [Cout][Cin][3][3]
+  const float* w; const float* bias;   // w: [Cout][Cin][kt][3][3]
   float* out; int ldo;
   int Bn, H, W;
+  int F, kt; long long st;             // frames per sequence, temporal taps, frame stride of the input
+  int relu;
 };
 
-struct SmallOutParams {            // 3x3 conv with Cout <= 4, Cin % 4 == 0
+struct SmallOutParams {            // 3x3 (ks=3) or pointwise (ks=1) conv with Cout <= 4, Cin % 16 == 0
   const float* in; int ld; int Cin, Cout;
-  const float* w; const float* bias;   // w: [Cout][Cin][3][3]
+  const float* w; const float* bias;   // w: [Cout][Cin][ks][ks]
   int Bn, H, W;
+  int F, ks;                           // frames per sequence (pixels per image = F*H*W), kernel size
   float* out; int out_nchw; int ldo;   // NCHW (ldo unused) or NHWC with pixel stride ldo
   const float* res;                    // NCHW residual (same shape as out) or null
   const float* extra;                  // NCHW [B,1,H,W] copied into channel Cout (NHWC mode) or null
@@ -89,5 +92,8 @@ hipError_t launch_attn_fold(const float* reduced, int slot_floats, const float* 
 hipError_t launch_dwconv_gate(const GateParams& p, hipStream_t s);
 hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s);
 hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s);
+// MaxPool (1,2,2) / MaxPool2d(2) on NHWC views: [N frames][H][W][C] -> [N][H/2][W/2][C] (floor)
+hipError_t launch_maxpool2(const float* in, int ldi, float* out, int ldo, int C, long long nframes, int H, int W,
+                           hipStream_t s);
 
 }  // namespace kdlae
