@@ -128,6 +128,36 @@ int64_t kdlae_s_workspace_bytes(const kdlae_s_handle* h, int B, int F, int H, in
 int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int W, float* out,
                     void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------ ASDQE
+ * Ctor kwargs of DenoiseRatePredictor (ASDQE/ASDQE_model.py:127).  The HIP path supports
+ * in_channels 1..4 and dim a multiple of 16 (16..256).  Eval-mode semantics only: BatchNorm uses
+ * its running statistics (folded into the conv weights at commit), Dropout is the identity.
+ */
+typedef struct asdqe_config {
+  int in_channels;
+  int dim;
+} asdqe_config;
+
+typedef struct asdqe_handle asdqe_handle;
+
+/* replaces DenoiseRatePredictor.__init__ (ASDQE_model.py:127-156). */
+int asdqe_create(const asdqe_config* cfg, int device, asdqe_handle** out);
+int asdqe_destroy(asdqe_handle* h);
+/* state_dict surface incl. BatchNorm buffers (num_batches_tracked: 1 element, ignored).  The
+ * reference loads its checkpoint with strict=False (ASDQE_test.py:79); this surface is strict. */
+int asdqe_num_params(const asdqe_handle* h);
+int asdqe_param_info(const asdqe_handle* h, int index, const char** name, int64_t* numel);
+int asdqe_set_param(asdqe_handle* h, const char* name, const float* host_data, int64_t numel);
+int asdqe_commit_params(asdqe_handle* h, void* stream);
+int64_t asdqe_workspace_bytes(const asdqe_handle* h, int B, int H, int W);
+/* replaces DenoiseRatePredictor.forward (ASDQE_model.py:158-171) in eval mode:
+ *   lq, gt [B, in_channels, H, W]  (any H, W: zero-padded bottom/right to a multiple of dim)
+ *   score  [B, 1]                   (tanh output)
+ *   feat   optional (NULL to skip): the UNet output map, NHWC [B, H', W', 3*dim] — an inspection
+ *          hook; the score path folds the 1x1 outc after the pool and does not need it. */
+int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int H, int W, float* score,
+                  float* feat, void* workspace, int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

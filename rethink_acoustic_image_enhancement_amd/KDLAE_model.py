@@ -128,7 +128,7 @@ class _Engine:
         self._fin = weakref.finalize(self, getattr(L, prefix + "_destroy"), h)
 
     def sync_params(self, module: nn.Module, stream) -> None:
-        params = list(module.parameters())
+        params = list(module.parameters()) + list(module.buffers())
         sig = tuple((id(p), p._version, p.data_ptr()) for p in params)
         if sig == self.signature:
             return

@@ -26,6 +26,8 @@ EXPORTS = (
     "kdlae_t_probe_arm", "kdlae_t_probe_read",
     "kdlae_s_create", "kdlae_s_destroy", "kdlae_s_num_params", "kdlae_s_param_info",
     "kdlae_s_set_param", "kdlae_s_commit_params", "kdlae_s_workspace_bytes", "kdlae_s_forward",
+    "asdqe_create", "asdqe_destroy", "asdqe_num_params", "asdqe_param_info", "asdqe_set_param",
+    "asdqe_commit_params", "asdqe_workspace_bytes", "asdqe_forward",
 )
 
 
@@ -47,6 +49,12 @@ class SConfig(ctypes.Structure):
         ("inp_channels", c_int), ("out_channels", c_int), ("residual", c_int), ("num_hidden", c_int),
         ("hidden_channels", c_int * 8), ("kernel_size", c_int),
     ]
+
+
+class AConfig(ctypes.Structure):
+    """asdqe_config (include/kdlae.h) = DenoiseRatePredictor ctor kwargs (ASDQE_model.py:127)."""
+
+    _fields_ = [("in_channels", c_int), ("dim", c_int)]
 
 
 _lib = None
@@ -87,6 +95,16 @@ def lib() -> ctypes.CDLL:
     L.kdlae_s_workspace_bytes.restype = c_int64
     L.kdlae_s_forward.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64,
                                   c_void_p]
+    L.asdqe_create.argtypes = [ctypes.POINTER(AConfig), c_int, ctypes.POINTER(c_void_p)]
+    L.asdqe_destroy.argtypes = [c_void_p]
+    L.asdqe_num_params.argtypes = [c_void_p]
+    L.asdqe_param_info.argtypes = [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64)]
+    L.asdqe_set_param.argtypes = [c_void_p, c_char_p, c_void_p, c_int64]
+    L.asdqe_commit_params.argtypes = [c_void_p, c_void_p]
+    L.asdqe_workspace_bytes.argtypes = [c_void_p, c_int, c_int, c_int]
+    L.asdqe_workspace_bytes.restype = c_int64
+    L.asdqe_forward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                c_int64, c_void_p]
     for name in EXPORTS:
         if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes")):
             getattr(L, name).restype = c_int

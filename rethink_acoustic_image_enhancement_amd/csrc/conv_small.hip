@@ -17,6 +17,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
   extern __shared__ float wsm[];  // [Cout][36] (ci-major then taps, zero past Cin*kt*9) then bias[Cout]
   const int taps = 9 * p.kt;
+  const int vh = p.vh ? p.vh : p.H, vw = p.vw ? p.vw : p.W;
   const int nw = p.Cout * 36;
   for (int i = threadIdx.x; i < nw; i += 256) {
     const int co = i / 36, k = i - (i / 36) * 36;
@@ -44,10 +45,11 @@ __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
       const int t9 = tap % 9;
       const int tt = t0 + (p.kt == 3 ? tap / 9 - 1 : 0);
       const int yy = y + (t9 / 3 - 1) * p.dil, xx = x + (t9 % 3 - 1) * p.dil;
-      const bool ok = ci < p.Cin && (unsigned)tt < (unsigned)p.F && (unsigned)yy < (unsigned)p.H &&
-                      (unsigned)xx < (unsigned)p.W;
+      const bool ok = ci < p.Cin && (unsigned)tt < (unsigned)p.F && (unsigned)yy < (unsigned)vh &&
+                      (unsigned)xx < (unsigned)vw;
       const long long off = ok ? b * p.sb + ci * p.sc + tt * p.st + yy * p.sy + xx * p.sx : 0;
-      const float v = p.in[off];
+      float v = p.in[off];
+      if (p.in_sub) v -= p.in_sub[off];
       in[k] = ok ? v : 0.f;
     }
     float* o = p.out + pix * p.ldo + og * 16;

@@ -69,6 +69,8 @@ struct SmallInParams {             // 3x3 (kt=1) or 3x3x3 (kt=3) conv, Cin * 9 *
   int Bn, H, W;
   int F, kt; long long st;             // frames per sequence, temporal taps, frame stride of the input
   int relu;
+  const float* in_sub;                 // if set, the conv input is (in - in_sub) (ASDQE diff extractor)
+  int vh, vw;                          // valid input extent (zero pad bottom/right beyond it); 0 = H, W
 };
 
 struct SmallOutParams {            // 3x3 (ks=3) or pointwise (ks=1) conv with Cout <= 4, Cin % 16 == 0
@@ -95,5 +97,25 @@ hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s);
 // MaxPool (1,2,2) / MaxPool2d(2) on NHWC views: [N frames][H][W][C] -> [N][H/2][W/2][C] (floor)
 hipError_t launch_maxpool2(const float* in, int ldi, float* out, int ldo, int C, long long nframes, int H, int W,
                            hipStream_t s);
+
+// Bilinear x2, align_corners=True (ASDQE_model.py:53): NHWC [N][h][w][C] -> [N][2h][2w][C] into a
+// strided destination (a concat half).  C % 4 == 0.
+hipError_t launch_upsample2x(const float* in, int ldi, float* out, int ldo, int C, int N, int h, int w,
+                             hipStream_t s);
+// Global average pool, pass 1: partial[b][slot][C] = sum over the slot's pixel range (fixed order).
+hipError_t launch_gap_partial(const float* in, int ld, int C, int B, long long HW, int slots, float* partial,
+                              hipStream_t s);
+// ASDQE head (ASDQE_model.py:144-154 + the linear outc folded ahead of the pool): per image
+// g = mean(partial) [C]; f = Wo g + bo [M]; h1 = relu(W1 f + b1) [N1]; h2 = relu(W2 h1 + b2) [N2];
+// score = tanh(w3 . h2 + b3).
+struct HeadParams {
+  const float* partial; int slots, C; float inv_hw;
+  const float* wo; const float* bo; int M;
+  const float* w1; const float* b1; int N1;
+  const float* w2; const float* b2; int N2;
+  const float* w3; const float* b3;
+  float* score; int B;
+};
+hipError_t launch_asdqe_head(const HeadParams& p, hipStream_t s);
 
 }  // namespace kdlae

@@ -165,15 +165,29 @@ ASDQE_CASES = {
 
 
 def asdqe_goldens(AM, out):
+    """Score plus the intermediates a near-constant score cannot pin: pooled UNet features (float64),
+    a [::4, ::4] subsample of the UNet output map and of the merged extractor features.  Images
+    differ per sample in brightness and noise level so that the score varies."""
     for name, (kw, shape) in ASDQE_CASES.items():
         m = _load_hash(AM.DenoiseRatePredictor(**kw))
-        lq = hash_images(f"lq:{name}", shape)
-        gt = np.clip(lq + 0.05 * hash_normal(f"gt:{name}", shape), 0, 1).astype(np.float32)
+        B = shape[0]
+        scale = (0.3 + 0.7 * np.arange(1, B + 1) / B).reshape(B, 1, 1, 1)
+        sigma = (0.02 + 0.2 * np.arange(B) / max(B - 1, 1)).reshape(B, 1, 1, 1)
+        gt = (hash_images(f"gt:{name}", shape) * scale).astype(np.float32)
+        lq = np.clip(gt + sigma * hash_normal(f"noise:{name}", shape), 0, 1).astype(np.float32)
+        cap = {}
+        h1 = m.unet.register_forward_hook(lambda mod, i, o: cap.__setitem__("feat", o.detach().clone()))
+        h2 = m.unet.register_forward_pre_hook(lambda mod, i: cap.__setitem__("merged", i[0].detach().clone()))
         with torch.no_grad():
             y = m(torch.from_numpy(lq), torch.from_numpy(gt)).numpy()
+        h1.remove()
+        h2.remove()
+        feat, merged = cap["feat"], cap["merged"]
         np.savez_compressed(os.path.join(out, f"{name}.npz"), lq=lq, gt=gt, score=y,
+                            gap64=feat.double().mean(dim=(2, 3)).numpy(),
+                            feat_sub=feat[:, :, ::4, ::4].numpy(), merged_sub=merged[:, :, ::4, ::4].numpy(),
                             cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8))
-        print(name, y.ravel())
+        print(name, y.ravel(), tuple(feat.shape))
 
 
 def main():

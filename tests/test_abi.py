@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "kdlae.h")).read()
-    return sorted(set(re.findall(r"\b(kdlae_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b((?:kdlae|asdqe)_\w+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -138,3 +138,42 @@ def test_student_config_validation():
     assert _s_create(KDLAE_student(inp_channels=2))[0] == 2
     assert _s_create(KDLAE_student(kernel_size=5))[0] == 2
     assert _s_create(KDLAE_student(hidden_channels=[16, 32, 64]))[0] == 0
+
+
+# ------------------------------------------------------------------ ASDQE handle
+from rethink_acoustic_image_enhancement_amd.ASDQE_model import DenoiseRatePredictor  # noqa: E402
+
+
+def _a_create(m):
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    rc = L.asdqe_create(ctypes.byref(m._c_config()), 0, ctypes.byref(h))
+    return rc, h
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(in_channels=1, dim=32)])
+def test_asdqe_param_enumeration(kw):
+    from oracle.asdqe_oracle import AsdqeCfg, asdqe_param_shapes
+    m = DenoiseRatePredictor(**kw)
+    rc, h = _a_create(m)
+    assert rc == 0, _lib.last_error()
+    L = _lib.lib()
+    sd = m.state_dict()
+    shapes = asdqe_param_shapes(AsdqeCfg(**kw))
+    assert list(shapes) == list(sd)
+    if not kw:
+        assert len(sd) == 148   # 148 ASDQE keys incl. BN buffers
+    assert L.asdqe_num_params(h) == len(sd)
+    for i, (k, v) in enumerate(sd.items()):
+        assert tuple(v.shape) == tuple(shapes[k])
+        name, numel = ctypes.c_char_p(), ctypes.c_int64()
+        assert L.asdqe_param_info(h, i, ctypes.byref(name), ctypes.byref(numel)) == 0
+        assert name.value.decode() == k and numel.value == v.numel()
+    assert L.asdqe_workspace_bytes(h, 2, 37, 50) > 0
+    assert L.asdqe_commit_params(h, None) == 4
+    L.asdqe_destroy(h)
+
+
+def test_asdqe_config_validation():
+    assert _a_create(DenoiseRatePredictor(dim=8))[0] == 2
+    assert _a_create(DenoiseRatePredictor(in_channels=5))[0] == 2

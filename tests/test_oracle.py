@@ -59,3 +59,21 @@ def test_oracle_rejects_bad_shapes():
     with pytest.raises(NotImplementedError):
         teacher_forward(sd, torch.zeros(1, 3, 16, 16), torch.zeros(1, 1, 16, 16),
                         TeacherCfg(dim=16, dual_pixel_task=True))
+
+
+ASDQE = ["a_b4_64", "a_b2_40x56"]
+
+
+@pytest.mark.parametrize("name", ASDQE)
+def test_asdqe_oracle_matches_reference(name):
+    from oracle.asdqe_oracle import AsdqeCfg, asdqe_features, asdqe_param_shapes
+    d, kw = load_fixture(name)
+    cfg = AsdqeCfg(**kw)
+    shapes = asdqe_param_shapes(cfg)
+    sd = hash_sd_for(shapes)
+    with torch.no_grad():
+        f = asdqe_features(sd, torch.from_numpy(d["lq"]), torch.from_numpy(d["gt"]), cfg)
+    assert max_abs(f["feat"][:, :, ::4, ::4], torch.from_numpy(d["feat_sub"])) <= 1e-5
+    assert max_abs(f["merged"][:, :, ::4, ::4], torch.from_numpy(d["merged_sub"])) <= 1e-5
+    np.testing.assert_allclose(f["feat"].double().mean(dim=(2, 3)).numpy(), d["gap64"], rtol=0, atol=1e-6)
+    assert max_abs(f["score"], torch.from_numpy(d["score"])) <= 1e-6
