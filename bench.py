@@ -31,7 +31,8 @@ sys.path.insert(0, ROOT)
 
 from rethink_acoustic_image_enhancement_amd import _lib  # noqa: E402
 from rethink_acoustic_image_enhancement_amd.hashweights import hash_images, hash_uniform, load_hash_weights  # noqa: E402
-from rethink_acoustic_image_enhancement_amd.KDLAE_model import KDLAE_teacher  # noqa: E402
+from rethink_acoustic_image_enhancement_amd.KDLAE_model import KDLAE_student, KDLAE_teacher  # noqa: E402
+from rethink_acoustic_image_enhancement_amd.ASDQE_model import DenoiseRatePredictor  # noqa: E402
 
 METRIC = "images/sec KDLAE-T 1×512×512 fp32 at 1/2/4/8 MI355X; PSNR vs ref"
 KW = dict(inp_channels=3, out_channels=3, dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4,
@@ -50,13 +51,136 @@ def make_inputs(first: int, n: int, H: int, W: int):
     return torch.from_numpy(imgs), torch.from_numpy(rate)
 
 
+S_KW = dict(inp_channels=1, out_channels=1, residual=True, hidden_channels=[16, 32, 64])  # KDLAE-S.ipynb:106
+A_KW = dict(in_channels=3, dim=16)                                                          # ASDQE_test.py
+
+
+def student_flops(hc, B, F, H, W):
+    """Algorithmic FLOPs of one KDLAE-S forward (2 per MAC, un-padded channels)."""
+    L, f, cin = len(hc) - 1, 0, 1
+    for i in range(L):
+        P = B * F * (H >> i) * (W >> i)
+        f += 2 * P * 27 * (cin * hc[i] + hc[i] * hc[i])
+        cin = hc[i]
+    P = B * F * (H >> L) * (W >> L)
+    f += 2 * P * 27 * (cin * hc[L] + hc[L] * hc[L])
+    for i in range(L - 1, -1, -1):
+        P = B * F * (H >> i) * (W >> i)
+        cu = hc[L] if i == L - 1 else hc[i + 1]
+        f += 2 * P * cu * hc[i] + 2 * P * 27 * 2 * hc[i] * hc[i]
+    return f + 2 * B * F * H * W * hc[0]
+
+
+def asdqe_flops(ci, d, B, H, W):
+    """Algorithmic FLOPs of one ASDQE forward on the padded H' x W' grid (2 per MAC)."""
+    Hp, Wp = -(-H // d) * d, -(-W // d) * d
+    P = [B * (Hp >> i) * (Wp >> i) for i in range(4)]
+    c = lambda p, a, b: 2 * p * 9 * (a * b + b * b)  # noqa: E731  DoubleConv
+    f = 3 * c(P[0], ci, d) + c(P[0], 3 * d, 64) + c(P[1], 64, 128) + c(P[2], 128, 256) + c(P[3], 256, 256)
+    f += c(P[2], 512, 128) + c(P[1], 256, 64) + c(P[0], 128, 64)
+    return f
+
+
+def bench_secondary(args, world, rank, dev, distributed):
+    """S8 (KDLAE-S bs=8 4x512x512) and A64 (ASDQE bs=64 256x256): BASELINE.json configs[2], [3]."""
+    if args.workload == "s8":
+        B = args.batch or 8
+        Fr, H, W = 4, args.size or 512, args.size or 512
+        model = KDLAE_student(**S_KW)
+        x = torch.from_numpy(np.stack([hash_images(f"s8:{rank * B + i}", (Fr, H, W)) for i in range(B)]))
+        inputs = (x.to(dev),)
+        flops = student_flops(S_KW["hidden_channels"], B, Fr, H, W)
+        workload = f"KDLAE-S forward bs={B}/GPU {Fr}x{H}x{W} fp32 (hidden [16,32,64], residual)"
+        metric = "samples/sec KDLAE-S 4-frame 512x512 fp32 (BASELINE configs[2])"
+    else:
+        B = args.batch or 64
+        H = W = args.size or 256
+        model = DenoiseRatePredictor(**A_KW)
+        g = torch.from_numpy(np.stack([hash_images(f"a64gt:{rank * B + i}", (3, H, W)) for i in range(B)]))
+        lq = (g + 0.1 * torch.from_numpy(hash_uniform("a64n", g.numel()).astype(np.float32)).view_as(g)).clamp(0, 1)
+        inputs = (lq.to(dev), g.to(dev))
+        flops = asdqe_flops(3, 16, B, H, W)
+        workload = f"ASDQE forward bs={B}/GPU 3x{H}x{W} fp32 (dim 16, eval)"
+        metric = "images/sec ASDQE 256x256 fp32 (BASELINE configs[3])"
+    load_hash_weights(model)
+    model = model.to(dev).eval()
+
+    def step():
+        with torch.no_grad():
+            return model(*inputs)
+
+    out = None
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        out = step()
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1)
+    if distributed:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # the whole forward runs on torch's current stream, so torch events bracket every launch
+    ach = flops * args.steps / (dev_ms / 1e3) / 1e12
+    roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": "whole forward (all launches)",
+            "algorithmic_flops_per_step": flops}
+    total = world * B * args.steps
+    res = {"metric": metric, "value": round(total / elapsed, 3), "unit": "images/s" if args.workload == "a64"
+           else "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp32", "data": "synthetic (hash-uniform inputs, hash weights)",
+           "config": {"workload": workload, "global_batch": world * B, "per_gpu_batch": B,
+                      "parallelism": f"dp{world} (batch-sharded, no data-path collective)"},
+           "roofline": roof}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        torch.set_num_threads(threads)
+        sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        # bounded sample: whole samples of the workload until >= 10 s of CPU work (at most B)
+        n, dt, ref = 0, 0.0, None
+        while n < B and dt < 10.0:
+            t0 = time.perf_counter()
+            with torch.no_grad():
+                if args.workload == "s8":
+                    from oracle.kdlae_oracle import StudentCfg, student_forward
+                    r = student_forward(sd, inputs[0][n:n + 1].cpu(), StudentCfg(**S_KW))
+                else:
+                    from oracle.asdqe_oracle import AsdqeCfg, asdqe_forward
+                    r = asdqe_forward(sd, inputs[0][n:n + 1].cpu(), inputs[1][n:n + 1].cpu(), AsdqeCfg(**A_KW))
+            dt += time.perf_counter() - t0
+            ref = r if ref is None else torch.cat([ref, r])
+            n += 1
+        got = out[:n].cpu()
+        res["cpu_baseline"] = {"value": round(n / dt, 5), "unit": res["unit"], "cores": threads, "kind": "port",
+                               "sample": f"first {n} samples of the workload batch, torch-CPU oracle, {threads} "
+                                         f"threads, {dt:.1f} s"}
+        res["parity"] = {"vs": f"CPU oracle, samples 0..{n - 1}", "max_abs": float((got - ref).abs().max())}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["t16", "s8", "a64"], default="t16",
+                    help="t16 = KDLAE-T bs16 512^2 (headline); s8 = KDLAE-S; a64 = ASDQE")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
-    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=0, help="images per GPU (0 = workload default)")
+    ap.add_argument("--size", type=int, default=0, help="frame size (0 = workload default)")
     ap.add_argument("--probe", type=int, default=1, help="kernel class for the roofline (0 = off)")
     ap.add_argument("--probe-level", type=int, default=0, help="channel filter for the probe (0 = all)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -71,8 +195,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    H = W = args.size
-    B = args.batch
+    if args.workload != "t16":
+        return bench_secondary(args, world, rank, dev, distributed)
+    H = W = args.size or 512
+    B = args.batch or 16
 
     model = KDLAE_teacher(**KW)
     load_hash_weights(model)
