@@ -105,9 +105,14 @@ def bench_secondary(args, world, rank, dev, distributed):
     load_hash_weights(model)
     model = model.to(dev).eval()
 
+    gather = distributed and not args.no_gather
+    if gather:
+        from rethink_acoustic_image_enhancement_amd.shard import gather_outputs
+
     def step():
         with torch.no_grad():
-            return model(*inputs)
+            o = model(*inputs)
+            return gather_outputs(o) if gather else o
 
     out = None
     for _ in range(args.warmup):
@@ -141,7 +146,8 @@ def bench_secondary(args, world, rank, dev, distributed):
            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (hash-uniform inputs, hash weights)",
            "config": {"workload": workload, "global_batch": world * B, "per_gpu_batch": B,
-                      "parallelism": f"dp{world} (batch-sharded, no data-path collective)"},
+                      "parallelism": f"dp{world} (batch-sharded" + (", RCCL all-gather of outputs in every step)"
+                                                                   if gather else ", no data-path collective)")},
            "roofline": roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -184,6 +190,8 @@ def main():
     ap.add_argument("--probe", type=int, default=1, help="kernel class for the roofline (0 = off)")
     ap.add_argument("--probe-level", type=int, default=0, help="channel filter for the probe (0 = all)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: skip the RCCL all-gather of outputs (default: gathered inside each step, §8e)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
@@ -206,9 +214,16 @@ def main():
     img, rate = make_inputs(rank * B, B, H, W)
     batch = {"img": img.to(dev), "denoise_rate": rate.to(dev)}
 
+    gather = distributed and not args.no_gather
+    if gather:
+        from rethink_acoustic_image_enhancement_amd.shard import gather_outputs
+
     def step():
         with torch.no_grad():
-            return model(batch)
+            out = model(batch)
+            if gather:  # the scaling metric runs to the end of the output all-gather
+                out = {k: gather_outputs(v) if v is not None else None for k, v in out.items()}
+            return out
 
     eng = model.engine(dev)
     L = _lib.lib()
@@ -268,7 +283,8 @@ def main():
         "data": "synthetic (hash-uniform images, hash weights of the real architecture)",
         "config": {"workload": f"KDLAE-T forward bs={B}/GPU {H}x{W} fp32 (static=train, params=cat, BiasFree)",
                    "global_batch": world * B, "per_gpu_batch": B, "H": H, "W": W,
-                   "parallelism": f"dp{world} (batch-sharded, no data-path collective)"},
+                   "parallelism": f"dp{world} (batch-sharded" + (", RCCL all-gather of hq/sr in every step)"
+                                                                if gather else ", no data-path collective)")},
         "roofline": roof,
     }
     # algorithmic per-image figures of SURVEY.md §8d (KDLAE-T 512^2 static=train)
