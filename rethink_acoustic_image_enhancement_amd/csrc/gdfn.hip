@@ -1,0 +1,312 @@
+// Fused GDFN tail (KDLAE/KDLAE_model.py:101-106):
+//   out = x_res + project_out( gelu_erf(dw3x3(x1)) * dw3x3(x2) )
+// in ONE pass over the project_in output.  The gated hidden tensor (hid channels per pixel) never
+// reaches HBM: it is produced in registers in exactly the layout the MFMA B operand wants.
+//
+// Input layout (written by the project_in GEMM): per pixel 2*hidS floats, chunk-interleaved —
+// chunk g (16 hidden channels) occupies floats [32g, 32g+16) for x1 and [32g+16, 32g+32) for x2,
+// so one chunk of one pixel is a contiguous 128 B line.
+//
+// Block = 256 threads (4 waves, one workgroup per CU) on a 16 x 16 pixel tile; wave w owns tile
+// rows 4w..4w+3, lane l owns pixel column l & 15 and channel quad l >> 4.  Per hidden chunk g
+// (16 channels of x1 and the same 16 of x2):
+//   * LDS-DMA (global_load_lds, no VGPRs) brings the chunk's 18 x 18 halo tile (one 128 B line per
+//     pixel) and its depthwise weights + bias (2 KiB, repacked per chunk on the host) into a
+//     3-slot stage ring, and its project_out W fragments (NT x 1 KiB) into a 4-slot W ring.
+//     Iteration k issues chunk k+3, so chunks k+2 and k+3 are in flight while k+1 is gated and k
+//     is multiplied; waits are counted (vmcnt = one chunk's DMAs per wave) and barriers raw, so the
+//     in-flight chunks are never drained.  Nothing else in the loop reads global memory (an
+//     ordinary load would make hipcc drain the DMAs before its use);
+//   * the halo image is lane-linear [pixel][slot] with slot = quad ^ (pixel & 7) applied on the
+//     SOURCE address, so the column reads of the stencil are bank-conflict-free;
+//   * each lane computes the depthwise 3x3 + exact-erf gate for its 4 pixels (one per tile row) and
+//     4 channels — a float4 which IS its B operand for the chunk's 4 MFMA k-steps
+//     (B[k = 4(l>>4)+e][pixel l&15]); iteration g issues the MFMAs of chunk g in the same basic
+//     block as the gate VALU of chunk g+1, so the two overlap.
+// Epilogue: bias + residual, float4 stores of 4 consecutive output channels per lane.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <type_traits>
+
+#include "kernels.h"
+
+namespace kdlae {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kTile = 16;                          // output tile edge (pixels)
+constexpr int kHalo = kTile + 2;                   // 18
+constexpr int kHaloPx = kHalo * kHalo;             // 324
+constexpr int kStageItems = kHaloPx * 8;           // float4 items per chunk (x1 4 quads + x2 4 quads)
+constexpr int kStageF4 = 2624;                     // >= kStageItems; the last DMA round is wave 0's 64 lanes
+constexpr int kDwF4 = 128;                         // per-chunk dw block: [9][8] weights, [8] bias, pad
+constexpr int kNStage = 3;                         // stage ring (halo + dw block), read by gate(c) in iteration c-1
+constexpr int kNW = 4;                             // W ring, read by the MFMAs of chunk c in iteration c
+constexpr int kStageSlot = kStageF4 + kDwF4;       // 2752 float4
+
+// DMA rounds of the halo stage for WAVES waves (all waves issue rounds 0..R-2; round R-1 only wave 0)
+template <int WAVES> constexpr int stage_rounds() { return (kStageItems + 64 * WAVES - 1) / (64 * WAVES); }
+static_assert((stage_rounds<4>() - 1) * 256 + 64 == kStageF4, "stage layout (4 waves)");
+static_assert((stage_rounds<8>() - 1) * 512 + 64 == kStageF4, "stage layout (8 waves)");
+
+// DMA wave-instructions wave w issues per chunk: stage rounds, W records t with (t+1)%WAVES == w,
+// the 2 dw-block pieces on the last wave
+template <int NT, int WAVES> constexpr int dma_per_chunk(int w) {
+  int n = stage_rounds<WAVES>() - 1 + (w == 0 ? 1 : 0) + (w == WAVES - 1 ? 2 : 0);
+  for (int t = 0; t < NT; ++t) n += ((t + 1) % WAVES == w) ? 1 : 0;
+  return n;
+}
+
+// Exact-erf GELU, 0.5 x (1 + erf(x / sqrt 2)), with erf from Abramowitz & Stegun 7.1.26
+// (|error| <= 1.5e-7): branch-free, so the gate VALU stays in one basic block with the MFMAs it is
+// interleaved with.  The GELU error is <= 7.5e-8 |x|, at the level of fp32 rounding of the result.
+__device__ __forceinline__ float gelu_erf_g(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float poly = fmaf(1.061405429f, t, -1.453152027f);
+  poly = fmaf(poly, t, 1.421413741f);
+  poly = fmaf(poly, t, -0.284496736f);
+  poly = fmaf(poly, t, 0.254829592f);
+  poly *= t;
+  const float e = 1.0f - poly * __expf(-z * z);     // erf(|x| / sqrt 2)
+  return 0.5f * x * (1.0f + copysignf(e, x));
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// s_waitcnt with only a vmcnt limit (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt/lgkmcnt at max)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+__device__ __forceinline__ void dma16(const void* src, f32x4* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds_wave_base, 16, 0, 0);
+}
+
+}  // namespace
+
+template <int NT, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
+  constexpr int kThreads = 64 * WAVES, RPW = kTile / WAVES;   // tile rows per wave
+  constexpr int kRounds = stage_rounds<WAVES>();
+  extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+  f32x4* wring = lds + kNStage * kStageSlot;        // [kNW][NT][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: per-wave branches and LDS bases stay in SGPRs
+  const int cx = lane & 15, q = lane >> 4;
+  const int kch = p.hidS >> 4;
+
+  // XCD-aware tile order: logical tiles [k*per, (k+1)*per) run on XCD k, so tiles that share halo
+  // rows/columns share an L2.  The grid is padded to a multiple of 8.
+  const int tx_n = (p.W + kTile - 1) / kTile, ty_n = (p.H + kTile - 1) / kTile;
+  const int ntiles = p.Bn * tx_n * ty_n;
+  const int per = (int)(gridDim.x >> 3);
+  int bid = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (bid >= ntiles) return;
+  const int tx = bid % tx_n;
+  bid /= tx_n;
+  const int ty = bid % ty_n;
+  const int b = bid / ty_n;
+  const int x0 = tx * kTile, y0 = ty * kTile;
+  const long long HW = (long long)p.H * p.W;
+  const float* X = p.x + (long long)b * HW * p.ld;
+
+  // per-thread halo sources as 32-bit byte offsets into the image (chunk g adds 128 g bytes);
+  // out-of-image pixels and tail items read the zero line (offset ~0u)
+  unsigned srco[kRounds];
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const int it = tid + kThreads * j;
+    const int px = it >> 3, slot = it & 7, quad = slot ^ (px & 7);
+    const int hy = px / kHalo, hx = px - hy * kHalo;
+    const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+    const bool ok = it < kStageItems && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+    srco[j] = ok ? (unsigned)(((yy * p.W + xx) * p.ld + 4 * quad) * 4) : ~0u;
+  }
+  const char* Xb = reinterpret_cast<const char*>(X);
+  const f32x4* Wf = reinterpret_cast<const f32x4*>(p.Wp);
+  const f32x4* Dw = reinterpret_cast<const f32x4*>(p.dw);
+  auto issue = [&](int g) {
+    f32x4* sl = lds + (g % kNStage) * kStageSlot;
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      if (j == kRounds - 1 && wave != 0) break;
+      dma16(srco[j] != ~0u ? (const void*)(Xb + srco[j] + 128u * g) : (const void*)p.zeros,
+            sl + kThreads * j + 64 * wave);
+    }
+    if (wave == WAVES - 1) {
+      dma16(Dw + (size_t)g * kDwF4 + lane, sl + kStageF4);
+      dma16(Dw + (size_t)g * kDwF4 + 64 + lane, sl + kStageF4 + 64);
+    }
+    f32x4* wl = wring + (g % kNW) * (64 * NT);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      if ((t + 1) % WAVES == wave) dma16(Wf + ((size_t)t * kch + g) * 64 + lane, wl + 64 * t);
+  };
+  // wait until only the youngest chunk's DMAs are outstanding, then a raw barrier (a
+  // __syncthreads() would wait vmcnt(0) and drain the ring)
+  auto wait_chunks = [&](auto nchunks) {
+    constexpr int K = decltype(nchunks)::value;
+    switch (wave) {
+      case 0: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(0)>(); break;
+      case 1: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(1)>(); break;
+      case 2: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(2)>(); break;
+      case 3: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(3)>(); break;
+      case 4: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(4 % WAVES)>(); break;
+      case 5: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(5 % WAVES)>(); break;
+      case 6: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(6 % WAVES)>(); break;
+      default: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(7 % WAVES)>(); break;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // no LDS read may move above the barrier
+  };
+  auto wait_keep_one = [&]() { wait_chunks(std::integral_constant<int, 1>{}); };
+  auto wait_keep_two = [&]() { wait_chunks(std::integral_constant<int, 2>{}); };
+  auto wait_all = [&]() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // no LDS read may move above the barrier
+  };
+
+  f32x4 acc[RPW][NT];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // gate(g): depthwise 3x3 (rows 4w..4w+3, column cx, channels 16g+4q..+3 of x1 and x2) + gate
+  auto gate = [&](int g, f32x4 (&gb)[RPW]) {
+    const f32x4* sl = lds + (g % kNStage) * kStageSlot;
+    const f32x4* dw = sl + kStageF4;               // [9][8] then bias [8]
+    f32x4 d[2][RPW];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 bb = dw[72 + 4 * h + q];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) d[h][r] = bb;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        f32x4 wv[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) wv[i] = dw[(3 * i + j) * 8 + 4 * h + q];
+#pragma unroll
+        for (int rr = 0; rr < RPW + 2; ++rr) {
+          const int px = (RPW * wave + rr) * kHalo + cx + j;
+          const f32x4 v = sl[px * 8 + ((4 * h + q) ^ (px & 7))];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int r = rr - i;
+            if (r >= 0 && r < RPW) d[h][r] = v * wv[i] + d[h][r];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      gb[r].x = gelu_erf_g(d[0][r].x) * d[1][r].x;
+      gb[r].y = gelu_erf_g(d[0][r].y) * d[1][r].y;
+      gb[r].z = gelu_erf_g(d[0][r].z) * d[1][r].z;
+      gb[r].w = gelu_erf_g(d[0][r].w) * d[1][r].w;
+    }
+  };
+  auto mfma_chunk = [&](int g, const f32x4 (&gb)[RPW]) {
+    const f32x4* wl = wring + (g % kNW) * (64 * NT);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f32x4 w = wl[64 * t + lane];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        acc[r][t] = mfma4(w.x, gb[r].x, acc[r][t]);
+        acc[r][t] = mfma4(w.y, gb[r].y, acc[r][t]);
+        acc[r][t] = mfma4(w.z, gb[r].z, acc[r][t]);
+        acc[r][t] = mfma4(w.w, gb[r].w, acc[r][t]);
+      }
+    }
+  };
+
+  // prologue: chunks 0, 1, 2 in flight; gate(0) once chunk 0 has landed
+  f32x4 gb[RPW];
+  issue(0);
+  if (kch > 1) issue(1);
+  if (kch > 2) issue(2);
+  if (kch > 2) wait_keep_two();
+  else if (kch > 1) wait_keep_one();
+  else wait_all();
+  gate(0, gb);
+  for (int g = 0; g + 1 < kch; ++g) {
+    // issued so far: chunks 0..g+2.  gate(g+1) needs chunk g+1; chunk g+2 may stay in flight.
+    if (g + 2 < kch) wait_keep_one();
+    else wait_all();
+    // past this barrier every wave is done with gate(g) (stage slot g%3) and mfma(g-1) (W slot
+    // (g-1)%4 == (g+3)%4): chunk g+3 can reuse both
+    if (g + 3 < kch) issue(g + 3);
+    f32x4 gbn[RPW];
+    gate(g + 1, gbn);
+    mfma_chunk(g, gb);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) gb[r] = gbn[r];
+  }
+  mfma_chunk(kch - 1, gb);
+
+  // epilogue: lane holds output channels 16t + 4q .. +3 of pixel (y0 + 4w + r, x0 + cx)
+  const int xo = x0 + cx;
+  if (xo >= p.W) return;
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int yo = y0 + RPW * wave + r;
+    if (yo >= p.H) continue;
+    const long long pix = (long long)b * HW + (long long)yo * p.W + xo;
+    // all residual loads of the row first (R may alias out, so loads cannot pass earlier stores)
+    f32x4 res[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      res[t] = p.R ? *reinterpret_cast<const f32x4*>(p.R + pix * p.ldr + 16 * t + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int ch = 16 * t + 4 * q;
+      f32x4 v = acc[r][t] + res[t];
+      if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + ch);
+      *reinterpret_cast<f32x4*>(p.out + pix * p.ldo + ch) = v;
+    }
+  }
+}
+
+bool gdfn_supported(int C, int hidS) {
+  return (C == 48 || C == 96) && hidS % 16 == 0 && hidS <= 256;
+}
+
+size_t gdfn_lds_bytes(int C) { return (size_t)(kNStage * kStageSlot + kNW * 64 * (C / 16)) * sizeof(f32x4); }
+
+hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
+  if (!gdfn_supported(C, p.hidS) || p.ld != 2 * p.hidS || p.ldo % 4 || (p.R && p.ldr % 4) || !p.zeros)
+    return hipErrorInvalidValue;
+  const long long tiles = (long long)p.Bn * ((p.H + kTile - 1) / kTile) * ((p.W + kTile - 1) / kTile);
+  const long long grid = (tiles + 7) / 8 * 8;
+  const size_t lds = gdfn_lds_bytes(C);
+  static const int waves = getenv("KDLAE_GDFN_WAVES") ? atoi(getenv("KDLAE_GDFN_WAVES")) : 8;
+  const int threads = waves == 4 ? 256 : 512;
+  switch ((C / 16) * 10 + (waves == 4 ? 4 : 8)) {
+    case 34: hipLaunchKernelGGL((gdfn_out_kernel<3, 4>), dim3((unsigned)grid), dim3(threads), lds, s, p); break;
+    case 38: hipLaunchKernelGGL((gdfn_out_kernel<3, 8>), dim3((unsigned)grid), dim3(threads), lds, s, p); break;
+    case 64: hipLaunchKernelGGL((gdfn_out_kernel<6, 4>), dim3((unsigned)grid), dim3(threads), lds, s, p); break;
+    case 68: hipLaunchKernelGGL((gdfn_out_kernel<6, 8>), dim3((unsigned)grid), dim3(threads), lds, s, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kdlae

@@ -30,6 +30,7 @@ struct BlockW {
   Gemm qkv, pin, pout, proj_gemm;  // proj_gemm: geometry of the per-image M GEMM
   size_t dwqkv = kNone, dwqkv_b = kNone, proj = kNone, proj_b = kNone, temp = kNone;
   size_t dwffn = kNone, dwffn_b = kNone;
+  bool fused_gdfn = false;  // project_in output chunk-interleaved; dwconv+gate+project_out in one kernel
 };
 
 }  // namespace kdlae
@@ -49,6 +50,7 @@ struct kdlae_t_handle {
   std::vector<BlockW> enc1, enc2, enc3, latent, dec3, dec2, dec1, refinement, refinement_out, enhance;
   SmallW patch_embed, output, output_param, output2, cen, outputen;
   Gemm down1_2, down2_3, down3_4, up4_3, up3_2, up2_1, upen, reduce3, reduce2;
+  size_t zeros = kNone;  // 64 zero floats (halo source for the fused GDFN kernel)
   // probe
   int probe_class = 0, probe_level = 0;
   std::vector<hipEvent_t> ev;
@@ -304,14 +306,34 @@ struct Packer {
     b.proj_gemm.k_true = C;
     b.proj_gemm.bias = b.proj_b;
     choose_variant(b.proj_gemm, true);
-    // FFN: project_in rows [x1 (hid) | x2 (hid)] -> stored [x1 padded to hidS | x2 padded to hidS]
-    auto rmap = [hid, hidS](int n) -> int {
+    // FFN: project_in rows [x1 (hid) | x2 (hid)].  Unfused: stored [x1 padded to hidS | x2 padded
+    // to hidS] for the gate kernel.  Fused (gdfn.hip): chunk-interleaved, 16 channels of x1 then the
+    // same 16 of x2 per 32-channel chunk, so each chunk of a pixel is one 128 B line.
+    b.fused_gdfn = gdfn_supported(C, hidS) && !getenv("KDLAE_NO_GDFN_FUSION");
+    const bool fz = b.fused_gdfn;
+    auto rmap = [hid, hidS, fz](int n) -> int {
+      if (fz) {
+        const int c = 16 * (n >> 5) + (n & 15);
+        if (c >= hid) return -1;
+        return (n & 16) ? hid + c : c;
+      }
       if (n < hidS) return n < hid ? n : -1;
       const int m = n - hidS;
       return m < hid ? hid + m : -1;
     };
     b.pin = pointwise(p + ".ffn.project_in", 2 * hid, C, C, 2 * hidS, rmap, p + ".norm2", c.bias, true);
-    {
+    if (fz) {
+      // per 32-channel chunk: [9 taps][32] weights, [32] bias at +288, zero pad to 512 (gdfn.hip)
+      std::vector<float> v((size_t)(hidS / 16) * 512, 0.f);
+      for (int n = 0; n < 2 * hidS; ++n) {
+        const int src = rmap(n);
+        if (src < 0) continue;
+        float* blk = v.data() + (size_t)(n >> 5) * 512;
+        for (int t = 0; t < 9; ++t) blk[t * 32 + (n & 31)] = (*fw)[(size_t)src * 9 + t];
+        if (fb) blk[288 + (n & 31)] = (*fb)[src];
+      }
+      b.dwffn = arena.add(v);
+    } else {
       std::vector<float> v((size_t)9 * 2 * hidS, 0.f), vb((size_t)2 * hidS, 0.f);
       for (int n = 0; n < 2 * hidS; ++n) {
         const int src = rmap(n);
@@ -522,6 +544,29 @@ struct Fwd {
     View fpre{buf(pl.fpre), 2 * b.hidS};
     rc = gemm(b.pin, h->P(b.pin.w), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
     if (rc) return rc;
+    if (b.fused_gdfn) {
+      GdfnParams gd{};
+      gd.x = fpre.p;
+      gd.ld = fpre.ld;
+      gd.hidS = b.hidS;
+      gd.dw = h->P(b.dwffn);
+      gd.Wp = h->P(b.pout.w);
+      gd.bias = h->P(b.pout.bias);
+      gd.R = x.p;
+      gd.ldr = x.ld;
+      gd.out = x.p;
+      gd.ldo = x.ld;
+      gd.Bn = B;
+      gd.H = Hh;
+      gd.W = Ww;
+      gd.zeros = h->P(h->zeros);
+      if ((rc = probe_begin(3, b.C))) return rc;
+      tag = "gdfn C" + std::to_string(b.C) + " hid" + std::to_string(b.hid) + " HW" + std::to_string(HW);
+      HIPCHK(launch_gdfn_out(gd, b.C, s));
+      // algorithmic: read x1|x2 (2 hid) + residual (C), write C; dwconv + gate + project_out FLOPs
+      return probe_end(3, b.C, 4.0 * P * (2.0 * b.hid + 2.0 * b.C),
+                       2.0 * P * (18.0 * b.hid + (double)b.hid * b.C));
+    }
     GateParams ga{};
     ga.x = fpre.p;
     ga.ld = fpre.ld;
@@ -714,6 +759,7 @@ int kdlae_t_commit_params(kdlae_t_handle* h, void* stream) {
   HIPCHK(hipSetDevice(h->device));
   const kdlae_t_config& c = h->cfg;
   Packer pk{h};
+  h->zeros = pk.arena.add(std::vector<float>(64, 0.f));
   const int d = c.dim;
   const int* nb = c.num_blocks;
   const int* hd = c.heads;

@@ -98,6 +98,22 @@ hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s);
 hipError_t launch_maxpool2(const float* in, int ldi, float* out, int ldo, int C, long long nframes, int H, int W,
                            hipStream_t s);
 
+// Fused GDFN tail: out = R + project_out(gelu_erf(dw3x3(x1)) * dw3x3(x2)) (gdfn.hip).
+struct GdfnParams {
+  const float* x; int ld;          // project_in output, chunk-interleaved [g][x1 16 | x2 16] per pixel
+  int hidS;                        // padded hidden width (multiple of 16)
+  const float* dw;                 // per chunk g (hidS/16 of them) 512 floats: [9 taps][32 ch] weights,
+                                   // [32] bias at +288, zero pad (channel order as in x)
+  const float* Wp;                 // project_out fragments [C/16][hidS/16][64][4]
+  const float* bias;               // [C] or null
+  const float* R; int ldr;         // residual (may alias out) or null
+  float* out; int ldo;
+  int Bn, H, W;
+  const float* zeros;              // >= 16 B of zeros in device memory (source of out-of-image halo lines)
+};
+bool gdfn_supported(int C, int hidS);
+hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s);
+
 // Bilinear x2, align_corners=True (ASDQE_model.py:53): NHWC [N][h][w][C] -> [N][2h][2w][C] into a
 // strided destination (a concat half).  C % 4 == 0.
 hipError_t launch_upsample2x(const float* in, int ldi, float* out, int ldo, int C, int N, int h, int w,
