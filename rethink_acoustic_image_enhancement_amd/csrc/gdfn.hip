@@ -47,15 +47,16 @@ constexpr int kNStage = 3;                         // stage ring (halo + dw bloc
 constexpr int kNW = 4;                             // W ring, read by the MFMAs of chunk c in iteration c
 constexpr int kStageSlot = kStageF4 + kDwF4;       // 2752 float4
 
-// DMA rounds of the halo stage for WAVES waves (all waves issue rounds 0..R-2; round R-1 only wave 0)
-template <int WAVES> constexpr int stage_rounds() { return (kStageItems + 64 * WAVES - 1) / (64 * WAVES); }
-static_assert((stage_rounds<4>() - 1) * 256 + 64 == kStageF4, "stage layout (4 waves)");
-static_assert((stage_rounds<8>() - 1) * 512 + 64 == kStageF4, "stage layout (8 waves)");
+// The halo stage is kStagePieces lane-linear 1 KiB DMA wave-instructions (piece k -> items
+// 64k..64k+63), dealt round-robin: wave w issues pieces w, w + WAVES, ...
+constexpr int kStagePieces = (kStageItems + 63) / 64;  // 41
+static_assert(kStagePieces * 64 == kStageF4, "stage layout");
+template <int WAVES> constexpr int stage_pieces(int w) { return (kStagePieces - w + WAVES - 1) / WAVES; }
 
-// DMA wave-instructions wave w issues per chunk: stage rounds, W records t with (t+1)%WAVES == w,
-// the 2 dw-block pieces on the last wave
+// DMA wave-instructions wave w issues per chunk: its stage pieces, W records t with
+// (t+1)%WAVES == w, the 2 dw-block pieces on the last wave
 template <int NT, int WAVES> constexpr int dma_per_chunk(int w) {
-  int n = stage_rounds<WAVES>() - 1 + (w == 0 ? 1 : 0) + (w == WAVES - 1 ? 2 : 0);
+  int n = stage_pieces<WAVES>(w) + (w == WAVES - 1 ? 2 : 0);
   for (int t = 0; t < NT; ++t) n += ((t + 1) % WAVES == w) ? 1 : 0;
   return n;
 }
@@ -97,8 +98,8 @@ __device__ __forceinline__ void dma16(const void* src, f32x4* lds_wave_base) {
 
 template <int NT, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
-  constexpr int kThreads = 64 * WAVES, RPW = kTile / WAVES;   // tile rows per wave
-  constexpr int kRounds = stage_rounds<WAVES>();
+  constexpr int RPW = kTile / WAVES;                           // tile rows per wave
+  constexpr int kRounds = (kStagePieces + WAVES - 1) / WAVES;  // stage pieces per wave (max)
   extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
   f32x4* wring = lds + kNStage * kStageSlot;        // [kNW][NT][64]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
   unsigned srco[kRounds];
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
-    const int it = tid + kThreads * j;
+    const int it = (wave + WAVES * j) * 64 + lane;
     const int px = it >> 3, slot = it & 7, quad = slot ^ (px & 7);
     const int hy = px / kHalo, hx = px - hy * kHalo;
     const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
@@ -140,9 +141,9 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
     f32x4* sl = lds + (g % kNStage) * kStageSlot;
 #pragma unroll
     for (int j = 0; j < kRounds; ++j) {
-      if (j == kRounds - 1 && wave != 0) break;
-      dma16(srco[j] != ~0u ? (const void*)(Xb + srco[j] + 128u * g) : (const void*)p.zeros,
-            sl + kThreads * j + 64 * wave);
+      const int k = wave + WAVES * j;
+      if (k >= kStagePieces) break;
+      dma16(srco[j] != ~0u ? (const void*)(Xb + srco[j] + 128u * g) : (const void*)p.zeros, sl + 64 * k);
     }
     if (wave == WAVES - 1) {
       dma16(Dw + (size_t)g * kDwF4 + lane, sl + kStageF4);
@@ -158,14 +159,22 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
   auto wait_chunks = [&](auto nchunks) {
     constexpr int K = decltype(nchunks)::value;
     switch (wave) {
-      case 0: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(0)>(); break;
-      case 1: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(1)>(); break;
-      case 2: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(2)>(); break;
-      case 3: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(3)>(); break;
+      case 0: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(0 % WAVES)>(); break;
+      case 1: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(1 % WAVES)>(); break;
+      case 2: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(2 % WAVES)>(); break;
+      case 3: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(3 % WAVES)>(); break;
       case 4: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(4 % WAVES)>(); break;
       case 5: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(5 % WAVES)>(); break;
       case 6: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(6 % WAVES)>(); break;
-      default: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(7 % WAVES)>(); break;
+      case 7: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(7 % WAVES)>(); break;
+      case 8: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(8 % WAVES)>(); break;
+      case 9: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(9 % WAVES)>(); break;
+      case 10: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(10 % WAVES)>(); break;
+      case 11: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(11 % WAVES)>(); break;
+      case 12: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(12 % WAVES)>(); break;
+      case 13: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(13 % WAVES)>(); break;
+      case 14: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(14 % WAVES)>(); break;
+      default: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(15 % WAVES)>(); break;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -298,12 +307,14 @@ hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
   const long long grid = (tiles + 7) / 8 * 8;
   const size_t lds = gdfn_lds_bytes(C);
   static const int waves = getenv("KDLAE_GDFN_WAVES") ? atoi(getenv("KDLAE_GDFN_WAVES")) : 8;
-  const int threads = waves == 4 ? 256 : 512;
-  switch ((C / 16) * 10 + (waves == 4 ? 4 : 8)) {
-    case 34: hipLaunchKernelGGL((gdfn_out_kernel<3, 4>), dim3((unsigned)grid), dim3(threads), lds, s, p); break;
-    case 38: hipLaunchKernelGGL((gdfn_out_kernel<3, 8>), dim3((unsigned)grid), dim3(threads), lds, s, p); break;
-    case 64: hipLaunchKernelGGL((gdfn_out_kernel<6, 4>), dim3((unsigned)grid), dim3(threads), lds, s, p); break;
-    case 68: hipLaunchKernelGGL((gdfn_out_kernel<6, 8>), dim3((unsigned)grid), dim3(threads), lds, s, p); break;
+  const int w = (waves == 4 || waves == 16) ? waves : 8;
+  switch ((C / 16) * 100 + w) {
+    case 304: hipLaunchKernelGGL((gdfn_out_kernel<3, 4>), dim3((unsigned)grid), dim3(256), lds, s, p); break;
+    case 308: hipLaunchKernelGGL((gdfn_out_kernel<3, 8>), dim3((unsigned)grid), dim3(512), lds, s, p); break;
+    case 316: hipLaunchKernelGGL((gdfn_out_kernel<3, 16>), dim3((unsigned)grid), dim3(1024), lds, s, p); break;
+    case 604: hipLaunchKernelGGL((gdfn_out_kernel<6, 4>), dim3((unsigned)grid), dim3(256), lds, s, p); break;
+    case 608: hipLaunchKernelGGL((gdfn_out_kernel<6, 8>), dim3((unsigned)grid), dim3(512), lds, s, p); break;
+    case 616: hipLaunchKernelGGL((gdfn_out_kernel<6, 16>), dim3((unsigned)grid), dim3(1024), lds, s, p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
