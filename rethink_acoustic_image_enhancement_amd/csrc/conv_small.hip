@@ -13,10 +13,12 @@ namespace kdlae {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// thread = (16-channel output group, pixel); all lanes of a wave share the group -> LDS broadcast
+// thread = (16-channel output group, pixel); all lanes of a wave share the group -> LDS broadcast.
+// KT (temporal taps, 1 or 3) is a template parameter so the unrolled tap indexing folds to constants.
+template <int KT>
 __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
   extern __shared__ float wsm[];  // [Cout][36] (ci-major then taps, zero past Cin*kt*9) then bias[Cout]
-  const int taps = 9 * p.kt;
+  constexpr int taps = 9 * KT;
   const int vh = p.vh ? p.vh : p.H, vw = p.vw ? p.vw : p.W;
   const int nw = p.Cout * 36;
   for (int i = threadIdx.x; i < nw; i += 256) {
@@ -43,7 +45,7 @@ __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
     for (int k = 0; k < 36; ++k) {
       const int ci = k / taps, tap = k - (k / taps) * taps;  // taps = 9 (2-D) or 27 (3-D)
       const int t9 = tap % 9;
-      const int tt = t0 + (p.kt == 3 ? tap / 9 - 1 : 0);
+      const int tt = t0 + (KT == 3 ? tap / 9 - 1 : 0);
       const int yy = y + (t9 / 3 - 1) * p.dil, xx = x + (t9 % 3 - 1) * p.dil;
       const bool ok = ci < p.Cin && (unsigned)tt < (unsigned)p.F && (unsigned)yy < (unsigned)vh &&
                       (unsigned)xx < (unsigned)vw;
@@ -71,12 +73,15 @@ __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
 }
 
 hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s) {
-  if (p.Cin * 9 * p.kt > 36 || p.Cout % 16) return hipErrorInvalidValue;
+  if (p.Cin * 9 * p.kt > 36 || p.Cout % 16 || (p.kt != 1 && p.kt != 3)) return hipErrorInvalidValue;
   const long long total = (long long)p.Bn * p.F * p.H * p.W * (p.Cout / 16);
   long long blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   const size_t lds = (size_t)(p.Cout * 36 + p.Cout) * sizeof(float);
-  hipLaunchKernelGGL(conv_small_in_kernel, dim3((unsigned)blocks), dim3(256), lds, s, p);
+  if (p.kt == 3)
+    hipLaunchKernelGGL(conv_small_in_kernel<3>, dim3((unsigned)blocks), dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL(conv_small_in_kernel<1>, dim3((unsigned)blocks), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
@@ -141,8 +146,115 @@ __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
   }
 }
 
+// 3x3 / Cout <= 4 / single-frame head conv, LDS-tiled: a 256-thread block owns a 16 x 32 output tile,
+// thread = (column, pair of rows).  The 18 x 34 input halo is staged 16 channels at a time in
+// quad-planar LDS ([4 quads][612 px], conflict-free column reads), the next chunk's global loads are
+// in flight in registers meanwhile; weights sit in LDS as float4 (4 outputs) per (tap, channel).
+// Each input element is read from HBM ~1.1x instead of 9x through L2.
+constexpr int kSoTW = 16, kSoTH = 32, kSoHW = kSoTW + 2, kSoHH = kSoTH + 2, kSoPx = kSoHW * kSoHH;  // 612
+constexpr int kSoItems = kSoPx * 4;                                   // float4 per 16-channel chunk
+constexpr int kSoPer = (kSoItems + 255) / 256;                         // 10 per thread
+
+__global__ __launch_bounds__(256) void conv_small_out_tiled_kernel(SmallOutParams p) {
+  __shared__ f32x4 st[4][kSoPx];
+  extern __shared__ __attribute__((aligned(16))) f32x4 wq[];           // [9][Cin] (4 outputs each)
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 9 * p.Cin; i += 256) {
+    const int t = i / p.Cin, ci = i - t * p.Cin;
+    f32x4 w4;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) w4[o] = o < p.Cout ? p.w[(o * p.Cin + ci) * 9 + t] : 0.f;
+    wq[i] = w4;
+  }
+  const int tx_n = (p.W + kSoTW - 1) / kSoTW, ty_n = (p.H + kSoTH - 1) / kSoTH;
+  int bid = blockIdx.x;
+  const int tx = bid % tx_n;
+  bid /= tx_n;
+  const int ty = bid % ty_n;
+  const int b = bid / ty_n;
+  const int x0 = tx * kSoTW, y0 = ty * kSoTH;
+  const long long HW = (long long)p.H * p.W;
+  const float* X = p.in + (long long)b * HW * p.ld;
+  const int cx = tid & 15, r0 = 2 * (tid >> 4);                       // rows r0, r0 + 1 of the tile
+  f32x4 pf[kSoPer];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < kSoPer; ++j) {
+      const int it = tid + 256 * j;
+      const int px = it >> 2, q = it & 3;
+      const int hy = px / kSoHW, hx = px - hy * kSoHW;
+      const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+      const bool ok = it < kSoItems && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(X + (ok ? ((long long)yy * p.W + xx) * p.ld + c0 + 4 * q : 0));
+      pf[j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int j = 0; j < kSoPer; ++j) {
+      const int it = tid + 256 * j;
+      if (it < kSoItems) st[it & 3][it >> 2] = pf[j];
+    }
+  };
+  f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  fetch(0);
+  for (int c0 = 0; c0 < p.Cin; c0 += 16) {
+    __syncthreads();                                                   // previous chunk consumed
+    put();
+    __syncthreads();
+    if (c0 + 16 < p.Cin) fetch(c0 + 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        f32x4 v[4];                                                    // halo rows r0 .. r0 + 3
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) v[rr] = st[q][(r0 + rr) * kSoHW + cx + kx];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const f32x4* w = wq + (ky * 3 + kx) * p.Cin + c0 + 4 * q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f32x4 w4 = w[e];
+            a0 += v[ky][e] * w4;
+            a1 += v[ky + 1][e] * w4;
+          }
+        }
+      }
+    }
+  }
+  const int xo = x0 + cx;
+  if (xo >= p.W) return;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int yo = y0 + r0 + k;
+    if (yo >= p.H) continue;
+    const f32x4 acc = k ? a1 : a0;
+    const long long pl = (long long)yo * p.W + xo, pix = (long long)b * HW + pl;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      if (o >= p.Cout) break;
+      float v = acc[o] + (p.bias ? p.bias[o] : 0.f);
+      if (p.out_nchw) {
+        const long long oi = ((long long)b * p.Cout + o) * HW + pl;
+        if (p.res) v += p.res[oi];
+        p.out[oi] = v;
+      } else {
+        p.out[pix * p.ldo + o] = v;
+      }
+    }
+    if (!p.out_nchw && p.extra) p.out[pix * p.ldo + p.Cout] = p.extra[pix];
+  }
+}
+
 hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s) {
   if (p.Cin % 16 || (p.ks != 1 && p.ks != 3)) return hipErrorInvalidValue;
+  if (p.ks == 3 && p.F == 1 && p.ld % 4 == 0 && p.Cin <= 256) {
+    const long long blocks = (long long)p.Bn * ((p.H + kSoTH - 1) / kSoTH) * ((p.W + kSoTW - 1) / kSoTW);
+    const size_t lds = (size_t)9 * p.Cin * sizeof(f32x4);
+    hipLaunchKernelGGL(conv_small_out_tiled_kernel, dim3((unsigned)blocks), dim3(256), lds, s, p);
+    return hipGetLastError();
+  }
   const long long P = (long long)p.Bn * p.F * p.H * p.W;
   long long blocks = (P + 63) / 64;
   if (blocks > 16384) blocks = 16384;
