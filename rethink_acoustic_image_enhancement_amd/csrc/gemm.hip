@@ -158,27 +158,67 @@ __device__ __forceinline__ void mfma_chunk(const f32x4* __restrict__ wl, int ldk
   }
 }
 
-template <int NT, int OUT>
+template <int NT, int OUT, bool HASR>
 __device__ __forceinline__ void epilogue(const GemmParams& p, int b, int row0, int nt0, int tmax, int li, int lq,
-                                         int HW, f32x4 (&acc)[NT][kGemmRT]) {
+                                         int HW, f32x4 (&acc)[NT][kGemmRT], const f32x4* bl) {
+  // bl: this n-chunk's bias in LDS, 4 float4 per output tile (zeros when the layer has none).
+  // vmcnt retires in order, so waiting for a global load issued after a store also drains that
+  // store.  The residual of tile t+1 is therefore loaded before tile t is stored (one tile ahead),
+  // and the bias comes from LDS: no load ever waits behind the store it follows.
   const float* __restrict__ Rb = p.R ? p.R + (long long)b * HW * p.ldr : nullptr;
   float* __restrict__ Ob = p.out + (OUT == 0 ? (long long)b * HW * p.ldo : 0);
+  if constexpr (OUT == 0) {
+    // residual loads are unconditional (addresses clamped in bounds, value selected after) so the
+    // epilogue stays one basic block and the compiler can count vmcnt exactly
+    auto load_res = [&](int t, f32x4 (&rv)[kGemmRT]) {
+      const int nq = (nt0 + t) * 16 + 4 * lq;
+      const bool tok = t < tmax && nq < p.N;
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r) {
+        const int pl = row0 + r * 16 + li;
+        const bool ok = tok && pl < HW;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(Rb + (ok ? pl * p.ldr + nq : 0));
+        rv[r] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    [[maybe_unused]] f32x4 rc[kGemmRT], rn[kGemmRT];
+    if constexpr (HASR) load_res(0, rc);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if constexpr (HASR) {
+        if (t + 1 < NT) load_res(t + 1, rn);
+      }
+      const int nq = (nt0 + t) * 16 + 4 * lq;
+      if (t < tmax && nq < p.N) {
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) {
+          const int pl = row0 + r * 16 + li;
+          if (pl >= HW) continue;
+          f32x4 v = acc[t][r] + bl[4 * t + lq];
+          if constexpr (HASR) v += rc[r];
+          if (p.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+          *reinterpret_cast<f32x4*>(Ob + pl * p.ldo + nq) = v;
+        }
+      }
+      if constexpr (HASR) {
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) rc[r] = rn[r];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int n0 = (nt0 + t) * 16;
     if (t >= tmax || n0 >= p.N) continue;
     const int nq = n0 + 4 * lq;
-    const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + nq) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 bias = bl[4 * t + lq];
 #pragma unroll
     for (int r = 0; r < kGemmRT; ++r) {
       const int pl = row0 + r * 16 + li;
       if (pl >= HW) continue;
       f32x4 v = acc[t][r] + bias;
-      if (OUT == 0) {
-        if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + pl * p.ldr + nq);
-        if (p.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
-        *reinterpret_cast<f32x4*>(Ob + pl * p.ldo + nq) = v;
-      } else {
+      {
         const int fhw = p.H * p.W;
         const int t = pl / fhw;
         const int rem = pl - t * fhw;
@@ -244,6 +284,12 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
         const int n4pad = ((gtiles + NT - 1) / NT) * NT * p.kgroups * 64;  // partial last chunk reads zeros
         for (int idx = tid; idx < n4pad; idx += kGemmThreads)
           wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+        const int nb4 = ((gtiles + NT - 1) / NT) * NT * 4;                  // bias of the group's tiles
+        for (int idx = tid; idx < nb4; idx += kGemmThreads) {
+          const int n = g0 * 16 + 4 * idx;
+          wlds[n4pad + idx] = (p.bias && idx < gtiles * 4 && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n)
+                                                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
         __syncthreads();
         staged = wkey;
       }
@@ -269,7 +315,9 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
 #pragma unroll
           for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
         mfma_chunk<NT, KG>(wlds + (size_t)c0 * p.kgroups * 64, p.kgroups, lane, a, acc);
-        epilogue<NT, OUT>(p, b, row0, g0 + c0, gtiles - c0, li, lq, HW, acc);
+        const f32x4* bl = wlds + ((gtiles + NT - 1) / NT) * NT * p.kgroups * 64 + c0 * 4;
+        if (p.R) epilogue<NT, OUT, true>(p, b, row0, g0 + c0, gtiles - c0, li, lq, HW, acc, bl);
+        else epilogue<NT, OUT, false>(p, b, row0, g0 + c0, gtiles - c0, li, lq, HW, acc, bl);
       }
     }
   } else {
@@ -298,13 +346,20 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
             v = *reinterpret_cast<const f32x4*>(wbase + ((long long)(gt * p.kgroups + gg) * 64 + l) * 4);
           wlds[idx] = v;
         }
+        if (kc == 0)
+          for (int idx = tid; idx < NT * 4; idx += kGemmThreads) {  // bias of the block's NT tiles
+            const int n = nc * NT * 16 + 4 * idx;
+            wlds[NT * KG * 64 + idx] =
+                (p.bias && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
         __syncthreads();
         f32x4 a[kGemmRT][KG];
         load_a<KG, CONV3>(p, Ab, row0, kc, li, lq, HW, a);
         if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
         mfma_chunk<NT, KG>(wlds, KG, lane, a, acc);
       }
-      epilogue<NT, OUT>(p, b, row0, nc * NT, NT, li, lq, HW, acc);
+      if (p.R) epilogue<NT, OUT, true>(p, b, row0, nc * NT, NT, li, lq, HW, acc, wlds + NT * KG * 64);
+      else epilogue<NT, OUT, false>(p, b, row0, nc * NT, NT, li, lq, HW, acc, wlds + NT * KG * 64);
     }
   }
 }
@@ -358,13 +413,15 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
   if (p.out_mode == 0 && (p.N % 16)) return hipErrorInvalidValue;  // plain stores are whole 16-channel tiles
   int grid_y;
   size_t lds;
+  // LDS: packed weights, then the bias of the same output tiles (64 B per tile)
   if (res) {
     if (p.kgroups != KG || p.kchunks != 1) return hipErrorInvalidValue;
     grid_y = (p.ntiles + p.group_tiles - 1) / p.group_tiles;
-    lds = (size_t)((p.group_tiles + NT - 1) / NT) * NT * p.kgroups * 1024;
+    const size_t tiles_pad = (size_t)((p.group_tiles + NT - 1) / NT) * NT;
+    lds = tiles_pad * p.kgroups * 1024 + tiles_pad * 64;
   } else {
     grid_y = (p.ntiles + NT - 1) / NT;
-    lds = (size_t)NT * KG * 1024;
+    lds = (size_t)NT * KG * 1024 + (size_t)NT * 64;
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
 #define X(a, b, c, o, f, w, r)                                                                 \
