@@ -158,6 +158,30 @@ int64_t asdqe_workspace_bytes(const asdqe_handle* h, int B, int H, int W);
 int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int H, int W, float* score,
                   float* feat, void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------ pre/post-processing
+ * The steps either side of the forward in KDLAE/KDLAE_T.ipynb (load_image_as_tensor, reflect pad,
+ * denoise_rate map; clamp, crop, img_as_ubyte, zero-mask of black input pixels) and ASDQE's
+ * ToTensor, on device buffers.
+ */
+#include <stdint.h>
+
+/* (H, W) the notebook pads (h, w) to: ((h + m) / m) * m when h % m != 0, else h (same for w). */
+void kdlae_padded_size(int h, int w, int multiple, int* H, int* W);
+
+/* images u8 [B, h, w, channels] (channels 1, 3 or 4; alpha dropped; bgr != 0 swaps B and R like
+ * cv2.cvtColor(BGR2RGB)) -> img f32 [B, min(channels, 3), H, W] = x / 255, reflect-padded on the
+ * bottom/right to kdlae_padded_size(h, w, multiple) (multiple 1 = no padding: ASDQE ToTensor).
+ * rate f32 [B] (nullable) -> rate_map f32 [B, 1, H, W] (nullable): the constant denoise_rate map. */
+int kdlae_preprocess_u8(const uint8_t* images, int B, int h, int w, int channels, int bgr, int multiple,
+                        const float* rate, float* img, float* rate_map, void* stream);
+
+/* out f32 [B, C, Hs, Ws] (model output, C <= 4) -> dst u8 [B, h*scale, w*scale, C]:
+ * clamp(0, 1), crop, rint(x * 255) (skimage img_as_ubyte), and 0 where the input pixel
+ * lq u8 [B, h, w, lq_channels] (nullable) is black in every colour channel; scale 2 maps each
+ * output pixel to its nearest input pixel (the notebook's np.repeat x2 mask for sr). */
+int kdlae_postprocess_u8(const float* out, int B, int C, int Hs, int Ws, int h, int w, int scale,
+                         const uint8_t* lq, int lq_channels, uint8_t* dst, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,6 +28,7 @@ EXPORTS = (
     "kdlae_s_set_param", "kdlae_s_commit_params", "kdlae_s_workspace_bytes", "kdlae_s_forward",
     "asdqe_create", "asdqe_destroy", "asdqe_num_params", "asdqe_param_info", "asdqe_set_param",
     "asdqe_commit_params", "asdqe_workspace_bytes", "asdqe_forward",
+    "kdlae_padded_size", "kdlae_preprocess_u8", "kdlae_postprocess_u8",
 )
 
 
@@ -105,8 +106,14 @@ def lib() -> ctypes.CDLL:
     L.asdqe_workspace_bytes.restype = c_int64
     L.asdqe_forward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                 c_int64, c_void_p]
+    L.kdlae_padded_size.argtypes = [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
+    L.kdlae_padded_size.restype = None
+    L.kdlae_preprocess_u8.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                      c_void_p, c_void_p]
+    L.kdlae_postprocess_u8.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                       c_void_p, c_void_p]
     for name in EXPORTS:
-        if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes")):
+        if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes", "_padded_size")):
             getattr(L, name).restype = c_int
     _lib = L
     return L

@@ -11,6 +11,8 @@
 // v_mfma_f32_16x16x4_f32 consumes over four k-steps, so a wave reads it as one contiguous 1 KiB.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <cstdint>
 #include <stdint.h>
 
 namespace kdlae {
@@ -113,6 +115,22 @@ struct GdfnParams {
 };
 bool gdfn_supported(int C, int hidS);
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s);
+
+// Pre/post-processing around the forward (pipeline.hip)
+struct PreParams {
+  const uint8_t* in; int B, h, w, cin, cout, bgr;  // u8 [B][h][w][cin]
+  int H, W;                                          // padded size (reflect, bottom/right)
+  float* img;                                        // f32 [B][cout][H][W]
+  const float* rate; float* rate_map;                // per-image rate [B] -> [B][1][H][W] (optional)
+};
+struct PostParams {
+  const float* src; int B, C, Hs, Ws;                // f32 [B][C][Hs][Ws] (model output)
+  int h, w, scale;                                   // crop (h*scale, w*scale) of the output
+  const uint8_t* lq; int cin;                        // u8 [B][h][w][cin] input for the black mask (optional)
+  uint8_t* out;                                      // u8 [B][h*scale][w*scale][C]
+};
+hipError_t launch_preprocess_u8(const PreParams& p, hipStream_t s);
+hipError_t launch_postprocess_u8(const PostParams& p, hipStream_t s);
 
 // Bilinear x2, align_corners=True (ASDQE_model.py:53): NHWC [N][h][w][C] -> [N][2h][2w][C] into a
 // strided destination (a concat half).  C % 4 == 0.
