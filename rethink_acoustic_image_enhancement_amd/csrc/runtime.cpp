@@ -44,11 +44,13 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
       for (int nt : nts) {
         if (!gemm_has_variant(nt, g.kgroups, false, w, true, g.out_mode)) continue;
         const long long padded = ceil_div(gt, nt) * nt;
-        if (padded * g.kgroups > budget_kb + 8) continue;
-        // default policy: 4 waves/SIMD only for the store-heavy K <= 48 shapes
+        // weights (1 KiB per tile x k-group) + the group's bias (64 B per tile) must fit 160 KiB
+        if (padded * g.kgroups + ceil_div(padded, 16) > (w == 4 ? 80 : 158)) continue;
+        // default policy: 2 waves/SIMD.  4 waves/SIMD used to win on the store-heavy K <= 48 shapes
+        // while every epilogue load drained the stores; with that fixed, 2 waves measure 10-15%
+        // faster on all of them (r01 probe: C48 project_in @1024^2 5864 -> 5099 us)
         double cost = (double)padded / gt + 0.01 * (12 - nt) + (ngroups - 1) * 0.05;
-        if (!forced_wpe() && w == 4 && g.kgroups > 3) cost += 1.0;
-        if (!forced_wpe() && w == 2 && g.kgroups <= 3) cost += 0.5;
+        if (!forced_wpe() && w == 4) cost += 1.0;
         if (cost < best) {
           best = cost;
           best_nt = nt;
