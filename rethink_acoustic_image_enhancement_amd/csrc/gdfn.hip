@@ -234,15 +234,17 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
   };
   auto mfma_chunk = [&](int g, const f32x4 (&gb)[RPW]) {
     const f32x4* wl = wring + (g % kNW) * (64 * NT);
+    f32x4 w[NT];                                   // every W fragment first: one LDS wait per chunk
+#pragma unroll
+    for (int t = 0; t < NT; ++t) w[t] = wl[64 * t + lane];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const f32x4 w = wl[64 * t + lane];
 #pragma unroll
       for (int r = 0; r < RPW; ++r) {
-        acc[r][t] = mfma4(w.x, gb[r].x, acc[r][t]);
-        acc[r][t] = mfma4(w.y, gb[r].y, acc[r][t]);
-        acc[r][t] = mfma4(w.z, gb[r].z, acc[r][t]);
-        acc[r][t] = mfma4(w.w, gb[r].w, acc[r][t]);
+        acc[r][t] = mfma4(w[t].x, gb[r].x, acc[r][t]);
+        acc[r][t] = mfma4(w[t].y, gb[r].y, acc[r][t]);
+        acc[r][t] = mfma4(w[t].z, gb[r].z, acc[r][t]);
+        acc[r][t] = mfma4(w[t].w, gb[r].w, acc[r][t]);
       }
     }
   };
@@ -272,25 +274,30 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
   mfma_chunk(kch - 1, gb);
 
   // epilogue: lane holds output channels 16t + 4q .. +3 of pixel (y0 + 4w + r, x0 + cx)
+  // All loads (bias, every row's residual; clamped rows, unconditional) before the first store: vmcnt
+  // retires in order, so a load issued after a store would make its wait drain that store.
   const int xo = x0 + cx;
   if (xo >= p.W) return;
+  f32x4 bias[NT], res[RPW][NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    bias[t] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + 16 * t + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int yo = min(y0 + RPW * wave + r, p.H - 1);
+    const long long pix = (long long)b * HW + (long long)yo * p.W + xo;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      res[r][t] = p.R ? *reinterpret_cast<const f32x4*>(p.R + pix * p.ldr + 16 * t + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int yo = y0 + RPW * wave + r;
     if (yo >= p.H) continue;
     const long long pix = (long long)b * HW + (long long)yo * p.W + xo;
-    // all residual loads of the row first (R may alias out, so loads cannot pass earlier stores)
-    f32x4 res[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
-      res[t] = p.R ? *reinterpret_cast<const f32x4*>(p.R + pix * p.ldr + 16 * t + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int ch = 16 * t + 4 * q;
-      f32x4 v = acc[r][t] + res[t];
-      if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + ch);
-      *reinterpret_cast<f32x4*>(p.out + pix * p.ldo + ch) = v;
-    }
+      *reinterpret_cast<f32x4*>(p.out + pix * p.ldo + 16 * t + 4 * q) = acc[r][t] + res[r][t] + bias[t];
   }
 }
 
