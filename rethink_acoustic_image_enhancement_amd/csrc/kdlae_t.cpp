@@ -529,6 +529,7 @@ struct Fwd {
     gp.H = Hh;
     gp.W = Ww;
     gp.nslots = nslots_for(Hh, Ww, B, b.heads);
+    gp.zeros = getenv("KDLAE_NO_GRAM_RING") ? nullptr : h->P(h->zeros);
     const int CT = b.Ch / 16;
     gp.slot_floats = CT * CT * 256 + 2 * b.Ch;
     if ((rc = probe_begin(2, b.C))) return rc;

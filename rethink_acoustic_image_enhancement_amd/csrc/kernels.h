@@ -52,6 +52,7 @@ struct GramParams {
   int C, heads, Ch;
   int Bn, H, W;
   int nslots, slot_floats;
+  const float* zeros;              // >= 16 zero floats (DMA source for padding); null -> no ring kernel
 };
 
 struct GateParams {

@@ -13,7 +13,10 @@
 //   3. attn_fold: A = softmax(G / (max(|q|,eps) max(|k|,eps)) * temp); M = W_proj . blockdiag(A)
 //      written directly in the packed GEMM fragment order, so "A v then project_out" is ONE GEMM
 //      (conv_gemm with per-image weights M and the residual add in its epilogue).
+#include <type_traits>
+
 #include "kernels.h"
+#include "lds_dma.h"
 
 namespace kdlae {
 
@@ -339,8 +342,244 @@ __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(
   for (int idx = threadIdx.x; idx < 2 * Ch; idx += 64 * NW) out[CT * CT * 256 + idx] = nred[idx];
 }
 
+// DMA-ring row sweep (same blocking as the sweep kernel: 16-column strip x row segment of one
+// head).  Rows of the block's input arrive by LDS-DMA into a 6-row ring, and the work is software-
+// pipelined by one row: iteration y runs the Gram MFMAs of row y (staging buffer buf) interleaved,
+// per k-step, with the depthwise stencil of row y+1 (ring rows y..y+2 -> buffer buf^1), while rows
+// y+3, y+4 are in flight and row y+5 is issued.  One barrier per row.
+//  * ring row = 18 pixels (strip columns -1..16) x [q | k | v of this head | 1 pad float4];
+//    the pad makes the pixel stride 3 Ch + 4 floats, so the stencil's column reads (16 channels x
+//    4 pixel groups per wave) fall on 64 distinct banks.  Pad items and out-of-image pixels read
+//    p.zeros;
+//  * two wave classes.  "DMA waves" (those whose stencil jobs are all q/k) issue every ring DMA,
+//    exactly PPD pieces each per row (an uneven tail re-issues the last piece: same source, same
+//    destination), and their only VMEM ops are those DMAs, so "row y+2 has landed" is the
+//    compile-time s_waitcnt vmcnt(PPD * rows issued after it).  The other waves store v and never
+//    wait on vmcnt: the barrier after the DMA waves' wait covers them.  The loop body is
+//    instantiated per class, so neither carries the other's branches;
+//  * Gram MFMA k-step s takes pixel 4 s + (lane >> 4), so the q/k operand reads are
+//    bank-conflict-free (S = Ch padded to 16 mod 32).
+template <int CT>
+struct GramRing {
+  static constexpr int Ch = CT * 16;
+  static constexpr int NW = gram_waves(CT);
+  static constexpr int NJ = 3 * CT;
+  static constexpr int PS4 = 3 * Ch / 4 + 1;          // float4 per ring pixel
+  static constexpr int PS = 4 * PS4;                  // floats per ring pixel
+  static constexpr int Items = 18 * PS4;
+  static constexpr int Pieces = (Items + 63) / 64;    // 1 KiB DMA wave-instructions per row
+  static constexpr int RowF4 = Pieces * 64;
+  static constexpr int NSlot = 6;
+  static constexpr int S = (Ch % 32 == 16) ? Ch : Ch + 16;
+  static constexpr size_t lds_bytes = (size_t)NSlot * RowF4 * 16 + 4 * 16 * S * 4 + 2 * Ch * 4;
+  // DMA waves: the leading waves none of whose jobs (w, w + NW, ...) is a v job (job >= 2 CT)
+  static constexpr int dma_waves() {
+    int n = 0;
+    while (n < NW && n + NW * ((NJ - 1 - n) / NW) < 2 * CT) ++n;
+    return n;
+  }
+  static constexpr int NDW = dma_waves();
+  static constexpr int PPD = (Pieces + NDW - 1) / NDW;  // pieces per DMA wave per row
+};
+
+template <int CT>
+__global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_ring_kernel(GramParams p, int seg_rows) {
+  using R = GramRing<CT>;
+  using dma::f32x4;
+  constexpr int NW = R::NW, NJ = R::NJ, NDW = R::NDW, PPD = R::PPD;
+  constexpr int Ch = R::Ch, S = R::S, PS = R::PS, PS4 = R::PS4;
+  constexpr int JPW = (NJ + NW - 1) / NW;
+  constexpr int PPW = (CT * CT + NW - 1) / NW;
+  static_assert(NDW >= 1 && 3 * PPD < 64, "ring DMA accounting");
+  extern __shared__ __attribute__((aligned(16))) dma::f32x4 gring[];
+  float* ringf = reinterpret_cast<float*>(gring);
+  float* qs = ringf + R::NSlot * R::RowF4 * 4;  // [2][16 * S]
+  float* ks = qs + 2 * 16 * S;                  // [2][16 * S]
+  float* nred = ks + 2 * 16 * S;                // [2 Ch]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, lq = lane >> 4;
+  const int strips = p.W >> 4;
+  const int slot = blockIdx.x;
+  const int strip = slot % strips, seg = slot / strips;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int HW = p.H * p.W;
+  const int C = p.C;
+  const float* __restrict__ X = p.qkv + (long long)b * HW * p.ld;
+  float* __restrict__ V = p.v_out + (long long)b * HW * p.ldv;
+  const int xs = strip * 16;
+  const int y0 = seg * seg_rows, y1 = min(y0 + seg_rows, p.H);
+
+  // stencil jobs (part, channel tile) dealt round-robin; weights in registers before any DMA
+  int part[JPW], ctj[JPW];
+  float w[JPW][9], bias[JPW], n2[JPW];
+#pragma unroll
+  for (int j = 0; j < JPW; ++j) {
+    const int jb = wave + NW * j;
+    const int job = jb < NJ ? jb : 0;
+    part[j] = job / CT;
+    ctj[j] = job - part[j] * CT;
+    const int c = part[j] * C + h * Ch + ctj[j] * 16 + li;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) w[j][t] = p.wdw[t * 3 * C + c];
+    bias[j] = p.bdw ? p.bdw[c] : 0.f;
+    n2[j] = 0.f;
+  }
+  // DMA sources (DMA waves): piece k covers ring items 64k..64k+63; byte offset of the item's
+  // column within an image row, ~0u -> zero line
+  unsigned colo[PPD];
+#pragma unroll
+  for (int j = 0; j < PPD; ++j) {
+    const int k = min(wave + NDW * j, R::Pieces - 1);
+    const int it = k * 64 + lane;
+    const int px = it / PS4, r = it - (it / PS4) * PS4;
+    const int xx = xs - 1 + px;
+    const int pt = r / (Ch / 4), c4 = r - pt * (Ch / 4);
+    const bool ok = it < R::Items && r < PS4 - 1 && (unsigned)xx < (unsigned)p.W;
+    colo[j] = ok ? (unsigned)((xx * p.ld + pt * C + h * Ch + 4 * c4) * 4) : ~0u;
+  }
+  const unsigned rowbytes = (unsigned)p.W * (unsigned)p.ld * 4u;
+  const char* Xb = reinterpret_cast<const char*>(X);
+  auto issue = [&](int yy) {
+    f32x4* sl = gring + ((yy + R::NSlot) % R::NSlot) * R::RowF4;
+    const bool oky = (unsigned)yy < (unsigned)p.H;
+#pragma unroll
+    for (int j = 0; j < PPD; ++j) {
+      const int k = min(wave + NDW * j, R::Pieces - 1);
+      const void* src = (oky && colo[j] != ~0u) ? (const void*)(Xb + (unsigned)yy * rowbytes + colo[j])
+                                                 : (const void*)p.zeros;
+      dma::dma16(src, sl + 64 * k);
+    }
+  };
+  // DMA waves: wait until only the DMAs of the `ra` youngest rows are outstanding
+  auto wait_rows = [&](int ra) {
+    if (ra >= 3) dma::wait_vmcnt<3 * PPD>();
+    else if (ra == 2) dma::wait_vmcnt<2 * PPD>();
+    else if (ra == 1) dma::wait_vmcnt<PPD>();
+    else dma::wait_vmcnt<0>();
+  };
+
+  f32x4 acc[PPW];
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  dma::wait_vmcnt<0>();  // the weight loads above, so the first stencil does not drain the ring
+
+  auto run = [&](auto dma_wave) {
+    constexpr bool D = decltype(dma_wave)::value;
+    // stencil of output pixel s (of this lane's 4) of ring row r for every job; q/k -> staging
+    // buffer sb, v -> HBM (non-DMA waves only)
+    float win[JPW][3][6];
+    auto load_win = [&](int r) {
+      const float* rm = ringf + ((r + 5) % R::NSlot) * R::RowF4 * 4 + 4 * lq * PS + li;
+      const float* r0 = ringf + (r % R::NSlot) * R::RowF4 * 4 + 4 * lq * PS + li;
+      const float* rp = ringf + ((r + 1) % R::NSlot) * R::RowF4 * 4 + 4 * lq * PS + li;
+#pragma unroll
+      for (int j = 0; j < JPW; ++j) {
+        const int co = part[j] * Ch + ctj[j] * 16;
+#pragma unroll
+        for (int c6 = 0; c6 < 6; ++c6) {
+          win[j][0][c6] = rm[c6 * PS + co];
+          win[j][1][c6] = r0[c6 * PS + co];
+          win[j][2][c6] = rp[c6 * PS + co];
+        }
+      }
+    };
+    auto stencil = [&](int r, int sb, int s) {
+#pragma unroll
+      for (int j = 0; j < JPW; ++j) {
+        if (NJ % NW == 0 || wave + NW * j < NJ) {
+          float a = bias[j];
+#pragma unroll
+          for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) a = fmaf(win[j][rr][s + dx], w[j][3 * rr + dx], a);
+          const int lp = 4 * lq + s;
+          if (D || part[j] < 2) {
+            float* dst = part[j] == 0 ? qs : ks;
+            dst[sb * 16 * S + lp * S + ctj[j] * 16 + li] = a;
+            n2[j] = fmaf(a, a, n2[j]);
+          } else {
+            V[(r * p.W + xs + lp) * p.ldv + h * Ch + ctj[j] * 16 + li] = a;
+          }
+        }
+      }
+    };
+
+    // prologue: rows y0-1 .. min(y0+4, y1) in flight; stencil(y0) once rows y0-1..y0+1 landed
+    if (D)
+      for (int yy = y0 - 1; yy <= min(y0 + 4, y1); ++yy) issue(yy);
+    if (y0 < y1) {
+      if (D) wait_rows(max(0, min(y0 + 4, y1) - (y0 + 1)));
+      dma::barrier_lds();
+      load_win(y0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) stencil(y0, 0, s);
+    }
+    int buf = 0;
+    for (int y = y0; y < y1; ++y) {
+      const bool st = y + 1 < y1;
+      // rows y..y+2 landed: the younger DMAs are rows y+3 .. min(y+4, y1)
+      if (D && st) wait_rows(max(0, min(y + 4, y1) - (y + 2)));
+      dma::barrier_lds();
+      if (D && y + 5 <= y1) issue(y + 5);  // into the slot of row y-1, last read by stencil(y)
+      float qv[PPW][4], kv[PPW][4];
+#pragma unroll
+      for (int k = 0; k < PPW; ++k) {
+        const int pi = (CT * CT) % NW == 0 ? wave * PPW + k : min(wave * PPW + k, CT * CT - 1);
+        const int i = pi / CT, jj = pi - (pi / CT) * CT;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int lp = 4 * s + lq;
+          qv[k][s] = qs[buf * 16 * S + lp * S + 16 * i + li];
+          kv[k][s] = ks[buf * 16 * S + lp * S + 16 * jj + li];
+        }
+      }
+      if (st) load_win(y + 1);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int k = 0; k < PPW; ++k)
+          if ((CT * CT) % NW == 0 || wave * PPW + k < CT * CT) acc[k] = mfma4(qv[k][s], kv[k][s], acc[k]);
+        if (st) stencil(y + 1, buf ^ 1, s);
+      }
+      buf ^= 1;
+    }
+  };
+  if (wave < NDW) run(std::true_type{});
+  else run(std::false_type{});
+
+  float* out = p.partial + (((long long)b * p.heads + h) * p.nslots + slot) * p.slot_floats;
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) {
+    const int pi = wave * PPW + k;
+    if (pi < CT * CT) *reinterpret_cast<f32x4*>(out + (pi * 64 + lane) * 4) = acc[k];
+  }
+#pragma unroll
+  for (int j = 0; j < JPW; ++j) {
+    float t = n2[j];
+    t += __shfl_xor(t, 16);
+    t += __shfl_xor(t, 32);
+    const int jb = wave + NW * j;
+    if (jb < NJ && part[j] < 2 && lq == 0) nred[part[j] * Ch + ctj[j] * 16 + li] = t;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 2 * Ch; idx += 64 * NW) out[CT * CT * 256 + idx] = nred[idx];
+}
+
 template <int CT>
 static void launch_gram_ct(const GramParams& p, hipStream_t s) {
+  if constexpr (CT <= 6) {
+    using R = GramRing<CT>;
+    if (p.zeros && p.W % 16 == 0 && p.nslots % (p.W / 16) == 0 && p.ld % 4 == 0 && p.C % 4 == 0 &&
+        (unsigned long long)p.H * p.W * p.ld * 4 < (1ull << 32)) {
+      const int nseg = p.nslots / (p.W / 16);
+      const int seg_rows = (p.H + nseg - 1) / nseg;
+      hipLaunchKernelGGL(dwconv_gram_ring_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(64 * gram_waves(CT)),
+                         R::lds_bytes, s, p, seg_rows);
+      return;
+    }
+  }
   if (p.W % 16 == 0 && p.nslots % (p.W / 16) == 0) {
     const int nseg = p.nslots / (p.W / 16);
     const int seg_rows = (p.H + nseg - 1) / nseg;
