@@ -182,6 +182,57 @@ int kdlae_preprocess_u8(const uint8_t* images, int B, int h, int w, int channels
 int kdlae_postprocess_u8(const float* out, int B, int C, int Hs, int Ws, int h, int w, int scale,
                          const uint8_t* lq, int lq_channels, uint8_t* dst, void* stream);
 
+/* ------------------------------------------------------------------ KDLAE-T training
+ * One optimisation step of BasicSR's ImageCleanModel on KDLAE_teacher
+ * (Train/basicsr/models/image_restoration_model.py:198-218): forward with saved activations,
+ * L1LossSr (Train/basicsr/models/losses/losses.py:135-194), backward of every layer,
+ * clip_grad_norm_(0.01) and AdamW.  Parameters and gradients are two flat caller-owned device
+ * buffers of kdlae_tt_num_floats floats in state_dict order (offsets from kdlae_tt_param_info);
+ * weights are read in their OIHW state_dict layout, so an optimizer update needs no repacking.
+ * The DDP gradient all-reduce (base_model.py:76-82) is one collective over the flat gradient
+ * buffer, done by the caller between kdlae_tt_backward and kdlae_train_clip_adamw.
+ */
+typedef struct kdlae_tt_handle kdlae_tt_handle;
+
+/* replaces KDLAE_teacher.__init__ for training (same config struct; dual_pixel_task -> ENOTIMPL). */
+int kdlae_tt_create(const kdlae_t_config* cfg, int device, kdlae_tt_handle** out);
+int kdlae_tt_destroy(kdlae_tt_handle* h);
+/* net_g.state_dict() layout: key, element count and offset (floats) in the flat buffers. */
+int kdlae_tt_num_params(const kdlae_tt_handle* h);
+int kdlae_tt_param_info(const kdlae_tt_handle* h, int index, const char** name, int64_t* numel, int64_t* offset);
+int64_t kdlae_tt_num_floats(const kdlae_tt_handle* h);
+/* Device bytes of the caller-owned workspace (saved activations + backward scratch) for B x H x W. */
+int64_t kdlae_tt_workspace_bytes(kdlae_tt_handle* h, int B, int H, int W);
+/* replaces `preds = self.net_g(self.lq)` in optimize_parameters (image_restoration_model.py:200):
+ * same tensors as kdlae_t_forward; theta = flat parameters.  Activations needed by the backward
+ * stay in `workspace`, which must be passed unchanged to kdlae_tt_backward. */
+int kdlae_tt_forward(kdlae_tt_handle* h, const float* theta, const float* img, const float* rate, int B, int H,
+                     int W, float* hq, float* sr, void* workspace, size_t workspace_bytes, void* stream);
+/* replaces `l_pix.backward()` (:213): dhq [B,C,H,W] / dsr [B,C,2H,2W] (nullable: zero) are the loss
+ * gradients; grad (flat, overwritten) receives d loss / d theta.  Inputs get no gradient. */
+int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, const float* dsr, float* grad,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* replaces self.cri_pix(pred, self.gt) with L1LossSr(loss_weight=1, reduction='mean') (losses.py:159-170):
+ * loss[0] = 0.5 l1(hq) + 0.25 l1(sr) + 0.25 (shadow(hq) + shadow(sr)); dhq / dsr receive its gradient
+ * (the shadow terms binarise at 0.1 and carry none).  pred_sr NULL = no sr term.  scratch: device
+ * buffer of kdlae_train_l1sr_scratch_floats() floats. */
+int64_t kdlae_train_l1sr_scratch_floats(void);
+int kdlae_train_l1sr(const float* pred_hq, const float* gt_hq, int64_t n_hq, const float* pred_sr,
+                     const float* gt_sr, int64_t n_sr, float* dhq, float* dsr, float* loss, float* scratch,
+                     void* stream);
+/* replaces torch.nn.utils.clip_grad_norm_(params, max_norm) + torch.optim.AdamW.step (:215-218) over
+ * flat buffers: g = gscale * grad (gscale = 1/world_size after a summing all-reduce), clipped to
+ * max_norm (<= 0: no clip); `step` counts from 1.  The norm covers all n gradients; the update
+ * covers the host array `ranges` of nranges [begin, end) pairs (nranges 0: all n), mirroring
+ * torch.optim skipping parameters whose .grad is None.  scratch: kdlae_train_adamw_scratch_floats()
+ * floats; after the call scratch[2048] holds the gradient norm (after gscale, before clipping). */
+int64_t kdlae_train_adamw_scratch_floats(void);
+int kdlae_train_clip_adamw(float* theta, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                           float gscale, float max_norm, float lr, float beta1, float beta2, float eps,
+                           float weight_decay, int step, const int64_t* ranges, int nranges, float* scratch,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

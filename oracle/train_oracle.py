@@ -1,0 +1,77 @@
+"""TEST INFRASTRUCTURE ONLY — CPU oracle for one KDLAE-T training step.
+
+A from-scratch restatement of BasicSR's ``ImageCleanModel.optimize_parameters``
+(Train/basicsr/models/image_restoration_model.py:198-218) on top of the functional forward in
+``kdlae_oracle.teacher_forward``: L1LossSr, ``loss.backward()`` (torch autograd on CPU),
+``clip_grad_norm_(params, 0.01)`` and ``torch.optim.AdamW``.  Only ``tests/`` and ``bench.py``'s
+cpu_baseline leg may call it; the HIP training path (``rethink_acoustic_image_enhancement_amd.train``)
+never imports it.
+
+Pinning: ``tests/golden/train_*.npz`` hold the loss and every parameter gradient of the *imported
+reference* ``KDLAE_teacher`` (autograd through the reference module) under this loss, plus the
+parameters after two clip+AdamW steps; ``tests/test_train.py`` checks this oracle against them.
+BasicSR itself cannot be imported here (``basicsr.utils`` needs cv2), so ``l1sr_loss`` is a
+restatement of ``losses.py:135-194`` and is the one piece pinned by reading, not by execution.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .kdlae_oracle import TeacherCfg, teacher_forward
+
+# KDLAET.yml (Train/Denoising/Options/paper202508/KDLAET.yml:113-128)
+YML_OPTIM = dict(lr=1e-5, weight_decay=0.5e-4, betas=(0.2, 0.999))
+YML_CLIP = 0.01  # image_restoration_model.py:216 clip_grad_norm_(..., 0.01) when use_grad_clip
+
+
+def shadow(pred, target):
+    """L1LossSr.shadow (losses.py:172-194): L1 between 0/1 masks at threshold 0.1 (no gradient)."""
+    pb = torch.where(pred > 0.1, torch.ones_like(pred), torch.zeros_like(pred))
+    tb = torch.where(target > 0.1, torch.ones_like(target), torch.zeros_like(target))
+    return F.l1_loss(pb, tb, reduction="mean")
+
+
+def l1sr_loss(pred: dict, target: dict, loss_weight: float = 1.0):
+    """L1LossSr.forward (losses.py:149-170): 0.5 l1(hq) + 0.25 l1(sr) + 0.25 (shadow(hq) + shadow(sr))."""
+    hl_shadow = loss_weight * shadow(pred["hq"], target["hq"])
+    hl = loss_weight * F.l1_loss(pred["hq"], target["hq"], reduction="mean")
+    if pred.get("sr") is not None:
+        sr_shadow = loss_weight * shadow(pred["sr"], target["sr"])
+        srl = loss_weight * F.l1_loss(pred["sr"], target["sr"], reduction="mean")
+    else:
+        sr_shadow = 0
+        srl = 0
+    return 0.5 * hl + 0.25 * srl + 0.25 * (hl_shadow + sr_shadow)
+
+
+def loss_and_grads(sd: dict, img, rate, gt: dict, cfg: TeacherCfg):
+    """Forward + L1LossSr + autograd; returns (loss, {key: grad}) in state_dict order."""
+    params = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
+    out = teacher_forward(params, img, rate, cfg)
+    loss = l1sr_loss(out, gt)
+    grads = torch.autograd.grad(loss, list(params.values()), allow_unused=True)
+    return loss.detach(), {k: (g if g is not None else torch.zeros_like(params[k])) for k, g in zip(params, grads)}
+
+
+class TrainStep:
+    """optimize_parameters (image_restoration_model.py:198-218) over a plain state_dict."""
+
+    def __init__(self, sd: dict, cfg: TeacherCfg, lr=YML_OPTIM["lr"], weight_decay=YML_OPTIM["weight_decay"],
+                 betas=YML_OPTIM["betas"], clip=YML_CLIP):
+        self.cfg = cfg
+        self.params = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
+        self.opt = torch.optim.AdamW(list(self.params.values()), lr=lr, weight_decay=weight_decay, betas=betas)
+        self.clip = clip
+
+    def step(self, img, rate, gt: dict):
+        self.opt.zero_grad()
+        out = teacher_forward(self.params, img, rate, self.cfg)
+        loss = l1sr_loss(out, gt)
+        loss.backward()
+        norm = torch.nn.utils.clip_grad_norm_(list(self.params.values()), self.clip) if self.clip else None
+        self.opt.step()
+        return loss.detach(), norm
+
+    def state_dict(self):
+        return {k: v.detach() for k, v in self.params.items()}

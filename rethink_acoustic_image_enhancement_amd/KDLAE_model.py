@@ -195,6 +195,7 @@ class KDLAE_teacher(nn.Module):
             self.enhance = _stage(num_refinement_blocks, hc // 2, hd[0], f, bias, ln)
             self.outputen = nn.Conv2d(hc // 2, out_channels, kernel_size=3, padding=1, bias=bias)
         self._engines = {}
+        self._train_engines = {}
         self._warned_grad = False
 
     # ------------------------------------------------------------------ HIP plumbing
@@ -240,10 +241,21 @@ class KDLAE_teacher(nn.Module):
         cat = self._cfg["params"] == "cat"
         if cat and tuple(denoise_rate.shape) != (B, 1, H, W):
             raise RuntimeError(f"denoise_rate must be [B,1,H,W]={B, 1, H, W}, got {tuple(denoise_rate.shape)}")
-        if torch.is_grad_enabled() and (img.requires_grad or any(p.requires_grad for p in self.parameters())):
-            if not self._warned_grad:
-                warnings.warn("KDLAE_teacher HIP forward is inference-only: outputs carry no autograd graph")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            # training: the HIP training engine behind an autograd node (train.py), so
+            # `l_pix.backward()` (image_restoration_model.py:213) runs the hand-written backward
+            if img.requires_grad and not self._warned_grad:
+                warnings.warn("KDLAE_teacher HIP training path: the input image receives no gradient")
                 self._warned_grad = True
+            from .train import TeacherTrainFn, TrainEngine
+            eng = self._train_engines.get(img.device.index)
+            if eng is None:
+                eng = TrainEngine(self, img.device)
+                self._train_engines[img.device.index] = eng
+            out = TeacherTrainFn.apply(eng, img, denoise_rate if cat else None, *self.parameters())
+            if self.static == "train":
+                return {"hq": out[0], "sr": out[1]}
+            return {"hq": out, "sr": None}
         dev = img.device
         stream = torch.cuda.current_stream(dev).cuda_stream
         eng = self.engine(dev)

@@ -29,6 +29,10 @@ EXPORTS = (
     "asdqe_create", "asdqe_destroy", "asdqe_num_params", "asdqe_param_info", "asdqe_set_param",
     "asdqe_commit_params", "asdqe_workspace_bytes", "asdqe_forward",
     "kdlae_padded_size", "kdlae_preprocess_u8", "kdlae_postprocess_u8",
+    "kdlae_tt_create", "kdlae_tt_destroy", "kdlae_tt_num_params", "kdlae_tt_param_info", "kdlae_tt_num_floats",
+    "kdlae_tt_workspace_bytes", "kdlae_tt_forward", "kdlae_tt_backward",
+    "kdlae_train_l1sr_scratch_floats", "kdlae_train_l1sr", "kdlae_train_adamw_scratch_floats",
+    "kdlae_train_clip_adamw",
 )
 
 
@@ -112,8 +116,32 @@ def lib() -> ctypes.CDLL:
                                       c_void_p, c_void_p]
     L.kdlae_postprocess_u8.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_void_p]
+    L.kdlae_tt_create.argtypes = [ctypes.POINTER(TConfig), c_int, ctypes.POINTER(c_void_p)]
+    L.kdlae_tt_destroy.argtypes = [c_void_p]
+    L.kdlae_tt_num_params.argtypes = [c_void_p]
+    L.kdlae_tt_param_info.argtypes = [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64),
+                                      ctypes.POINTER(c_int64)]
+    L.kdlae_tt_num_floats.argtypes = [c_void_p]
+    L.kdlae_tt_num_floats.restype = c_int64
+    L.kdlae_tt_workspace_bytes.argtypes = [c_void_p, c_int, c_int, c_int]
+    L.kdlae_tt_workspace_bytes.restype = c_int64
+    L.kdlae_tt_forward.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                   c_void_p, c_void_p, ctypes.c_size_t, c_void_p]
+    L.kdlae_tt_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_size_t,
+                                    c_void_p]
+    L.kdlae_train_l1sr_scratch_floats.argtypes = []
+    L.kdlae_train_l1sr_scratch_floats.restype = c_int64
+    L.kdlae_train_l1sr.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p]
+    L.kdlae_train_adamw_scratch_floats.argtypes = []
+    L.kdlae_train_adamw_scratch_floats.restype = c_int64
+    c_float = ctypes.c_float
+    L.kdlae_train_clip_adamw.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
+                                         c_float, c_float, c_float, c_float, c_float, c_int, c_void_p, c_int, c_void_p,
+                                         c_void_p]
     for name in EXPORTS:
-        if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes", "_padded_size")):
+        if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes", "_padded_size", "_num_floats",
+                              "_scratch_floats")):
             getattr(L, name).restype = c_int
     _lib = L
     return L

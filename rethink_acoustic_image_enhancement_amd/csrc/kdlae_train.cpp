@@ -1,0 +1,801 @@
+// KDLAE-T training engine (C ABI kdlae_tt_*, include/kdlae.h): forward with saved activations and
+// the hand-sequenced backward of KDLAE_teacher (KDLAE/KDLAE_model.py:204-336) on the train.hip
+// kernels, plus the L1LossSr and clip_grad_norm_ + AdamW steps of BasicSR's ImageCleanModel
+// (Train/basicsr/models/image_restoration_model.py:198-218).
+//
+// Parameters and their gradients live in two flat caller-owned device buffers laid out in
+// state_dict order (kdlae_tt_param_info gives each key's offset), so the optimizer is one kernel
+// over one buffer and the DDP gradient all-reduce is one RCCL call over one buffer.
+//
+// Workspace: [split-K partials][reduction partials][saved forward activations][backward scratch].
+// The same code runs in a dry mode (no launches) to size it, so the size is exact.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kdlae.h"
+#include "runtime.h"
+#include "train_kernels.h"
+
+using kdlae::fail;
+namespace tr = kdlae::train;
+
+namespace {
+
+constexpr size_t kSplitCap = 8u << 20;  // floats of split-K partials
+constexpr size_t kRedCap = 8u << 20;    // floats of reduction partials
+
+struct BlockRec {
+  std::string p;
+  int C = 0, heads = 0, hid = 0, Bn = 0, H = 0, W = 0;
+  float *x = nullptr, *xn1 = nullptr, *st1 = nullptr, *qkv = nullptr, *qkvd = nullptr, *sumsq = nullptr, *G = nullptr,
+        *A = nullptr, *ao = nullptr, *x1 = nullptr, *xn2 = nullptr, *st2 = nullptr, *y = nullptr, *yd = nullptr,
+        *g = nullptr, *out = nullptr;
+};
+
+struct Saved {
+  int B = 0, H = 0, W = 0;
+  const void* ws = nullptr;
+  size_t fwd_end = 0;
+  bool valid = false;
+  float *img_h = nullptr, *pe = nullptr, *enc1 = nullptr, *dn1c = nullptr, *enc2 = nullptr, *dn2c = nullptr,
+        *enc3 = nullptr, *dn3c = nullptr, *lat = nullptr, *cat3 = nullptr, *dec3 = nullptr, *cat2 = nullptr,
+        *dec2 = nullptr, *cat1 = nullptr, *dec1 = nullptr, *ref = nullptr, *catp = nullptr, *ro = nullptr,
+        *hq_h = nullptr, *cenc = nullptr, *enh = nullptr;
+  std::unordered_map<std::string, std::vector<BlockRec>> stages;
+};
+
+}  // namespace
+
+struct kdlae_tt_handle {
+  kdlae_t_config cfg{};
+  int device = 0;
+  std::vector<std::pair<std::string, int64_t>> keys;
+  std::unordered_map<std::string, int64_t> off;
+  int64_t total = 0;
+  Saved sv;
+};
+
+namespace {
+
+int hid_of(const kdlae_t_config& c, int dim) { return (int)((double)dim * c.ffn_expansion_factor); }
+
+// state_dict order of KDLAE_teacher (KDLAE_model.py:220-268; TransformerBlock :150-157)
+void build_keys(kdlae_tt_handle* h) {
+  const kdlae_t_config& c = h->cfg;
+  auto add = [&](const std::string& k, int64_t n) {
+    h->off[k] = h->total;
+    h->keys.emplace_back(k, n);
+    h->total += n;
+  };
+  auto conv = [&](const std::string& n, int co, int ci, int k, bool b) {
+    add(n + ".weight", (int64_t)co * ci * k * k);
+    if (b) add(n + ".bias", co);
+  };
+  auto block = [&](const std::string& p, int dim, int heads) {
+    const int hid = hid_of(c, dim);
+    add(p + ".norm1.body.weight", dim);
+    if (!c.layernorm_biasfree) add(p + ".norm1.body.bias", dim);
+    add(p + ".attn.temperature", heads);
+    conv(p + ".attn.qkv", 3 * dim, dim, 1, c.bias);
+    conv(p + ".attn.qkv_dwconv", 3 * dim, 1, 3, c.bias);
+    conv(p + ".attn.project_out", dim, dim, 1, c.bias);
+    add(p + ".norm2.body.weight", dim);
+    if (!c.layernorm_biasfree) add(p + ".norm2.body.bias", dim);
+    conv(p + ".ffn.project_in", 2 * hid, dim, 1, c.bias);
+    conv(p + ".ffn.dwconv", 2 * hid, 1, 3, c.bias);
+    conv(p + ".ffn.project_out", dim, hid, 1, c.bias);
+  };
+  auto stage = [&](const std::string& n, int cnt, int dim, int heads) {
+    for (int i = 0; i < cnt; ++i) block(n + "." + std::to_string(i), dim, heads);
+  };
+  const int d = c.dim, *nb = c.num_blocks, *hd = c.heads, nr = c.num_refinement_blocks;
+  conv("patch_embed.proj", d, c.inp_channels, 3, false);
+  stage("encoder_level1", nb[0], d, hd[0]);
+  conv("down1_2.body.0", d / 2, d, 3, false);
+  stage("encoder_level2", nb[1], 2 * d, hd[1]);
+  conv("down2_3.body.0", d, 2 * d, 3, false);
+  stage("encoder_level3", nb[2], 4 * d, hd[2]);
+  conv("down3_4.body.0", 2 * d, 4 * d, 3, false);
+  stage("latent", nb[3], 8 * d, hd[3]);
+  conv("up4_3.body.0", 16 * d, 8 * d, 3, false);
+  conv("reduce_chan_level3", 4 * d, 8 * d, 1, c.bias);
+  stage("decoder_level3", nb[2], 4 * d, hd[2]);
+  conv("up3_2.body.0", 8 * d, 4 * d, 3, false);
+  conv("reduce_chan_level2", 2 * d, 4 * d, 1, c.bias);
+  stage("decoder_level2", nb[1], 2 * d, hd[1]);
+  conv("up2_1.body.0", 4 * d, 2 * d, 3, false);
+  stage("decoder_level1", nb[0], 2 * d, hd[0]);
+  stage("refinement", nr, 2 * d, hd[0]);
+  conv("output", c.out_channels, 2 * d, 3, c.bias);
+  conv("output_param", 2 * d, c.out_channels + 1, 3, c.bias);
+  stage("refinement_out", nr, 2 * d, hd[0]);
+  conv("output2", c.out_channels, 2 * d, 3, c.bias);
+  if (c.static_train) {
+    const int hc = 2 * d;
+    conv("cen", hc, c.out_channels, 3, c.bias);
+    conv("upen.body.0", 2 * hc, hc, 3, false);
+    stage("enhance", nr, hc / 2, hd[0]);
+    conv("outputen", c.out_channels, hc / 2, 3, c.bias);
+  }
+}
+
+int validate(const kdlae_t_config& c) {
+  if (c.dual_pixel_task)
+    return fail(KDLAE_ENOTIMPL, "dual_pixel_task=True: the reference forward raises NameError (KDLAE_model.py:305-321)");
+  if (c.dim <= 0 || c.dim % 2 || 8 * c.dim > 512)
+    return fail(KDLAE_EINVAL_CONFIG, "training path: dim must be even and 8*dim <= 512 (LayerNorm wave kernel)");
+  if (c.inp_channels < 1 || c.inp_channels != c.out_channels)
+    return fail(KDLAE_EINVAL_CONFIG, "inp_channels must equal out_channels (hq = out + inp_img, KDLAE_model.py:321)");
+  for (int i = 0; i < 4; ++i)
+    if (c.num_blocks[i] < 0 || c.heads[i] <= 0) return fail(KDLAE_EINVAL_CONFIG, "bad num_blocks/heads");
+  if (c.num_refinement_blocks < 0) return fail(KDLAE_EINVAL_CONFIG, "bad num_refinement_blocks");
+  auto head_ok = [](int C, int heads) { return C % heads == 0 && C / heads <= 120; };
+  const int d = c.dim;
+  const int lv[4] = {d, 2 * d, 4 * d, 8 * d};
+  for (int i = 0; i < 4; ++i)
+    if (!head_ok(lv[i], c.heads[i]))
+      return fail(KDLAE_EINVAL_CONFIG, "training path: channels per head must divide C and be <= 120");
+  if (!head_ok(2 * d, c.heads[0]) || (c.static_train && !head_ok(d, c.heads[0])))
+    return fail(KDLAE_EINVAL_CONFIG, "training path: channels per head must divide C and be <= 120");
+  if (c.ffn_expansion_factor <= 0) return fail(KDLAE_EINVAL_CONFIG, "bad ffn_expansion_factor");
+  return KDLAE_OK;
+}
+
+struct Ctx {
+  const kdlae_tt_handle* h;
+  const float* th = nullptr;
+  float* gr = nullptr;
+  char* base = nullptr;
+  size_t off = 0, cap = 0, peak = 0;
+  bool dry = true;
+  hipStream_t s = nullptr;
+  float* splitk = nullptr;
+  float* red = nullptr;
+
+  float* alloc(size_t n) {
+    off = (off + 255) / 256 * 256;
+    float* p = reinterpret_cast<float*>(base + off);
+    off += n * sizeof(float);
+    if (off > peak) peak = off;
+    return p;
+  }
+  const float* W(const std::string& k) const {
+    auto it = h->off.find(k);
+    return it == h->off.end() ? nullptr : th + it->second;
+  }
+  float* G(const std::string& k) const {
+    auto it = h->off.find(k);
+    return it == h->off.end() ? nullptr : gr + it->second;
+  }
+};
+
+#define LAUNCH(x)                                                                                    \
+  do {                                                                                               \
+    if (!c.dry) {                                                                                    \
+      hipError_t e_ = (x);                                                                           \
+      if (e_ != hipSuccess) return fail(KDLAE_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    }                                                                                                \
+  } while (0)
+#define TRY(x)                  \
+  do {                          \
+    int r_ = (x);               \
+    if (r_ != KDLAE_OK) return r_; \
+  } while (0)
+
+int nblk_for(long long rows, long long ncols, int maxb = 1024) {
+  long long nb = rows / 128;
+  if (nb > maxb) nb = maxb;
+  const long long cap = (long long)(kRedCap / (size_t)(ncols > 0 ? ncols : 1));
+  if (nb > cap) nb = cap;
+  return nb < 1 ? 1 : (int)nb;
+}
+
+// ---- convolutions over NHWC views (weights OIHW straight from the flat parameter buffer)
+struct V {
+  float* p;
+  int ld;
+};
+
+int conv1(Ctx& c, const std::string& n, V x, int Cin, int Cout, long long P, V out, const float* R = nullptr,
+          int ldr = 0) {
+  tr::TGemm g;
+  g.A = x.p; g.sam = x.ld; g.sak = 1;
+  g.B = c.W(n + ".weight"); g.sbk = 1; g.sbn = Cin;
+  g.C = out.p; g.scm = out.ld; g.scn = 1;
+  g.bias = c.W(n + ".bias");
+  g.R = R; g.srm = ldr; g.srn = 1;
+  g.M = (int)P; g.N = Cout; g.K = Cin;
+  LAUNCH(tr::launch_tgemm(g, 0, c.s));
+  return KDLAE_OK;
+}
+
+int bias_grad(Ctx& c, V dy, int N, long long P, float* out) {
+  if (!out) return KDLAE_OK;
+  const int nb = nblk_for(P, N);
+  LAUNCH(tr::launch_colsum(dy.p, dy.ld, N, P, 1, 0, c.red, nb, c.s));
+  LAUNCH(tr::launch_part_reduce(c.red, nb, N, 1, out, 0, 1.f, c.s));
+  return KDLAE_OK;
+}
+
+// dW = dY^T X, db = colsum dY, dX = dY W (+R)
+int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long long P, V dx, const float* R = nullptr,
+              int ldr = 0) {
+  tr::TGemm g;
+  g.A = dy.p; g.sam = 1; g.sak = dy.ld;
+  g.B = x.p; g.sbk = x.ld; g.sbn = 1;
+  g.C = c.G(n + ".weight"); g.scm = Cin; g.scn = 1;
+  g.M = Cout; g.N = Cin; g.K = (int)P;
+  g.partial = c.splitk;
+  LAUNCH(tr::launch_tgemm(g, kSplitCap, c.s));
+  TRY(bias_grad(c, dy, Cout, P, c.G(n + ".bias")));
+  if (dx.p) {
+    tr::TGemm d;
+    d.A = dy.p; d.sam = dy.ld; d.sak = 1;
+    d.B = c.W(n + ".weight"); d.sbk = Cin; d.sbn = 1;
+    d.C = dx.p; d.scm = dx.ld; d.scn = 1;
+    d.R = R; d.srm = ldr; d.srn = 1;
+    d.M = (int)P; d.N = Cin; d.K = Cout;
+    LAUNCH(tr::launch_tgemm(d, 0, c.s));
+  }
+  return KDLAE_OK;
+}
+
+int conv3(Ctx& c, const std::string& n, V x, int Cin, int Cout, int Bn, int H, int W, int dil, V out,
+          const float* R = nullptr, int ldr = 0) {
+  tr::TGemm g;
+  g.A = x.p; g.amode = 1; g.lda = x.ld; g.Cg = Cin;
+  g.B = c.W(n + ".weight"); g.bmode = 2;
+  g.C = out.p; g.scm = out.ld; g.scn = 1;
+  g.bias = c.W(n + ".bias");
+  g.R = R; g.srm = ldr; g.srn = 1;
+  g.M = Bn * H * W; g.N = Cout; g.K = 9 * Cin;
+  g.Bn = Bn; g.H = H; g.W = W; g.dil = dil;
+  LAUNCH(tr::launch_tgemm(g, 0, c.s));
+  return KDLAE_OK;
+}
+
+int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn, int H, int W, int dil, V dx,
+              const float* R = nullptr, int ldr = 0) {
+  const long long P = (long long)Bn * H * W;
+  tr::TGemm g;  // dW[co][ci][t] = sum_p dY[p,co] X[p + off_t, ci]
+  g.A = dy.p; g.sam = 1; g.sak = dy.ld;
+  g.B = x.p; g.bmode = 1; g.ldb = x.ld;
+  g.C = c.G(n + ".weight"); g.scm = (long long)Cin * 9; g.scn = 9; g.bC2 = 1;
+  g.nz2 = 9;
+  g.M = Cout; g.N = Cin; g.K = (int)P;
+  g.Bn = Bn; g.H = H; g.W = W; g.dil = dil;
+  g.partial = c.splitk;
+  LAUNCH(tr::launch_tgemm(g, kSplitCap, c.s));
+  TRY(bias_grad(c, dy, Cout, P, c.G(n + ".bias")));
+  if (dx.p) {
+    tr::TGemm d;  // transposed conv: flipped taps, channels swapped
+    d.A = dy.p; d.amode = 1; d.lda = dy.ld; d.Cg = Cout;
+    d.B = c.W(n + ".weight"); d.bmode = 3;
+    d.C = dx.p; d.scm = dx.ld; d.scn = 1;
+    d.R = R; d.srm = ldr; d.srn = 1;
+    d.M = (int)P; d.N = Cin; d.K = 9 * Cout;
+    d.Bn = Bn; d.H = H; d.W = W; d.dil = dil;
+    LAUNCH(tr::launch_tgemm(d, 0, c.s));
+  }
+  return KDLAE_OK;
+}
+
+// ---- TransformerBlock (KDLAE_model.py:150-163)
+int block_fwd(Ctx& c, BlockRec& r) {
+  const kdlae_t_config& cf = c.h->cfg;
+  const int C = r.C, C3 = 3 * C, hid = r.hid, heads = r.heads, Ch = C / heads, Bn = r.Bn;
+  const long long HW = (long long)r.H * r.W, P = Bn * HW;
+  const int bf = cf.layernorm_biasfree;
+  const std::string& p = r.p;
+  r.xn1 = c.alloc(P * C);
+  r.st1 = c.alloc(2 * P);
+  LAUNCH(tr::launch_ln_fwd(r.x, C, c.W(p + ".norm1.body.weight"), c.W(p + ".norm1.body.bias"), C, P, bf, r.xn1, C,
+                           r.st1, c.s));
+  r.qkv = c.alloc(P * C3);
+  TRY(conv1(c, p + ".attn.qkv", {r.xn1, C}, C, C3, P, {r.qkv, C3}));
+  r.qkvd = c.alloc(P * C3);
+  LAUNCH(tr::launch_dw_fwd(r.qkv, C3, c.W(p + ".attn.qkv_dwconv.weight"), c.W(p + ".attn.qkv_dwconv.bias"), 0, C3,
+                           Bn, r.H, r.W, r.qkvd, C3, c.s));
+  // ||q||^2, ||k||^2 per image and channel (F.normalize over HW, :135-136)
+  r.sumsq = c.alloc((size_t)Bn * 2 * C);
+  {
+    const int nb = nblk_for(HW, (long long)2 * C * Bn, 256);
+    LAUNCH(tr::launch_colsum(r.qkvd, C3, 2 * C, HW, Bn, 1, c.red, nb, c.s));
+    LAUNCH(tr::launch_part_reduce(c.red, nb, 2 * C, Bn, r.sumsq, 0, 1.f, c.s));
+  }
+  const size_t mats = (size_t)Bn * heads * Ch * Ch;
+  r.G = c.alloc(mats);
+  {
+    tr::TGemm g;  // G = q^T k per (image, head), un-normalised
+    g.A = r.qkvd; g.sam = 1; g.sak = C3; g.bA1 = HW * C3; g.bA2 = Ch;
+    g.B = r.qkvd + C; g.sbk = C3; g.sbn = 1; g.bB1 = HW * C3; g.bB2 = Ch;
+    g.C = r.G; g.scm = Ch; g.scn = 1; g.bC1 = (long long)heads * Ch * Ch; g.bC2 = (long long)Ch * Ch;
+    g.M = Ch; g.N = Ch; g.K = (int)HW; g.nz1 = Bn; g.nz2 = heads;
+    g.partial = c.splitk;
+    LAUNCH(tr::launch_tgemm(g, kSplitCap, c.s));
+  }
+  r.A = c.alloc(mats);
+  LAUNCH(tr::launch_attn_softmax(r.G, r.sumsq, c.W(p + ".attn.temperature"), Bn, C, heads, r.A, c.s));
+  r.ao = c.alloc(P * C);
+  {
+    tr::TGemm g;  // out = A v  (per pixel: ao[p,i] = sum_j A[i,j] v[p,j])
+    g.A = r.qkvd + 2 * C; g.sam = C3; g.sak = 1; g.bA1 = HW * C3; g.bA2 = Ch;
+    g.B = r.A; g.sbk = 1; g.sbn = Ch; g.bB1 = (long long)heads * Ch * Ch; g.bB2 = (long long)Ch * Ch;
+    g.C = r.ao; g.scm = C; g.scn = 1; g.bC1 = HW * C; g.bC2 = Ch;
+    g.M = (int)HW; g.N = Ch; g.K = Ch; g.nz1 = Bn; g.nz2 = heads;
+    LAUNCH(tr::launch_tgemm(g, 0, c.s));
+  }
+  r.x1 = c.alloc(P * C);
+  TRY(conv1(c, p + ".attn.project_out", {r.ao, C}, C, C, P, {r.x1, C}, r.x, C));
+  r.xn2 = c.alloc(P * C);
+  r.st2 = c.alloc(2 * P);
+  LAUNCH(tr::launch_ln_fwd(r.x1, C, c.W(p + ".norm2.body.weight"), c.W(p + ".norm2.body.bias"), C, P, bf, r.xn2, C,
+                           r.st2, c.s));
+  r.y = c.alloc(P * 2 * hid);
+  TRY(conv1(c, p + ".ffn.project_in", {r.xn2, C}, C, 2 * hid, P, {r.y, 2 * hid}));
+  r.yd = c.alloc(P * 2 * hid);
+  LAUNCH(tr::launch_dw_fwd(r.y, 2 * hid, c.W(p + ".ffn.dwconv.weight"), c.W(p + ".ffn.dwconv.bias"), 0, 2 * hid, Bn,
+                           r.H, r.W, r.yd, 2 * hid, c.s));
+  r.g = c.alloc(P * hid);
+  LAUNCH(tr::launch_gate_fwd(r.yd, 2 * hid, hid, P, r.g, hid, c.s));
+  r.out = c.alloc(P * C);
+  TRY(conv1(c, p + ".ffn.project_out", {r.g, hid}, hid, C, P, {r.out, C}, r.x1, C));
+  return KDLAE_OK;
+}
+
+int dw_wgrad(Ctx& c, const float* dy, const float* x, int C, int Bn, int H, int W, const std::string& n) {
+  const long long P = (long long)Bn * H * W;
+  const int nb = nblk_for(P, 10LL * C, 512);
+  LAUNCH(tr::launch_dw_wgrad(dy, C, x, C, C, Bn, H, W, c.red, nb, c.s));
+  const bool has_b = c.G(n + ".bias") != nullptr;
+  LAUNCH(tr::launch_part_reduce(c.red, nb, has_b ? 10 * C : 9 * C, 1, c.G(n + ".weight"), 0, 1.f, c.s, 10 * C));
+  return KDLAE_OK;
+}
+
+int ln_bwd(Ctx& c, const float* dy, const float* x, const float* st, int C, long long P, const std::string& n,
+           const float* R, float* dx) {
+  const int bf = c.h->cfg.layernorm_biasfree;
+  const int ncol = bf ? C : 2 * C;
+  const int nb = nblk_for(P, ncol);
+  LAUNCH(tr::launch_ln_bwd(dy, C, x, C, c.W(n + ".weight"), st, C, P, bf, R, C, dx, C, c.red, nb, c.s));
+  LAUNCH(tr::launch_part_reduce(c.red, nb, ncol, 1, c.G(n + ".weight"), 0, 1.f, c.s));
+  return KDLAE_OK;
+}
+
+// d: [P][C] gradient of the block output on entry, of the block input on exit
+int block_bwd(Ctx& c, const BlockRec& r, float* d) {
+  const int C = r.C, C3 = 3 * C, hid = r.hid, heads = r.heads, Ch = C / heads, Bn = r.Bn;
+  const long long HW = (long long)r.H * r.W, P = Bn * HW;
+  const std::string& p = r.p;
+  const size_t mark = c.off;
+  // ffn (KDLAE_model.py:101-106)
+  float* dg = c.alloc(P * hid);
+  TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, hid}, {d, C}, hid, C, P, {dg, hid}));
+  float* dyd = c.alloc(P * 2 * hid);
+  LAUNCH(tr::launch_gate_bwd(dg, hid, r.yd, 2 * hid, hid, P, dyd, 2 * hid, c.s));
+  float* dy = c.alloc(P * 2 * hid);
+  LAUNCH(tr::launch_dw_fwd(dyd, 2 * hid, c.W(p + ".ffn.dwconv.weight"), nullptr, 1, 2 * hid, Bn, r.H, r.W, dy,
+                           2 * hid, c.s));
+  TRY(dw_wgrad(c, dyd, r.y, 2 * hid, Bn, r.H, r.W, p + ".ffn.dwconv"));
+  float* dxn2 = c.alloc(P * C);
+  TRY(conv1_bwd(c, p + ".ffn.project_in", {r.xn2, C}, {dy, 2 * hid}, C, 2 * hid, P, {dxn2, C}));
+  float* dx1 = c.alloc(P * C);
+  TRY(ln_bwd(c, dxn2, r.x1, r.st2, C, P, p + ".norm2.body", d, dx1));
+  // attention (KDLAE_model.py:124-145)
+  float* dao = c.alloc(P * C);
+  TRY(conv1_bwd(c, p + ".attn.project_out", {r.ao, C}, {dx1, C}, C, C, P, {dao, C}));
+  const size_t mats = (size_t)Bn * heads * Ch * Ch;
+  float* dA = c.alloc(mats);
+  float* dqkvd = c.alloc(P * C3);
+  {
+    tr::TGemm g;  // dA[i,j] = sum_p dao[p,i] v[p,j]
+    g.A = dao; g.sam = 1; g.sak = C; g.bA1 = HW * C; g.bA2 = Ch;
+    g.B = r.qkvd + 2 * C; g.sbk = C3; g.sbn = 1; g.bB1 = HW * C3; g.bB2 = Ch;
+    g.C = dA; g.scm = Ch; g.scn = 1; g.bC1 = (long long)heads * Ch * Ch; g.bC2 = (long long)Ch * Ch;
+    g.M = Ch; g.N = Ch; g.K = (int)HW; g.nz1 = Bn; g.nz2 = heads;
+    g.partial = c.splitk;
+    LAUNCH(tr::launch_tgemm(g, kSplitCap, c.s));
+  }
+  {
+    tr::TGemm g;  // dv[p,j] = sum_i dao[p,i] A[i,j]
+    g.A = dao; g.sam = C; g.sak = 1; g.bA1 = HW * C; g.bA2 = Ch;
+    g.B = r.A; g.sbk = Ch; g.sbn = 1; g.bB1 = (long long)heads * Ch * Ch; g.bB2 = (long long)Ch * Ch;
+    g.C = dqkvd + 2 * C; g.scm = C3; g.scn = 1; g.bC1 = HW * C3; g.bC2 = Ch;
+    g.M = (int)HW; g.N = Ch; g.K = Ch; g.nz1 = Bn; g.nz2 = heads;
+    LAUNCH(tr::launch_tgemm(g, 0, c.s));
+  }
+  float* Mq = c.alloc(mats);
+  float* cq = c.alloc((size_t)Bn * heads * Ch);
+  float* ck = c.alloc((size_t)Bn * heads * Ch);
+  float* dtp = c.alloc((size_t)Bn * heads);
+  LAUNCH(tr::launch_attn_bwd(r.G, r.sumsq, c.W(p + ".attn.temperature"), r.A, dA, Bn, C, heads, Mq, cq, ck, dtp, c.s));
+  LAUNCH(tr::launch_part_reduce(dtp, Bn, heads, 1, c.G(p + ".attn.temperature"), 0, 1.f, c.s));
+  {
+    tr::TGemm g;  // dq[p,i] = sum_j Mq[i,j] k[p,j] + cq[i] q[p,i]
+    g.A = r.qkvd + C; g.sam = C3; g.sak = 1; g.bA1 = HW * C3; g.bA2 = Ch;
+    g.B = Mq; g.sbk = 1; g.sbn = Ch; g.bB1 = (long long)heads * Ch * Ch; g.bB2 = (long long)Ch * Ch;
+    g.C = dqkvd; g.scm = C3; g.scn = 1; g.bC1 = HW * C3; g.bC2 = Ch;
+    g.R = r.qkvd; g.srm = C3; g.srn = 1; g.bR1 = HW * C3; g.bR2 = Ch;
+    g.rs = cq; g.brs1 = (long long)heads * Ch; g.brs2 = Ch;
+    g.M = (int)HW; g.N = Ch; g.K = Ch; g.nz1 = Bn; g.nz2 = heads;
+    LAUNCH(tr::launch_tgemm(g, 0, c.s));
+    g.A = r.qkvd;  // dk[p,j] = sum_i Mq[i,j] q[p,i] + ck[j] k[p,j]
+    g.B = Mq; g.sbk = Ch; g.sbn = 1;
+    g.C = dqkvd + C;
+    g.R = r.qkvd + C;
+    g.rs = ck;
+    LAUNCH(tr::launch_tgemm(g, 0, c.s));
+  }
+  float* dqkv = c.alloc(P * C3);
+  LAUNCH(tr::launch_dw_fwd(dqkvd, C3, c.W(p + ".attn.qkv_dwconv.weight"), nullptr, 1, C3, Bn, r.H, r.W, dqkv, C3, c.s));
+  TRY(dw_wgrad(c, dqkvd, r.qkv, C3, Bn, r.H, r.W, p + ".attn.qkv_dwconv"));
+  float* dxn1 = c.alloc(P * C);
+  TRY(conv1_bwd(c, p + ".attn.qkv", {r.xn1, C}, {dqkv, C3}, C, C3, P, {dxn1, C}));
+  TRY(ln_bwd(c, dxn1, r.x, r.st1, C, P, p + ".norm1.body", dx1, d));
+  c.off = mark;
+  return KDLAE_OK;
+}
+
+int stage_fwd(Ctx& c, const std::string& name, int n, int C, int heads, int Bn, int H, int W, float* x, float** out) {
+  std::vector<BlockRec>& recs = const_cast<kdlae_tt_handle*>(c.h)->sv.stages[name];
+  recs.assign(n, BlockRec{});
+  for (int i = 0; i < n; ++i) {
+    BlockRec& r = recs[i];
+    r.p = name + "." + std::to_string(i);
+    r.C = C; r.heads = heads; r.hid = hid_of(c.h->cfg, C); r.Bn = Bn; r.H = H; r.W = W;
+    r.x = x;
+    TRY(block_fwd(c, r));
+    x = r.out;
+  }
+  *out = x;
+  return KDLAE_OK;
+}
+
+int stage_bwd(Ctx& c, const std::string& name, float* d) {
+  const auto& recs = c.h->sv.stages.at(name);
+  for (int i = (int)recs.size() - 1; i >= 0; --i) TRY(block_bwd(c, recs[i], d));
+  return KDLAE_OK;
+}
+
+// ---- whole network (KDLAE_model.py:270-336)
+int net_fwd(Ctx& c, const float* img, const float* rate, float* hq, float* sr) {
+  kdlae_tt_handle* h = const_cast<kdlae_tt_handle*>(c.h);
+  Saved& s = h->sv;
+  const kdlae_t_config& cf = h->cfg;
+  const int B = s.B, H = s.H, W = s.W, d = cf.dim, oc = cf.out_channels, ic = cf.inp_channels;
+  const int* nb = cf.num_blocks;
+  const int* hd = cf.heads;
+  const int nr = cf.num_refinement_blocks;
+  const long long P1 = (long long)B * H * W, P2 = P1 / 4, P3 = P1 / 16, P4 = P1 / 64;
+  const int H2 = H / 2, W2 = W / 2, H3 = H / 4, W3 = W / 4, H4 = H / 8, W4 = W / 8;
+
+  s.img_h = c.alloc(P1 * ic);
+  LAUNCH(tr::launch_nchw_to_nhwc(img, ic, B, (long long)H * W, s.img_h, ic, 0, c.s));
+  s.pe = c.alloc(P1 * d);
+  TRY(conv3(c, "patch_embed.proj", {s.img_h, ic}, ic, d, B, H, W, 1, {s.pe, d}));
+  TRY(stage_fwd(c, "encoder_level1", nb[0], d, hd[0], B, H, W, s.pe, &s.enc1));
+  s.dn1c = c.alloc(P1 * (d / 2));
+  TRY(conv3(c, "down1_2.body.0", {s.enc1, d}, d, d / 2, B, H, W, 1, {s.dn1c, d / 2}));
+  float* dn1 = c.alloc(P2 * 2 * d);
+  LAUNCH(tr::launch_shuffle(s.dn1c, d / 2, dn1, 2 * d, d / 2, B, H2, W2, 0, c.s));
+  TRY(stage_fwd(c, "encoder_level2", nb[1], 2 * d, hd[1], B, H2, W2, dn1, &s.enc2));
+  s.dn2c = c.alloc(P2 * d);
+  TRY(conv3(c, "down2_3.body.0", {s.enc2, 2 * d}, 2 * d, d, B, H2, W2, 1, {s.dn2c, d}));
+  float* dn2 = c.alloc(P3 * 4 * d);
+  LAUNCH(tr::launch_shuffle(s.dn2c, d, dn2, 4 * d, d, B, H3, W3, 0, c.s));
+  TRY(stage_fwd(c, "encoder_level3", nb[2], 4 * d, hd[2], B, H3, W3, dn2, &s.enc3));
+  s.dn3c = c.alloc(P3 * 2 * d);
+  TRY(conv3(c, "down3_4.body.0", {s.enc3, 4 * d}, 4 * d, 2 * d, B, H3, W3, 1, {s.dn3c, 2 * d}));
+  float* dn3 = c.alloc(P4 * 8 * d);
+  LAUNCH(tr::launch_shuffle(s.dn3c, 2 * d, dn3, 8 * d, 2 * d, B, H4, W4, 0, c.s));
+  TRY(stage_fwd(c, "latent", nb[3], 8 * d, hd[3], B, H4, W4, dn3, &s.lat));
+  // decoder level 3: cat [up4_3(latent), enc3] -> reduce_chan_level3 (KDLAE_model.py:288-291)
+  float* u43 = c.alloc(P4 * 16 * d);
+  TRY(conv3(c, "up4_3.body.0", {s.lat, 8 * d}, 8 * d, 16 * d, B, H4, W4, 1, {u43, 16 * d}));
+  s.cat3 = c.alloc(P3 * 8 * d);
+  LAUNCH(tr::launch_shuffle(u43, 16 * d, s.cat3, 8 * d, 4 * d, B, H4, W4, 1, c.s));
+  LAUNCH(tr::launch_copy_cols(s.enc3, 4 * d, s.cat3 + 4 * d, 8 * d, 4 * d, P3, 0, c.s));
+  float* rc3 = c.alloc(P3 * 4 * d);
+  TRY(conv1(c, "reduce_chan_level3", {s.cat3, 8 * d}, 8 * d, 4 * d, P3, {rc3, 4 * d}));
+  TRY(stage_fwd(c, "decoder_level3", nb[2], 4 * d, hd[2], B, H3, W3, rc3, &s.dec3));
+  // decoder level 2 (:293-296)
+  float* u32 = c.alloc(P3 * 8 * d);
+  TRY(conv3(c, "up3_2.body.0", {s.dec3, 4 * d}, 4 * d, 8 * d, B, H3, W3, 1, {u32, 8 * d}));
+  s.cat2 = c.alloc(P2 * 4 * d);
+  LAUNCH(tr::launch_shuffle(u32, 8 * d, s.cat2, 4 * d, 2 * d, B, H3, W3, 1, c.s));
+  LAUNCH(tr::launch_copy_cols(s.enc2, 2 * d, s.cat2 + 2 * d, 4 * d, 2 * d, P2, 0, c.s));
+  float* rc2 = c.alloc(P2 * 2 * d);
+  TRY(conv1(c, "reduce_chan_level2", {s.cat2, 4 * d}, 4 * d, 2 * d, P2, {rc2, 2 * d}));
+  TRY(stage_fwd(c, "decoder_level2", nb[1], 2 * d, hd[1], B, H2, W2, rc2, &s.dec2));
+  // decoder level 1 (:298-300), refinement (:302)
+  float* u21 = c.alloc(P2 * 4 * d);
+  TRY(conv3(c, "up2_1.body.0", {s.dec2, 2 * d}, 2 * d, 4 * d, B, H2, W2, 1, {u21, 4 * d}));
+  s.cat1 = c.alloc(P1 * 2 * d);
+  LAUNCH(tr::launch_shuffle(u21, 4 * d, s.cat1, 2 * d, d, B, H2, W2, 1, c.s));
+  LAUNCH(tr::launch_copy_cols(s.enc1, d, s.cat1 + d, 2 * d, d, P1, 0, c.s));
+  TRY(stage_fwd(c, "decoder_level1", nb[0], 2 * d, hd[0], B, H, W, s.cat1, &s.dec1));
+  TRY(stage_fwd(c, "refinement", nr, 2 * d, hd[0], B, H, W, s.dec1, &s.ref));
+  // output heads (:314-321)
+  s.hq_h = c.alloc(P1 * oc);
+  if (cf.params_cat) {
+    s.catp = c.alloc(P1 * (oc + 1));
+    TRY(conv3(c, "output", {s.ref, 2 * d}, 2 * d, oc, B, H, W, 1, {s.catp, oc + 1}));
+    LAUNCH(tr::launch_nchw_to_nhwc(rate, 1, B, (long long)H * W, s.catp + oc, oc + 1, 0, c.s));
+    float* op = c.alloc(P1 * 2 * d);
+    TRY(conv3(c, "output_param", {s.catp, oc + 1}, oc + 1, 2 * d, B, H, W, 2, {op, 2 * d}));
+    TRY(stage_fwd(c, "refinement_out", nr, 2 * d, hd[0], B, H, W, op, &s.ro));
+    TRY(conv3(c, "output2", {s.ro, 2 * d}, 2 * d, oc, B, H, W, 1, {s.hq_h, oc}, s.img_h, ic));
+  } else {
+    TRY(conv3(c, "output", {s.ref, 2 * d}, 2 * d, oc, B, H, W, 1, {s.hq_h, oc}, s.img_h, ic));
+  }
+  LAUNCH(tr::launch_nhwc_to_nchw(s.hq_h, oc, nullptr, oc, B, (long long)H * W, hq, c.s));
+  // super-resolution branch (:324-329)
+  if (cf.static_train) {
+    const int hc = 2 * d;
+    s.cenc = c.alloc(P1 * hc);
+    TRY(conv3(c, "cen", {s.hq_h, oc}, oc, hc, B, H, W, 1, {s.cenc, hc}));
+    float* upc = c.alloc(P1 * 2 * hc);
+    TRY(conv3(c, "upen.body.0", {s.cenc, hc}, hc, 2 * hc, B, H, W, 1, {upc, 2 * hc}));
+    float* ups = c.alloc(P1 * 4 * (hc / 2));
+    LAUNCH(tr::launch_shuffle(upc, 2 * hc, ups, hc / 2, hc / 2, B, H, W, 1, c.s));
+    TRY(stage_fwd(c, "enhance", nr, hc / 2, hd[0], B, 2 * H, 2 * W, ups, &s.enh));
+    float* srh = c.alloc(P1 * 4 * oc);
+    TRY(conv3(c, "outputen", {s.enh, hc / 2}, hc / 2, oc, B, 2 * H, 2 * W, 1, {srh, oc}));
+    LAUNCH(tr::launch_nhwc_to_nchw(srh, oc, nullptr, oc, B, 4LL * H * W, sr, c.s));
+  }
+  return KDLAE_OK;
+}
+
+// has_dsr: the sr branch is differentiated (dsr given); the dry sizing pass always takes it
+int net_bwd(Ctx& c, const float* dhq, const float* dsr, bool has_dsr) {
+  const Saved& s = c.h->sv;
+  const kdlae_t_config& cf = c.h->cfg;
+  const int B = s.B, H = s.H, W = s.W, d = cf.dim, oc = cf.out_channels, ic = cf.inp_channels;
+  const long long P1 = (long long)B * H * W, P2 = P1 / 4, P3 = P1 / 16, P4 = P1 / 64;
+  const int H2 = H / 2, W2 = W / 2, H3 = H / 4, W3 = W / 4, H4 = H / 8, W4 = W / 8;
+
+  float* dhq_h = c.alloc(P1 * oc);
+  if (dhq) LAUNCH(tr::launch_nchw_to_nhwc(dhq, oc, B, (long long)H * W, dhq_h, oc, 0, c.s));
+  else LAUNCH(hipMemsetAsync(dhq_h, 0, P1 * oc * sizeof(float), c.s));
+  if (cf.static_train && has_dsr) {
+    const int hc = 2 * d;
+    float* dsr_h = c.alloc(P1 * 4 * oc);
+    LAUNCH(tr::launch_nchw_to_nhwc(dsr, oc, B, 4LL * H * W, dsr_h, oc, 0, c.s));
+    float* denh = c.alloc(P1 * 4 * (hc / 2));
+    TRY(conv3_bwd(c, "outputen", {s.enh, hc / 2}, {dsr_h, oc}, hc / 2, oc, B, 2 * H, 2 * W, 1, {denh, hc / 2}));
+    TRY(stage_bwd(c, "enhance", denh));
+    float* dupc = c.alloc(P1 * 2 * hc);
+    LAUNCH(tr::launch_shuffle(denh, hc / 2, dupc, 2 * hc, hc / 2, B, H, W, 0, c.s));
+    // upen's input (cenc) is recomputed-free: it was saved in the forward
+    float* dcen = c.alloc(P1 * hc);
+    TRY(conv3_bwd(c, "upen.body.0", {s.cenc, hc}, {dupc, 2 * hc}, hc, 2 * hc, B, H, W, 1, {dcen, hc}));
+    TRY(conv3_bwd(c, "cen", {s.hq_h, oc}, {dcen, hc}, oc, hc, B, H, W, 1, {dhq_h, oc}, dhq_h, oc));
+  } else if (cf.static_train) {
+    // sr unused by the loss: its parameters get zero gradients (grad buffer is zeroed up front)
+  }
+  // hq = out + img: d(out) = dhq
+  float* dref = c.alloc(P1 * 2 * d);
+  if (cf.params_cat) {
+    float* dro = c.alloc(P1 * 2 * d);
+    TRY(conv3_bwd(c, "output2", {s.ro, 2 * d}, {dhq_h, oc}, 2 * d, oc, B, H, W, 1, {dro, 2 * d}));
+    TRY(stage_bwd(c, "refinement_out", dro));
+    float* dcatp = c.alloc(P1 * (oc + 1));
+    TRY(conv3_bwd(c, "output_param", {s.catp, oc + 1}, {dro, 2 * d}, oc + 1, 2 * d, B, H, W, 2, {dcatp, oc + 1}));
+    TRY(conv3_bwd(c, "output", {s.ref, 2 * d}, {dcatp, oc + 1}, 2 * d, oc, B, H, W, 1, {dref, 2 * d}));
+  } else {
+    TRY(conv3_bwd(c, "output", {s.ref, 2 * d}, {dhq_h, oc}, 2 * d, oc, B, H, W, 1, {dref, 2 * d}));
+  }
+  TRY(stage_bwd(c, "refinement", dref));
+  TRY(stage_bwd(c, "decoder_level1", dref));  // dref now holds d(cat1) = [d up2_1 | d enc1]
+  float* de1 = c.alloc(P1 * d);
+  LAUNCH(tr::launch_copy_cols(dref + d, 2 * d, de1, d, d, P1, 0, c.s));
+  float* du21 = c.alloc(P2 * 4 * d);
+  LAUNCH(tr::launch_shuffle(dref, 2 * d, du21, 4 * d, d, B, H2, W2, 0, c.s));
+  float* ddec2 = c.alloc(P2 * 2 * d);
+  TRY(conv3_bwd(c, "up2_1.body.0", {s.dec2, 2 * d}, {du21, 4 * d}, 2 * d, 4 * d, B, H2, W2, 1, {ddec2, 2 * d}));
+  TRY(stage_bwd(c, "decoder_level2", ddec2));
+  float* dcat2 = c.alloc(P2 * 4 * d);
+  TRY(conv1_bwd(c, "reduce_chan_level2", {s.cat2, 4 * d}, {ddec2, 2 * d}, 4 * d, 2 * d, P2, {dcat2, 4 * d}));
+  float* de2 = c.alloc(P2 * 2 * d);
+  LAUNCH(tr::launch_copy_cols(dcat2 + 2 * d, 4 * d, de2, 2 * d, 2 * d, P2, 0, c.s));
+  float* du32 = c.alloc(P3 * 8 * d);
+  LAUNCH(tr::launch_shuffle(dcat2, 4 * d, du32, 8 * d, 2 * d, B, H3, W3, 0, c.s));
+  float* ddec3 = c.alloc(P3 * 4 * d);
+  TRY(conv3_bwd(c, "up3_2.body.0", {s.dec3, 4 * d}, {du32, 8 * d}, 4 * d, 8 * d, B, H3, W3, 1, {ddec3, 4 * d}));
+  TRY(stage_bwd(c, "decoder_level3", ddec3));
+  float* dcat3 = c.alloc(P3 * 8 * d);
+  TRY(conv1_bwd(c, "reduce_chan_level3", {s.cat3, 8 * d}, {ddec3, 4 * d}, 8 * d, 4 * d, P3, {dcat3, 8 * d}));
+  float* de3 = c.alloc(P3 * 4 * d);
+  LAUNCH(tr::launch_copy_cols(dcat3 + 4 * d, 8 * d, de3, 4 * d, 4 * d, P3, 0, c.s));
+  float* du43 = c.alloc(P4 * 16 * d);
+  LAUNCH(tr::launch_shuffle(dcat3, 8 * d, du43, 16 * d, 4 * d, B, H4, W4, 0, c.s));
+  float* dlat = c.alloc(P4 * 8 * d);
+  TRY(conv3_bwd(c, "up4_3.body.0", {s.lat, 8 * d}, {du43, 16 * d}, 8 * d, 16 * d, B, H4, W4, 1, {dlat, 8 * d}));
+  TRY(stage_bwd(c, "latent", dlat));
+  // encoder, deepest first; each Downsample's dX accumulates into the skip gradient
+  float* ddn3c = c.alloc(P3 * 2 * d);
+  LAUNCH(tr::launch_shuffle(dlat, 8 * d, ddn3c, 2 * d, 2 * d, B, H4, W4, 1, c.s));
+  TRY(conv3_bwd(c, "down3_4.body.0", {s.enc3, 4 * d}, {ddn3c, 2 * d}, 4 * d, 2 * d, B, H3, W3, 1, {de3, 4 * d}, de3,
+                4 * d));
+  TRY(stage_bwd(c, "encoder_level3", de3));
+  float* ddn2c = c.alloc(P2 * d);
+  LAUNCH(tr::launch_shuffle(de3, 4 * d, ddn2c, d, d, B, H3, W3, 1, c.s));
+  TRY(conv3_bwd(c, "down2_3.body.0", {s.enc2, 2 * d}, {ddn2c, d}, 2 * d, d, B, H2, W2, 1, {de2, 2 * d}, de2, 2 * d));
+  TRY(stage_bwd(c, "encoder_level2", de2));
+  float* ddn1c = c.alloc(P1 * (d / 2));
+  LAUNCH(tr::launch_shuffle(de2, 2 * d, ddn1c, d / 2, d / 2, B, H2, W2, 1, c.s));
+  TRY(conv3_bwd(c, "down1_2.body.0", {s.enc1, d}, {ddn1c, d / 2}, d, d / 2, B, H, W, 1, {de1, d}, de1, d));
+  TRY(stage_bwd(c, "encoder_level1", de1));
+  TRY(conv3_bwd(c, "patch_embed.proj", {s.img_h, ic}, {de1, d}, ic, d, B, H, W, 1, {nullptr, 0}));
+  return KDLAE_OK;
+}
+
+void ctx_init(Ctx& c, const kdlae_tt_handle* h, void* ws, size_t ws_bytes, bool dry, hipStream_t s) {
+  c.h = h;
+  c.dry = dry;
+  c.s = s;
+  c.base = dry ? nullptr : static_cast<char*>(ws);
+  c.cap = ws_bytes;
+  c.off = 0;
+  c.splitk = c.alloc(kSplitCap);
+  c.red = c.alloc(kRedCap);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kdlae_tt_create(const kdlae_t_config* cfg, int device, kdlae_tt_handle** out) {
+  if (!cfg || !out) return fail(KDLAE_EINVAL_CONFIG, "null argument");
+  int rc = validate(*cfg);
+  if (rc) return rc;
+  auto* h = new kdlae_tt_handle();
+  h->cfg = *cfg;
+  h->device = device;
+  build_keys(h);
+  *out = h;
+  return KDLAE_OK;
+}
+
+int kdlae_tt_destroy(kdlae_tt_handle* h) {
+  delete h;
+  return KDLAE_OK;
+}
+
+int kdlae_tt_num_params(const kdlae_tt_handle* h) { return h ? (int)h->keys.size() : 0; }
+
+int kdlae_tt_param_info(const kdlae_tt_handle* h, int index, const char** name, int64_t* numel, int64_t* offset) {
+  if (!h || index < 0 || index >= (int)h->keys.size()) return fail(KDLAE_EPARAM, "param index out of range");
+  if (name) *name = h->keys[index].first.c_str();
+  if (numel) *numel = h->keys[index].second;
+  if (offset) *offset = h->off.at(h->keys[index].first);
+  return KDLAE_OK;
+}
+
+int64_t kdlae_tt_num_floats(const kdlae_tt_handle* h) { return h ? h->total : -1; }
+
+static int check_shape(int B, int H, int W) {
+  if (B <= 0 || H <= 0 || W <= 0) return fail(KDLAE_EINVAL_SHAPE, "B, H, W must be positive");
+  if (H % 8 || W % 8)
+    return fail(KDLAE_EINVAL_SHAPE, "H and W must be divisible by 8 (pixel_unshuffle x3, KDLAE_model.py:186-187)");
+  if ((long long)B * H * W * 4 > (1LL << 31) - 1) return fail(KDLAE_EINVAL_SHAPE, "too many pixels for one step");
+  return KDLAE_OK;
+}
+
+int64_t kdlae_tt_workspace_bytes(kdlae_tt_handle* h, int B, int H, int W) {
+  if (!h) return -1;
+  if (check_shape(B, H, W)) return -1;
+  Saved keep = h->sv;
+  Ctx c;
+  ctx_init(c, h, nullptr, 0, true, nullptr);
+  h->sv = Saved{};
+  h->sv.B = B; h->sv.H = H; h->sv.W = W;
+  int rc = net_fwd(c, nullptr, nullptr, nullptr, nullptr);
+  if (rc == KDLAE_OK) rc = net_bwd(c, nullptr, nullptr, h->cfg.static_train != 0);
+  h->sv = keep;
+  return rc == KDLAE_OK ? (int64_t)c.peak : -1;
+}
+
+int kdlae_tt_forward(kdlae_tt_handle* h, const float* theta, const float* img, const float* rate, int B, int H, int W,
+                     float* hq, float* sr, void* ws, size_t ws_bytes, void* stream) {
+  if (!h || !theta || !img || !hq || !ws) return fail(KDLAE_EINVAL_CONFIG, "null argument");
+  int rc = check_shape(B, H, W);
+  if (rc) return rc;
+  if (h->cfg.params_cat && !rate) return fail(KDLAE_EINVAL_CONFIG, "params='cat' needs denoise_rate");
+  if (h->cfg.static_train && !sr) return fail(KDLAE_EINVAL_CONFIG, "static='train' needs the sr output");
+  const int64_t need = kdlae_tt_workspace_bytes(h, B, H, W);
+  if (need < 0 || (size_t)need > ws_bytes) return fail(KDLAE_ESTATE, "training workspace too small");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
+  Ctx c;
+  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
+  c.th = theta;
+  h->sv = Saved{};
+  h->sv.B = B; h->sv.H = H; h->sv.W = W;
+  rc = net_fwd(c, img, rate, hq, sr);
+  if (rc) return rc;
+  h->sv.ws = ws;
+  h->sv.fwd_end = c.off;
+  h->sv.valid = true;
+  return KDLAE_OK;
+}
+
+int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, const float* dsr, float* grad, void* ws,
+                      size_t ws_bytes, void* stream) {
+  if (!h || !theta || !grad || !ws) return fail(KDLAE_EINVAL_CONFIG, "null argument");
+  if (!h->sv.valid || h->sv.ws != ws)
+    return fail(KDLAE_ESTATE, "kdlae_tt_backward needs a preceding kdlae_tt_forward on the same workspace");
+  const bool has_dsr = h->cfg.static_train && dsr;
+  {  // size the backward before launching anything
+    Ctx d;
+    ctx_init(d, h, nullptr, 0, true, nullptr);
+    d.off = h->sv.fwd_end;
+    int rc = net_bwd(d, dhq, dsr, has_dsr);
+    if (rc) return rc;
+    if (d.peak > ws_bytes) return fail(KDLAE_ESTATE, "training workspace too small for the backward");
+  }
+  Ctx c;
+  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
+  c.th = theta;
+  c.gr = grad;
+  c.off = h->sv.fwd_end;
+  hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
+  if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
+  return net_bwd(c, dhq, dsr, has_dsr);
+}
+
+int64_t kdlae_train_l1sr_scratch_floats(void) { return 4 * 1024; }
+
+int kdlae_train_l1sr(const float* pred_hq, const float* gt_hq, int64_t n_hq, const float* pred_sr, const float* gt_sr,
+                     int64_t n_sr, float* dhq, float* dsr, float* loss, float* scratch, void* stream) {
+  if (!pred_hq || !gt_hq || !loss || !scratch || n_hq <= 0) return fail(KDLAE_EINVAL_CONFIG, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = 1024;
+  float* p0 = scratch;
+  float* p1 = scratch + 2 * nb;
+  // L1LossSr (losses.py:159-170): 0.5 l1(hq) + 0.25 l1(sr) + 0.25 (shadow(hq) + shadow(sr))
+  hipError_t e = tr::launch_l1sr(pred_hq, gt_hq, n_hq, 0.5f, dhq, p0, nb, s);
+  if (e == hipSuccess && pred_sr) e = tr::launch_l1sr(pred_sr, gt_sr, n_sr, 0.25f, dsr, p1, nb, s);
+  if (e == hipSuccess)
+    e = tr::launch_l1sr_final(p0, nb, n_hq, 0.5f, 0.25f, pred_sr ? p1 : nullptr, pred_sr ? nb : 0, pred_sr ? n_sr : 1,
+                              0.25f, 0.25f, loss, s);
+  if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
+  return KDLAE_OK;
+}
+
+int64_t kdlae_train_adamw_scratch_floats(void) { return 2048 + 2; }
+
+int kdlae_train_clip_adamw(float* theta, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float gscale,
+                           float max_norm, float lr, float beta1, float beta2, float eps, float weight_decay, int step,
+                           const int64_t* ranges, int nranges, float* scratch, void* stream) {
+  if (!theta || !grad || !exp_avg || !exp_avg_sq || !scratch || n <= 0 || step < 1 || nranges < 0 ||
+      (nranges > 0 && !ranges))
+    return fail(KDLAE_EINVAL_CONFIG, "bad argument");
+  for (int r = 0; r < nranges; ++r)
+    if (ranges[2 * r] < 0 || ranges[2 * r] > ranges[2 * r + 1] || ranges[2 * r + 1] > n)
+      return fail(KDLAE_EINVAL_CONFIG, "bad parameter range");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = 2048;
+  float* state = scratch + nb;  // [0] = grad norm, [1] = applied grad scale
+  // the norm covers every gradient (clip_grad_norm_ over net_g.parameters()); the update only the
+  // parameters that received a gradient (torch.optim skips p.grad is None, e.g. output_param when
+  // params != 'cat')
+  hipError_t e = tr::launch_sumsq(grad, n, scratch, nb, s);
+  if (e == hipSuccess) e = tr::launch_clip_coef(scratch, nb, gscale, max_norm, state, s);
+  const int64_t whole[2] = {0, n};
+  const int64_t* rg = nranges ? ranges : whole;
+  for (int r = 0; r < (nranges ? nranges : 1) && e == hipSuccess; ++r) {
+    const int64_t b = rg[2 * r], len = rg[2 * r + 1] - b;
+    if (len > 0)
+      e = tr::launch_adamw(theta + b, grad + b, exp_avg + b, exp_avg_sq + b, len, state, lr, beta1, beta2, eps,
+                           weight_decay, step, s);
+  }
+  if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
+  return KDLAE_OK;
+}
+
+}  // extern "C"

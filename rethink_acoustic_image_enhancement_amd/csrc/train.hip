@@ -1,0 +1,820 @@
+// KDLAE-T training kernels for gfx950 (MI355X): generic MFMA GEMM with im2col / shifted-B modes and a
+// deterministic split-K, LayerNorm forward/backward with wavefront-shuffle channel reductions,
+// depthwise 3x3 forward / dX / dW, the MDTA softmax and its backward, the GELU gate, PixelShuffle,
+// L1LossSr, grad-norm clip and AdamW.  Every reduction over pixels is two-pass (per-block partials,
+// then a fixed-order sum), so a training step is bit-reproducible run to run.
+//
+// Reference semantics: KDLAE/KDLAE_model.py (LayerNorm :38-83, FeedForward :89-106, Attention
+// :112-145), Train/basicsr/models/losses/losses.py:135-194 (L1LossSr),
+// Train/basicsr/models/image_restoration_model.py:198-218 (clip_grad_norm_ 0.01, optimizer step).
+#include <math.h>
+
+#include "train_kernels.h"
+
+namespace kdlae {
+namespace train {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+static inline int grid_for(long long n, int threads, int cap = 1 << 20) {
+  long long g = (n + threads - 1) / threads;
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}
+
+// ---------------------------------------------------------------------------------------------- GEMM
+constexpr int BM = 64, BN = 64, BK = 16, LDP = BM + 4;
+
+struct Pix { int b, y, x; };
+
+__device__ __forceinline__ Pix decompose(long long p, int H, int W) {
+  const long long hw = (long long)H * W;
+  Pix r;
+  r.b = (int)(p / hw);
+  const int rem = (int)(p - (long long)r.b * hw);
+  r.y = rem / W;
+  r.x = rem - r.y * W;
+  return r;
+}
+
+template <int AM>
+__device__ __forceinline__ float a_at(const TGemm& g, const float* A, int m, int k, const Pix& pm) {
+  if (m >= g.M || k >= g.K) return 0.f;
+  if (AM == 0) return A[(long long)m * g.sam + (long long)k * g.sak];
+  const int tap = k / g.Cg, c = k - tap * g.Cg;
+  const int yy = pm.y + (tap / 3 - 1) * g.dil, xx = pm.x + (tap % 3 - 1) * g.dil;
+  if (yy < 0 || yy >= g.H || xx < 0 || xx >= g.W) return 0.f;
+  return A[(((long long)pm.b * g.H + yy) * g.W + xx) * g.lda + c];
+}
+
+template <int BMODE>
+__device__ __forceinline__ float b_at(const TGemm& g, const float* B, int k, int n, const Pix& pk, int tap) {
+  if (k >= g.K || n >= g.N) return 0.f;
+  if (BMODE == 0) return B[(long long)k * g.sbk + (long long)n * g.sbn];
+  if (BMODE == 1) {
+    const int yy = pk.y + (tap / 3 - 1) * g.dil, xx = pk.x + (tap % 3 - 1) * g.dil;
+    if (yy < 0 || yy >= g.H || xx < 0 || xx >= g.W) return 0.f;
+    return B[(((long long)pk.b * g.H + yy) * g.W + xx) * g.ldb + n];
+  }
+  const int t = k / g.Cg, c = k - t * g.Cg;
+  if (BMODE == 2) return B[((long long)n * g.Cg + c) * 9 + t];
+  return B[((long long)c * g.N + n) * 9 + (8 - t)];
+}
+
+__device__ __forceinline__ float epi(const TGemm& g, float acc, int m, int n, const float* R, const float* rs) {
+  float v = g.alpha * acc;
+  if (g.bias) v += g.bias[n];
+  if (R) {
+    const float r = R[(long long)m * g.srm + (long long)n * g.srn];
+    v += rs ? rs[n] * r : r;
+  }
+  return v;
+}
+
+template <int AM, int BMODE>
+__global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk) {
+  __shared__ float As[BK][LDP];
+  __shared__ float Bs[BK][LDP];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv & 1, wn = wv >> 1;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
+  const int z = blockIdx.z, z1 = z / g.nz2, z2 = z - z1 * g.nz2;
+  const float* A = g.A + z1 * g.bA1 + z2 * g.bA2;
+  const float* B = g.B + (BMODE == 1 ? z1 * g.bB1 : z1 * g.bB1 + z2 * g.bB2);
+  const int ks = blockIdx.y;
+  const int kbeg = ks * kchunk, kend = min(g.K, kbeg + kchunk);
+
+  // load mappings (uniform per launch)
+  const bool a_kc = (AM == 1) || (g.sak == 1);           // k contiguous in memory
+  const bool b_nc = (BMODE == 1) || (BMODE == 0 && g.sbn == 1);
+  const int a_m = a_kc ? (tid >> 2) : (tid & 15) * 4;
+  const int a_k = a_kc ? (tid & 3) * 4 : (tid >> 4);
+  const int b_k = b_nc ? (tid >> 4) : (tid & 3) * 4;
+  const int b_n = b_nc ? (tid & 15) * 4 : (tid >> 2);
+  Pix pa{0, 0, 0};
+  if (AM == 1 && m0 + a_m < g.M) pa = decompose(m0 + a_m, g.H, g.W);
+
+  float ra[4], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = a_kc ? m0 + a_m : m0 + a_m + e;
+      const int k = a_kc ? k0 + a_k + e : k0 + a_k;
+      Pix pm = pa;
+      if (AM == 1 && !a_kc) pm = decompose(m, g.H, g.W);
+      ra[e] = (k < kend) ? a_at<AM>(g, A, m, k, pm) : 0.f;
+    }
+    Pix pk{0, 0, 0};
+    if (BMODE == 1) {
+      const int k = k0 + b_k;  // b_nc: one k per thread
+      if (k < kend) pk = decompose(k, g.H, g.W);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = b_nc ? k0 + b_k : k0 + b_k + e;
+      const int n = b_nc ? n0 + b_n + e : n0 + b_n;
+      rb[e] = (k < kend) ? b_at<BMODE>(g, B, k, n, pk, z2) : 0.f;
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (a_kc) As[a_k + e][a_m] = ra[e];
+      else As[a_k][a_m + e] = ra[e];
+      if (b_nc) Bs[b_k][b_n + e] = rb[e];
+      else Bs[b_k + e][b_n] = rb[e];
+    }
+    __syncthreads();
+    if (k0 + BK < kend) load(k0 + BK);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kr = kk * 4 + (lane >> 4);
+      float av[2], bv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) av[i] = As[kr][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[j] = Bs[kr][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+    }
+  }
+
+  // epilogue: C/D lane map col = lane & 15, row = 4 * (lane >> 4) + r
+  const bool split = g.splits > 1;
+  float* C = g.C + z1 * g.bC1 + z2 * g.bC2;
+  const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
+  const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
+  float* part = split ? g.partial + ((long long)z * g.splits + ks) * g.M * g.N : nullptr;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
+        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (m >= g.M || n >= g.N) continue;
+        if (split) part[(long long)m * g.N + n] = acc[i][j][r];
+        else C[(long long)m * g.scm + (long long)n * g.scn] = epi(g, acc[i][j][r], m, n, R, rs);
+      }
+}
+
+__global__ void tgemm_reduce_kernel(TGemm g) {
+  const long long MN = (long long)g.M * g.N;
+  const long long total = MN * g.nz1 * g.nz2;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int z = (int)(idx / MN);
+    const long long mn = idx - (long long)z * MN;
+    const int m = (int)(mn / g.N), n = (int)(mn - (long long)m * g.N);
+    const int z1 = z / g.nz2, z2 = z - z1 * g.nz2;
+    const float* part = g.partial + (long long)z * g.splits * MN + mn;
+    float s = 0.f;
+    for (int k = 0; k < g.splits; ++k) s += part[(long long)k * MN];
+    float* C = g.C + z1 * g.bC1 + z2 * g.bC2;
+    const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
+    const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
+    C[(long long)m * g.scm + (long long)n * g.scn] = epi(g, s, m, n, R, rs);
+  }
+}
+
+template <int AM, int BMODE>
+static void launch_t(const TGemm& g, int kchunk, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((tgemm_kernel<AM, BMODE>), grid, dim3(256), 0, s, g, kchunk);
+}
+
+hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  const long long batch = (long long)g.nz1 * g.nz2;
+  int splits = 1;
+  if (g.partial && partial_cap > 0) {
+    // fill ~2048 blocks, each split at least 256 deep
+    const long long blocks = tiles * batch;
+    long long want = (2048 + blocks - 1) / blocks;
+    const long long maxk = (g.K + 255) / 256;
+    if (want > maxk) want = maxk;
+    const long long cap = (long long)(partial_cap / ((size_t)g.M * g.N * batch));
+    if (want > cap) want = cap;
+    if (want > 1) splits = (int)want;
+  }
+  int kchunk = (g.K + splits - 1) / splits;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  splits = (g.K + kchunk - 1) / kchunk;
+  if (splits < 1) splits = 1;
+  g.splits = splits;
+  dim3 grid(tiles, splits, (unsigned)batch);
+  if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, grid, s);
+  else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, grid, s);
+  else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, grid, s);
+  else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, grid, s);
+  else return hipErrorInvalidValue;
+  if (splits > 1) {
+    const long long total = (long long)g.M * g.N * batch;
+    hipLaunchKernelGGL(tgemm_reduce_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, s, g);
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------- LayerNorm
+constexpr int LN_MAXV = 8;  // C <= 512
+
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ w,
+                                                     const float* __restrict__ b, int C, long long P, int biasfree,
+                                                     float* __restrict__ y, int ldy, float* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long p = blockIdx.x * 4LL + (threadIdx.x >> 6); p < P; p += nw) {
+    float v[LN_MAXV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = c < C ? x[p * ldx + c] : 0.f;
+      s += v[i];
+    }
+    const float mu = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) q += (v[i] - mu) * (v[i] - mu);
+    }
+    const float var = wave_sum(q) / C;
+    const float sd = sqrtf(var + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) y[p * ldy + c] = biasfree ? v[i] / sd * w[c] : (v[i] - mu) / sd * w[c] + b[c];
+    }
+    if (lane == 0) {
+      stats[2 * p] = mu;
+      stats[2 * p + 1] = 1.f / sd;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, int ldd, const float* __restrict__ x,
+                                                     int ldx, const float* __restrict__ w,
+                                                     const float* __restrict__ stats, int C, long long P, int biasfree,
+                                                     const float* R, int ldr, float* dx, int lddx,
+                                                     float* __restrict__ part) {
+  __shared__ float red[4][2 * 64 * LN_MAXV];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float aw[LN_MAXV], ab[LN_MAXV];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) aw[i] = ab[i] = 0.f;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long p = blockIdx.x * 4LL + wv; p < P; p += nw) {
+    const float mu = stats[2 * p], r = stats[2 * p + 1];
+    float xv[LN_MAXV], gv[LN_MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      float d = 0.f, xx = 0.f, ww = 0.f;
+      if (c < C) {
+        d = dy[p * ldd + c];
+        xx = x[p * ldx + c];
+        ww = w[c];
+      }
+      const float xh = biasfree ? xx * r : (xx - mu) * r;
+      aw[i] += d * xh;
+      ab[i] += d;
+      gv[i] = d * ww;
+      xv[i] = xx;
+      s1 += gv[i] * (biasfree ? xx : xh);
+      s2 += gv[i];
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c >= C) continue;
+      float d;
+      if (biasfree) d = r * gv[i] - r * r * r * (xv[i] - mu) * s1;
+      else d = r * (gv[i] - s2 - (xv[i] - mu) * r * s1);
+      if (R) d += R[p * ldr + c];
+      dx[p * lddx + c] = d;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    red[wv][64 * i + lane] = aw[i];
+    red[wv][64 * LN_MAXV + 64 * i + lane] = ab[i];
+  }
+  __syncthreads();
+  const int ncol = biasfree ? C : 2 * C;
+  for (int c = threadIdx.x; c < ncol; c += blockDim.x) {
+    const int off = c < C ? c : 64 * LN_MAXV + (c - C);
+    part[(long long)blockIdx.x * ncol + c] = ((red[0][off] + red[1][off]) + red[2][off]) + red[3][off];
+  }
+}
+
+hipError_t launch_ln_fwd(const float* x, int ldx, const float* w, const float* b, int C, long long P, int biasfree,
+                         float* y, int ldy, float* stats, hipStream_t s) {
+  if (C > 64 * LN_MAXV) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3(grid_for(P, 4, 16384)), dim3(256), 0, s, x, ldx, w, b, C, P, biasfree, y,
+                     ldy, stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, const float* w, const float* stats, int C,
+                         long long P, int biasfree, const float* R, int ldr, float* dx, int lddx, float* part, int nblk,
+                         hipStream_t s) {
+  if (C > 64 * LN_MAXV) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nblk), dim3(256), 0, s, dy, ldd, x, ldx, w, stats, C, P, biasfree, R, ldr,
+                     dx, lddx, part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------- depthwise 3x3
+__global__ void dw_fwd_kernel(const float* __restrict__ in, int ldi, const float* __restrict__ w,
+                              const float* __restrict__ b, int flip, int C, int Bn, int H, int W,
+                              float* __restrict__ out, int ldo) {
+  const long long total = (long long)Bn * H * W * C;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const long long p = idx / C;
+    const int c = (int)(idx - p * C);
+    const int x = (int)(p % W);
+    const long long t = p / W;
+    const int y = (int)(t % H);
+    const long long rowbase = (t - y) * W;  // first pixel of this image
+    float acc = b ? b[c] : 0.f;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= H) continue;
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int xx = x + dx;
+        if (xx < 0 || xx >= W) continue;
+        const int tap = (dy + 1) * 3 + (dx + 1);
+        acc += w[c * 9 + (flip ? 8 - tap : tap)] * in[(rowbase + (long long)yy * W + xx) * ldi + c];
+      }
+    }
+    out[p * ldo + c] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(const float* __restrict__ dy, int ldd,
+                                                       const float* __restrict__ in, int ldi, int C, int Bn, int H,
+                                                       int W, float* __restrict__ part) {
+  const long long P = (long long)Bn * H * W;
+  const long long per = (P + gridDim.x - 1) / gridDim.x;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a[10];
+#pragma unroll
+    for (int t = 0; t < 10; ++t) a[t] = 0.f;
+    for (long long p = p0; p < p1; ++p) {
+      const float d = dy[p * ldd + c];
+      const int x = (int)(p % W);
+      const long long t = p / W;
+      const int y = (int)(t % H);
+      const long long rowbase = (t - y) * W;
+      a[9] += d;
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty) {
+        const int yy = y + ty - 1;
+        if (yy < 0 || yy >= H) continue;
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) {
+          const int xx = x + tx - 1;
+          if (xx < 0 || xx >= W) continue;
+          a[ty * 3 + tx] += d * in[(rowbase + (long long)yy * W + xx) * ldi + c];
+        }
+      }
+    }
+    float* o = part + (long long)blockIdx.x * 10 * C;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) o[c * 9 + t] = a[t];
+    o[9 * C + c] = a[9];
+  }
+}
+
+hipError_t launch_dw_fwd(const float* in, int ldi, const float* w, const float* b, int flip, int C, int Bn, int H,
+                         int W, float* out, int ldo, hipStream_t s) {
+  const long long total = (long long)Bn * H * W * C;
+  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, in, ldi, w, b, flip, C, Bn, H,
+                     W, out, ldo);
+  return hipGetLastError();
+}
+
+hipError_t launch_dw_wgrad(const float* dy, int ldd, const float* in, int ldi, int C, int Bn, int H, int W,
+                           float* part, int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(dw_wgrad_kernel, dim3(nblk), dim3(256), 0, s, dy, ldd, in, ldi, C, Bn, H, W, part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------- column reductions
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, int ldx, int ncols,
+                                                     long long rows_per_seg, int square, float* __restrict__ part) {
+  const int seg = blockIdx.y, nblk = gridDim.x;
+  const long long per = (rows_per_seg + nblk - 1) / nblk;
+  const long long r0 = blockIdx.x * per, r1 = min(rows_per_seg, r0 + per);
+  const float* xs = x + (long long)seg * rows_per_seg * ldx;
+  for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
+    float a = 0.f;
+    for (long long r = r0; r < r1; ++r) {
+      const float v = xs[r * ldx + c];
+      a += square ? v * v : v;
+    }
+    part[((long long)seg * nblk + blockIdx.x) * ncols + c] = a;
+  }
+}
+
+__global__ void part_reduce_kernel(const float* __restrict__ part, int nblk, int ncols, int pstride, int nseg,
+                                   float* out, int accumulate, float scale) {
+  const long long total = (long long)nseg * ncols;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int seg = (int)(idx / ncols), c = (int)(idx - (long long)seg * ncols);
+    const float* p = part + (long long)seg * nblk * pstride + c;
+    float a = 0.f;
+    for (int b = 0; b < nblk; ++b) a += p[(long long)b * pstride];
+    a *= scale;
+    out[idx] = accumulate ? out[idx] + a : a;
+  }
+}
+
+hipError_t launch_colsum(const float* x, int ldx, int ncols, long long rows_per_seg, int nseg, int square, float* part,
+                         int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_kernel, dim3(nblk, nseg), dim3(256), 0, s, x, ldx, ncols, rows_per_seg, square, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_part_reduce(const float* part, int nblk, int ncols, int nseg, float* out, int accumulate,
+                              float scale, hipStream_t s, int pstride) {
+  hipLaunchKernelGGL(part_reduce_kernel, dim3(grid_for((long long)nseg * ncols, 256, 4096)), dim3(256), 0, s, part,
+                     nblk, ncols, pstride > 0 ? pstride : ncols, nseg, out, accumulate, scale);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------- GELU gate
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+__global__ void gate_fwd_kernel(const float* __restrict__ y, int ldy, int hid, long long P, float* __restrict__ g,
+                                int ldg) {
+  const long long total = P * hid;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const long long p = idx / hid;
+    const int c = (int)(idx - p * hid);
+    g[p * ldg + c] = gelu_erf(y[p * ldy + c]) * y[p * ldy + hid + c];
+  }
+}
+
+__global__ void gate_bwd_kernel(const float* __restrict__ dg, int ldg, const float* __restrict__ y, int ldy, int hid,
+                                long long P, float* __restrict__ dy, int lddy) {
+  const long long total = P * hid;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const long long p = idx / hid;
+    const int c = (int)(idx - p * hid);
+    const float x1 = y[p * ldy + c], x2 = y[p * ldy + hid + c], d = dg[p * ldg + c];
+    const float cdf = 0.5f * (1.f + erff(x1 * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * expf(-0.5f * x1 * x1);
+    dy[p * lddy + c] = d * x2 * (cdf + x1 * pdf);
+    dy[p * lddy + hid + c] = d * x1 * cdf;
+  }
+}
+
+hipError_t launch_gate_fwd(const float* y, int ldy, int hid, long long P, float* g, int ldg, hipStream_t s) {
+  hipLaunchKernelGGL(gate_fwd_kernel, dim3(grid_for(P * hid, 256, 65536)), dim3(256), 0, s, y, ldy, hid, P, g, ldg);
+  return hipGetLastError();
+}
+
+hipError_t launch_gate_bwd(const float* dg, int ldg, const float* y, int ldy, int hid, long long P, float* dy, int lddy,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(gate_bwd_kernel, dim3(grid_for(P * hid, 256, 65536)), dim3(256), 0, s, dg, ldg, y, ldy, hid, P,
+                     dy, lddy);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------- MDTA core
+constexpr float kNormEps = 1e-12f;  // F.normalize eps (KDLAE_model.py:135-136)
+
+__global__ __launch_bounds__(256) void attn_softmax_kernel(const float* __restrict__ G, const float* __restrict__ sumsq,
+                                                           const float* __restrict__ temp, int C, int heads,
+                                                           float* __restrict__ Attn) {
+  const int bh = blockIdx.x, b = bh / heads, h = bh - b * heads;
+  const int Ch = C / heads;
+  const float t = temp[h];
+  const float* g = G + (long long)bh * Ch * Ch;
+  float* a = Attn + (long long)bh * Ch * Ch;
+  const float* sq = sumsq + (long long)b * 2 * C + h * Ch;
+  const float* sk = sumsq + (long long)b * 2 * C + C + h * Ch;
+  for (int i = threadIdx.x; i < Ch; i += blockDim.x) {
+    const float nq = fmaxf(sqrtf(sq[i]), kNormEps);
+    float mx = -INFINITY;
+    for (int j = 0; j < Ch; ++j) {
+      const float v = g[i * Ch + j] / (nq * fmaxf(sqrtf(sk[j]), kNormEps)) * t;
+      a[i * Ch + j] = v;
+      mx = fmaxf(mx, v);
+    }
+    float sum = 0.f;
+    for (int j = 0; j < Ch; ++j) {
+      const float e = expf(a[i * Ch + j] - mx);
+      a[i * Ch + j] = e;
+      sum += e;
+    }
+    const float inv = 1.f / sum;
+    for (int j = 0; j < Ch; ++j) a[i * Ch + j] *= inv;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__ G, const float* __restrict__ sumsq,
+                                                       const float* __restrict__ temp, const float* __restrict__ Attn,
+                                                       const float* __restrict__ dAttn, int C, int heads,
+                                                       float* __restrict__ Mq, float* __restrict__ cq,
+                                                       float* __restrict__ ck, float* __restrict__ dtemp_part) {
+  extern __shared__ float E[];  // [Ch][Ch] = dGhat * Ghat, then [256] for the dt reduction
+  const int bh = blockIdx.x, b = bh / heads, h = bh - b * heads;
+  const int Ch = C / heads;
+  const float t = temp[h];
+  const long long mo = (long long)bh * Ch * Ch;
+  const float* sq = sumsq + (long long)b * 2 * C + h * Ch;
+  const float* sk = sumsq + (long long)b * 2 * C + C + h * Ch;
+  float* red = E + Ch * Ch;
+  float dt = 0.f;
+  for (int i = threadIdx.x; i < Ch; i += blockDim.x) {
+    const float nq = fmaxf(sqrtf(sq[i]), kNormEps);
+    float rd = 0.f;
+    for (int j = 0; j < Ch; ++j) rd += dAttn[mo + i * Ch + j] * Attn[mo + i * Ch + j];
+    for (int j = 0; j < Ch; ++j) {
+      const float nk = fmaxf(sqrtf(sk[j]), kNormEps);
+      const float a = Attn[mo + i * Ch + j];
+      const float dS = a * (dAttn[mo + i * Ch + j] - rd);
+      const float gh = G[mo + i * Ch + j] / (nq * nk);
+      dt += dS * gh;
+      const float dgh = t * dS;
+      Mq[mo + i * Ch + j] = dgh / (nq * nk);
+      E[i * Ch + j] = dgh * gh;
+    }
+  }
+  red[threadIdx.x] = dt;
+  __syncthreads();
+  for (int i = threadIdx.x; i < Ch; i += blockDim.x) {
+    const float s = sqrtf(sq[i]);
+    float rsum = 0.f;
+    for (int j = 0; j < Ch; ++j) rsum += E[i * Ch + j];
+    cq[(long long)bh * Ch + i] = s >= kNormEps ? -rsum / (s * s) : 0.f;
+    const float sj = sqrtf(sk[i]);
+    float csum = 0.f;
+    for (int r = 0; r < Ch; ++r) csum += E[r * Ch + i];
+    ck[(long long)bh * Ch + i] = sj >= kNormEps ? -csum / (sj * sj) : 0.f;
+  }
+  if (threadIdx.x == 0) {
+    float a = 0.f;
+    for (int k = 0; k < (int)blockDim.x; ++k) a += red[k];
+    dtemp_part[bh] = a;
+  }
+}
+
+hipError_t launch_attn_softmax(const float* G, const float* sumsq, const float* temp, int Bn, int C, int heads,
+                               float* Attn, hipStream_t s) {
+  hipLaunchKernelGGL(attn_softmax_kernel, dim3(Bn * heads), dim3(128), 0, s, G, sumsq, temp, C, heads, Attn);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_bwd(const float* G, const float* sumsq, const float* temp, const float* Attn, const float* dAttn,
+                           int Bn, int C, int heads, float* Mq, float* cq, float* ck, float* dtemp_part,
+                           hipStream_t s) {
+  const int Ch = C / heads;
+  const size_t lds = ((size_t)Ch * Ch + 256) * sizeof(float);
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(Bn * heads), dim3(256), lds, s, G, sumsq, temp, Attn, dAttn, C, heads, Mq,
+                     cq, ck, dtemp_part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------- layout
+__global__ void shuffle_kernel(const float* __restrict__ in, int ldi, float* __restrict__ out, int ldo, int C, int Bn,
+                               int h, int w, int dir) {
+  // indexes the low-resolution side: (b, y, x, c, i, j) <-> high (b, 2y+i, 2x+j, c), low channel c*4+i*2+j
+  const long long total = (long long)Bn * h * w * C * 4;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int lc = (int)(idx % (4 * C));
+    const long long lp = idx / (4 * C);
+    const int x = (int)(lp % w);
+    const long long t = lp / w;
+    const int y = (int)(t % h);
+    const long long b = t / h;
+    const int c = lc >> 2, i = (lc >> 1) & 1, j = lc & 1;
+    const long long hp = (b * 2 * h + 2 * y + i) * (2LL * w) + 2 * x + j;
+    if (dir == 0) out[lp * ldo + lc] = in[hp * ldi + c];
+    else out[hp * ldo + c] = in[lp * ldi + lc];
+  }
+}
+
+__global__ void copy_cols_kernel(const float* __restrict__ in, int ldi, float* out, int ldo, int C, long long P,
+                                 int accumulate) {
+  const long long total = P * C;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const long long p = idx / C;
+    const int c = (int)(idx - p * C);
+    const float v = in[p * ldi + c];
+    out[p * ldo + c] = accumulate ? out[p * ldo + c] + v : v;
+  }
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ in, int C, long long HW, long long total, float* out,
+                                    int ldo, int accumulate) {
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const long long p = idx / C;  // global pixel (b*HW + s)
+    const int c = (int)(idx - p * C);
+    const long long b = p / HW, sp = p - b * HW;
+    const float v = in[(b * C + c) * HW + sp];
+    out[p * ldo + c] = accumulate ? out[p * ldo + c] + v : v;
+  }
+}
+
+__global__ void nhwc_to_nchw_kernel(const float* __restrict__ in, int ldi, const float* __restrict__ add, int C,
+                                    long long HW, long long total, float* __restrict__ out) {
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const long long sp = idx % HW;
+    const long long bc = idx / HW;
+    const long long b = bc / C;
+    const int c = (int)(bc - b * C);
+    float v = in[(b * HW + sp) * ldi + c];
+    if (add) v += add[idx];
+    out[idx] = v;
+  }
+}
+
+hipError_t launch_shuffle(const float* in, int ldi, float* out, int ldo, int C, int Bn, int h, int w, int dir,
+                          hipStream_t s) {
+  const long long total = (long long)Bn * h * w * C * 4;
+  hipLaunchKernelGGL(shuffle_kernel, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, in, ldi, out, ldo, C, Bn, h, w,
+                     dir);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_cols(const float* in, int ldi, float* out, int ldo, int C, long long P, int accumulate,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(copy_cols_kernel, dim3(grid_for(P * C, 256, 65536)), dim3(256), 0, s, in, ldi, out, ldo, C, P,
+                     accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_nchw_to_nhwc(const float* in, int C, int Bn, long long HW, float* out, int ldo, int accumulate,
+                               hipStream_t s) {
+  const long long total = (long long)Bn * HW * C;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, in, C, HW, total, out,
+                     ldo, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_nhwc_to_nchw(const float* in, int ldi, const float* add, int C, int Bn, long long HW, float* out,
+                               hipStream_t s) {
+  const long long total = (long long)Bn * HW * C;
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, in, ldi, add, C, HW,
+                     total, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------- loss, clip, AdamW
+__device__ __forceinline__ float block_sum_256(float v, float* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wv] = v;
+  __syncthreads();
+  return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+__global__ __launch_bounds__(256) void l1sr_kernel(const float* __restrict__ pred, const float* __restrict__ tgt,
+                                                   long long n, float gscale, float* __restrict__ grad,
+                                                   float* __restrict__ part) {
+  __shared__ float sh[4];
+  float a = 0.f, sb = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float d = pred[i] - tgt[i];
+    a += fabsf(d);
+    sb += fabsf((pred[i] > 0.1f ? 1.f : 0.f) - (tgt[i] > 0.1f ? 1.f : 0.f));
+    if (grad) grad[i] = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
+  }
+  a = block_sum_256(a, sh);
+  sb = block_sum_256(sb, sh);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = a;
+    part[2 * blockIdx.x + 1] = sb;
+  }
+}
+
+__global__ void l1sr_final_kernel(const float* part0, int nblk0, double n0, float wl0, float ws0, const float* part1,
+                                  int nblk1, double n1, float wl1, float ws1, float* out) {
+  if (threadIdx.x != 0) return;
+  float a0 = 0.f, s0 = 0.f, a1 = 0.f, s1 = 0.f;
+  for (int b = 0; b < nblk0; ++b) {
+    a0 += part0[2 * b];
+    s0 += part0[2 * b + 1];
+  }
+  for (int b = 0; b < nblk1; ++b) {
+    a1 += part1[2 * b];
+    s1 += part1[2 * b + 1];
+  }
+  float loss = wl0 * (float)(a0 / n0) + ws0 * (float)(s0 / n0);
+  if (part1) loss += wl1 * (float)(a1 / n1) + ws1 * (float)(s1 / n1);
+  out[0] = loss;
+}
+
+hipError_t launch_l1sr(const float* pred, const float* target, long long n, float w_l1, float* grad, float* part,
+                       int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(l1sr_kernel, dim3(nblk), dim3(256), 0, s, pred, target, n, (float)(w_l1 / (double)n), grad, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_l1sr_final(const float* part0, int nblk0, long long n0, float wl0, float ws0, const float* part1,
+                             int nblk1, long long n1, float wl1, float ws1, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(l1sr_final_kernel, dim3(1), dim3(64), 0, s, part0, nblk0, (double)n0, wl0, ws0, part1, nblk1,
+                     (double)n1, wl1, ws1, out);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, long long n, float* __restrict__ part) {
+  __shared__ float sh[4];
+  float a = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    a += g[i] * g[i];
+  a = block_sum_256(a, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = a;
+}
+
+__global__ void clip_coef_kernel(const float* part, int nblk, float gscale, float max_norm, float* state) {
+  if (threadIdx.x != 0) return;
+  double a = 0.0;
+  for (int b = 0; b < nblk; ++b) a += part[b];
+  const float norm = (float)sqrt(a) * gscale;
+  state[0] = norm;
+  float coef = 1.f;
+  if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+  state[1] = gscale * coef;
+}
+
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, long long n, const float* __restrict__ state, float lr,
+                             float beta1, float beta2, float eps, float wd, float bc1, float bc2s) {
+  const float gs = state[1];
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float gr = g[i] * gs;
+    float pv = p[i] * (1.f - lr * wd);
+    const float mv = m[i] + (1.f - beta1) * (gr - m[i]);
+    const float vv = v[i] * beta2 + (1.f - beta2) * gr * gr;
+    const float denom = sqrtf(vv) / bc2s + eps;
+    pv -= (lr / bc1) * mv / denom;
+    p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+hipError_t launch_sumsq(const float* g, long long n, float* part, int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, s, g, n, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_coef(const float* part, int nblk, float gscale, float max_norm, float* state, hipStream_t s) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, s, part, nblk, gscale, max_norm, state);
+  return hipGetLastError();
+}
+
+hipError_t launch_adamw(float* p, const float* g, float* m, float* v, long long n, const float* state, float lr,
+                        float beta1, float beta2, float eps, float wd, int step, hipStream_t s) {
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, p, g, m, v, n, state, lr, beta1,
+                     beta2, eps, wd, bc1, bc2s);
+  return hipGetLastError();
+}
+
+}  // namespace train
+}  // namespace kdlae

@@ -1,0 +1,315 @@
+"""KDLAE-T training on the MI355X HIP path.
+
+Three layers, all backed by ``libkdlae.so`` (``kdlae_tt_*`` / ``kdlae_train_*`` in include/kdlae.h):
+
+* ``TrainEngine`` — one training handle per (model, device): forward with saved activations and the
+  hand-sequenced backward of every KDLAE_teacher layer over flat parameter / gradient buffers.
+* Drop-in autograd: ``KDLAE_teacher.forward`` under grad mode routes through ``TeacherTrainFn`` and
+  ``L1LossSr`` here is an autograd-aware HIP loss, so the reference's own loop
+  (``preds = net_g(lq); l_pix = cri_pix(preds, gt); l_pix.backward(); clip_grad_norm_; opt.step()``,
+  Train/basicsr/models/image_restoration_model.py:198-218) runs unchanged with any torch optimizer.
+* ``KDLAETrainer`` — the fast path of that same loop: flat buffers end to end, the HIP L1LossSr, one
+  RCCL all-reduce of the flat gradient for DDP (base_model.py:76-82), and the fused
+  clip_grad_norm_ + AdamW kernel.  The model's parameters become views of the trainer's flat
+  buffer, so ``state_dict()``/checkpoints and the inference path always see the trained weights.
+
+There is no CPU fallback: every entry point raises on CPU tensors or a missing library.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+__all__ = ["TrainEngine", "TeacherTrainFn", "L1LossSr", "KDLAETrainer", "sync_gradients"]
+
+
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+class TrainEngine:
+    """``kdlae_tt_*`` handle for one KDLAE_teacher config on one device."""
+
+    def __init__(self, model, device: torch.device):
+        L = _lib.lib()
+        self.device = device
+        h = ctypes.c_void_p()
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        _lib.check(L.kdlae_tt_create(ctypes.byref(model._c_config()), idx, ctypes.byref(h)), "kdlae_tt_create")
+        self.handle = h
+        self._L = L
+        self.keys = []
+        for i in range(L.kdlae_tt_num_params(h)):
+            name, numel, off = ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_int64()
+            _lib.check(L.kdlae_tt_param_info(h, i, ctypes.byref(name), ctypes.byref(numel), ctypes.byref(off)),
+                       "kdlae_tt_param_info")
+            self.keys.append((name.value.decode(), int(numel.value), int(off.value)))
+        self.numel = int(L.kdlae_tt_num_floats(h))
+        names = [k for k, _, _ in self.keys]
+        sd_names = [k for k, _ in model.named_parameters()]
+        if names != sd_names:
+            raise RuntimeError("KDLAE_teacher parameters do not match the training handle's state_dict layout")
+        cfg = model._cfg
+        self.static_train = cfg["static"] == "train"
+        self.params_cat = cfg["params"] == "cat"
+        self.out_channels = cfg["out_channels"]
+        # parameters the reference forward never touches (KDLAE_model.py:315-319 when params != 'cat'):
+        # autograd leaves their .grad None and torch.optim skips them
+        unused = ("output_param.", "refinement_out.") if not self.params_cat else ()
+        self.used = [not k.startswith(unused) for k in names]
+        self.ws = None
+        self.ws_shape = None
+        self.generation = 0
+        self._dtor = L.kdlae_tt_destroy
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self._dtor(self.handle)
+        except Exception:
+            pass
+
+    def used_ranges(self):
+        """[begin, end) float ranges of the flat buffer that receive gradients (merged)."""
+        out = []
+        for (k, n, off), u in zip(self.keys, self.used):
+            if not u:
+                continue
+            if out and out[-1][1] == off:
+                out[-1][1] = off + n
+            else:
+                out.append([off, off + n])
+        return out
+
+    def flatten(self, tensors) -> torch.Tensor:
+        return torch.cat([t.detach().reshape(-1).to(torch.float32) for t in tensors])
+
+    def _workspace(self, B, H, W):
+        nbytes = int(self._L.kdlae_tt_workspace_bytes(self.handle, B, H, W))
+        if nbytes < 0:
+            _lib.check(1, "kdlae_tt_workspace_bytes")
+        if self.ws is None or self.ws.numel() < nbytes:
+            self.ws = None
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        return self.ws
+
+    def forward(self, theta, img, rate):
+        """KDLAE_teacher.forward (KDLAE_model.py:270-336) with activations kept for ``backward``."""
+        if img.device.type != "cuda":
+            raise RuntimeError("KDLAE training runs on ROCm devices only; there is no CPU fallback")
+        img = img.detach().to(torch.float32).contiguous()
+        B, _, H, W = img.shape
+        if H % 8 or W % 8:
+            raise RuntimeError(f"KDLAE_teacher needs H and W divisible by 8, got {H}x{W}")
+        rate = rate.detach().to(device=img.device, dtype=torch.float32).contiguous() if self.params_cat else None
+        oc = self.out_channels
+        hq = torch.empty((B, oc, H, W), device=img.device, dtype=torch.float32)
+        sr = torch.empty((B, oc, 2 * H, 2 * W), device=img.device, dtype=torch.float32) if self.static_train else None
+        ws = self._workspace(B, H, W)
+        rc = self._L.kdlae_tt_forward(self.handle, _vp(theta), _vp(img), _vp(rate), B, H, W, _vp(hq), _vp(sr),
+                                      _vp(ws), ws.numel(), _stream(img.device))
+        _lib.check(rc, "kdlae_tt_forward")
+        self.generation += 1
+        return hq, sr
+
+    def backward(self, theta, dhq, dsr, grad):
+        """d loss / d theta into ``grad`` (flat, overwritten) from the output gradients."""
+        dhq = dhq.detach().to(torch.float32).contiguous() if dhq is not None else None
+        dsr = dsr.detach().to(torch.float32).contiguous() if (dsr is not None and self.static_train) else None
+        rc = self._L.kdlae_tt_backward(self.handle, _vp(theta), _vp(dhq), _vp(dsr), _vp(grad), _vp(self.ws),
+                                       self.ws.numel(), _stream(grad.device))
+        _lib.check(rc, "kdlae_tt_backward")
+        return grad
+
+
+class TeacherTrainFn(torch.autograd.Function):
+    """Autograd node for one KDLAE_teacher forward on the training engine."""
+
+    @staticmethod
+    def forward(ctx, engine, img, rate, *params):
+        theta = engine.flatten(params)
+        hq, sr = engine.forward(theta, img, rate)
+        ctx.engine = engine
+        ctx.generation = engine.generation
+        ctx.theta = theta
+        ctx.shapes = [p.shape for p in params]
+        if sr is None:
+            return hq
+        return hq, sr
+
+    @staticmethod
+    def backward(ctx, dhq, dsr=None):
+        eng = ctx.engine
+        if eng.generation != ctx.generation:
+            raise RuntimeError("KDLAE_teacher: a second training forward ran before this graph's backward; "
+                               "the HIP engine keeps one set of saved activations per model and device")
+        grad = torch.empty(eng.numel, dtype=torch.float32, device=ctx.theta.device)
+        eng.backward(ctx.theta, dhq, dsr, grad)
+        grads = []
+        for (k, n, off), shape, used in zip(eng.keys, ctx.shapes, eng.used):
+            grads.append(grad[off:off + n].view(shape) if used else None)
+        return (None, None, None, *grads)
+
+
+class _L1LossSrFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, hq, gt_hq, sr, gt_sr, loss_weight):
+        L = _lib.lib()
+        dev = hq.device
+        hq = hq.detach().contiguous()
+        gt_hq = gt_hq.detach().to(torch.float32).contiguous()
+        dhq = torch.empty_like(hq)
+        dsr = None
+        if sr is not None:
+            sr = sr.detach().contiguous()
+            gt_sr = gt_sr.detach().to(torch.float32).contiguous()
+            dsr = torch.empty_like(sr)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        scratch = torch.empty(int(L.kdlae_train_l1sr_scratch_floats()), dtype=torch.float32, device=dev)
+        rc = L.kdlae_train_l1sr(_vp(hq), _vp(gt_hq), hq.numel(), _vp(sr), _vp(gt_sr),
+                                sr.numel() if sr is not None else 0, _vp(dhq), _vp(dsr), _vp(loss), _vp(scratch),
+                                _stream(dev))
+        _lib.check(rc, "kdlae_train_l1sr")
+        ctx.save_for_backward(dhq, dsr if dsr is not None else torch.empty(0, device=dev))
+        ctx.has_sr = sr is not None
+        ctx.w = loss_weight
+        return loss * loss_weight
+
+    @staticmethod
+    def backward(ctx, g):
+        dhq, dsr = ctx.saved_tensors
+        s = g * ctx.w
+        return dhq * s, None, (dsr * s if ctx.has_sr else None), None, None
+
+
+class L1LossSr(torch.nn.Module):
+    """L1LossSr (Train/basicsr/models/losses/losses.py:135-194) on the HIP path, autograd-aware.
+
+    loss = loss_weight * (0.5 l1(hq) + 0.25 l1(sr) + 0.25 (shadow(hq) + shadow(sr))), reduction 'mean'.
+    """
+
+    def __init__(self, loss_weight=1.0, reduction="mean"):
+        super().__init__()
+        if reduction not in ("none", "mean", "sum"):
+            raise ValueError(f"Unsupported reduction mode: {reduction}. Supported ones are: ['none', 'mean', 'sum']")
+        if reduction != "mean":
+            raise NotImplementedError("the HIP L1LossSr implements reduction='mean' (the KDLAET.yml setting)")
+        self.loss_weight = loss_weight
+        self.reduction = reduction
+
+    def forward(self, pred, target, weight=None, **kwargs):
+        if weight is not None:
+            raise NotImplementedError("element-wise loss weights are not used by the reference configs")
+        if pred["hq"].device.type != "cuda":
+            raise RuntimeError("L1LossSr (MI355X build) runs on ROCm devices only")
+        return _L1LossSrFn.apply(pred["hq"], target["hq"], pred.get("sr"), target.get("sr") if pred.get("sr")
+                                 is not None else None, float(self.loss_weight))
+
+
+def sync_gradients(grad: torch.Tensor, group=None) -> float:
+    """DDP gradient averaging (base_model.py:76-82) as ONE all-reduce over the flat gradient buffer.
+
+    Sums in place over the process group (RCCL on ROCm, gloo on CPU) and returns the scale
+    (1 / world size) that the clip + AdamW kernel folds in, so the mean never costs a pass."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1.0
+    ws = dist.get_world_size(group)
+    if ws == 1:
+        return 1.0
+    dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+    return 1.0 / ws
+
+
+class KDLAETrainer:
+    """ImageCleanModel.optimize_parameters for KDLAE_teacher (image_restoration_model.py:198-218).
+
+    Defaults follow Train/Denoising/Options/paper202508/KDLAET.yml: AdamW lr 1e-5,
+    weight_decay 5e-5, betas (0.2, 0.999); use_grad_clip -> clip_grad_norm_(0.01); L1LossSr."""
+
+    def __init__(self, model, lr=1e-5, weight_decay=0.5e-4, betas=(0.2, 0.999), eps=1e-8, use_grad_clip=True,
+                 max_norm=0.01, loss_weight=1.0, group=None):
+        params = list(model.parameters())
+        if not params or params[0].device.type != "cuda":
+            raise RuntimeError("KDLAETrainer: move the model to a ROCm device first (no CPU fallback)")
+        dev = params[0].device
+        self.model = model
+        self.engine = TrainEngine(model, dev)
+        eng = self.engine
+        # flat parameter buffer; the module's parameters become views of it
+        self.theta = eng.flatten(params).contiguous()
+        with torch.no_grad():
+            for (k, n, off), p in zip(eng.keys, params):
+                p.data = self.theta[off:off + n].view(p.shape)
+        self.grad = torch.zeros(eng.numel, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros_like(self.grad)
+        self.exp_avg_sq = torch.zeros_like(self.grad)
+        self.lr, self.weight_decay, self.betas, self.eps = lr, weight_decay, tuple(betas), eps
+        self.max_norm = max_norm if use_grad_clip else 0.0
+        self.loss_weight = loss_weight
+        self.group = group
+        self.step_count = 0
+        self.output = None
+        self.loss = None
+        ranges = eng.used_ranges()
+        self._ranges = (ctypes.c_int64 * (2 * len(ranges)))(*[v for r in ranges for v in r])
+        self._nranges = len(ranges) if len(ranges) != 1 or ranges[0] != [0, eng.numel] else 0
+        L = _lib.lib()
+        self._l1_scratch = torch.empty(int(L.kdlae_train_l1sr_scratch_floats()), dtype=torch.float32, device=dev)
+        self._opt_scratch = torch.empty(int(L.kdlae_train_adamw_scratch_floats()), dtype=torch.float32, device=dev)
+        self._loss = torch.zeros((), dtype=torch.float32, device=dev)
+
+    def forward_backward(self, lq: dict, gt: dict):
+        """preds = net_g(lq); l_pix = cri_pix(preds, gt); l_pix.backward()  (:198-213)."""
+        eng, L = self.engine, _lib.lib()
+        hq, sr = eng.forward(self.theta, lq["img"], lq.get("denoise_rate"))
+        self.output = {"hq": hq, "sr": sr}
+        dhq = torch.empty_like(hq)
+        dsr = torch.empty_like(sr) if sr is not None else None
+        gt_hq = gt["hq"].to(torch.float32).contiguous()
+        gt_sr = gt["sr"].to(torch.float32).contiguous() if sr is not None else None
+        rc = L.kdlae_train_l1sr(_vp(hq), _vp(gt_hq), hq.numel(), _vp(sr), _vp(gt_sr), sr.numel() if sr is not None
+                                else 0, _vp(dhq), _vp(dsr), _vp(self._loss), _vp(self._l1_scratch),
+                                _stream(hq.device))
+        _lib.check(rc, "kdlae_train_l1sr")
+        if self.loss_weight != 1.0:
+            dhq.mul_(self.loss_weight)
+            if dsr is not None:
+                dsr.mul_(self.loss_weight)
+        eng.backward(self.theta, dhq, dsr, self.grad)
+        self.loss = self._loss * self.loss_weight
+        return self.loss
+
+    def step(self, gscale: float = 1.0):
+        """clip_grad_norm_(net_g.parameters(), 0.01) + AdamW step (:215-218) over the flat buffers."""
+        self.step_count += 1
+        b1, b2 = self.betas
+        rc = _lib.lib().kdlae_train_clip_adamw(
+            _vp(self.theta), _vp(self.grad), _vp(self.exp_avg), _vp(self.exp_avg_sq), self.engine.numel,
+            float(gscale), float(self.max_norm), float(self.lr), float(b1), float(b2), float(self.eps),
+            float(self.weight_decay), self.step_count, self._ranges if self._nranges else None, self._nranges,
+            _vp(self._opt_scratch), _stream(self.theta.device))
+        _lib.check(rc, "kdlae_train_clip_adamw")
+        for eng in getattr(self.model, "_engines", {}).values():
+            eng.signature = None  # inference handles re-pack the updated weights on next use
+
+    def optimize_parameters(self, lq: dict, gt: dict):
+        """One full iteration: forward, L1LossSr, backward, DDP all-reduce, clip, AdamW."""
+        loss = self.forward_backward(lq, gt)
+        gscale = sync_gradients(self.grad, self.group)
+        self.step(gscale)
+        return loss
+
+    def grad_norm(self) -> torch.Tensor:
+        """Gradient norm of the last step (after DDP averaging, before clipping)."""
+        return self._opt_scratch[2048]
+
+    def get_current_log(self):
+        return {"l_pix": float(self.loss)} if self.loss is not None else {}

@@ -190,10 +190,71 @@ def asdqe_goldens(AM, out):
         print(name, y.ravel(), tuple(feat.shape))
 
 
+TRAIN_CASES = {
+    # name: (ctor kwargs, img shape); training step goldens
+    "train_tiny_biasfree": (dict(dim=8, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, heads=[1, 2, 4, 8],
+                                 LayerNorm_type="BiasFree", bias=False, static="train", params="cat"), (2, 3, 32, 32)),
+    "train_tiny_withbias": (dict(dim=8, num_blocks=[1, 2, 1, 1], num_refinement_blocks=1, heads=[1, 1, 2, 2],
+                                 LayerNorm_type="WithBias", bias=True, static="train", params="cat"), (1, 3, 24, 40)),
+    "train_nocat_nosr": (dict(dim=8, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, heads=[1, 1, 2, 2],
+                              LayerNorm_type="BiasFree", bias=False, static="no", params="plus"), (1, 3, 32, 24)),
+}
+TRAIN_OPT = dict(lr=1e-3, weight_decay=0.5e-4, betas=(0.2, 0.999))  # KDLAET.yml betas/wd, larger lr
+TRAIN_CLIP = 0.01
+TRAIN_SUB = 5  # flat gradients / parameter deltas are stored at every 5th element (+ per-key float64 sums)
+
+
+def train_goldens(KM, out):
+    """Loss + every parameter gradient of the reference module under L1LossSr, then the parameters
+    after two clip_grad_norm_(0.01) + AdamW steps (image_restoration_model.py:198-218).  The loss
+    is the oracle's restatement of losses.py:135-194 (basicsr is not importable here)."""
+    from oracle.train_oracle import l1sr_loss
+
+    for name, (kw, shape) in TRAIN_CASES.items():
+        t0 = time.time()
+        m = _load_hash(KM.KDLAE_teacher(**kw)).train()
+        b, c, h, w = shape
+        img = hash_images(f"img:{name}", shape)
+        rate = hash_images(f"rate:{name}", (b, 1, h, w))
+        gt_hq = hash_images(f"gt_hq:{name}", shape)
+        gt_sr = hash_images(f"gt_sr:{name}", (b, c, 2 * h, 2 * w))
+        inp = {"img": torch.from_numpy(img), "denoise_rate": torch.from_numpy(rate)}
+        gt = {"hq": torch.from_numpy(gt_hq), "sr": torch.from_numpy(gt_sr)}
+        params = list(m.parameters())
+        params0 = np.concatenate([p.detach().reshape(-1).numpy() for p in params]).astype(np.float64)
+        opt = torch.optim.AdamW(params, **TRAIN_OPT)
+        losses, norms = [], []
+        for step in range(2):
+            opt.zero_grad()
+            loss = l1sr_loss(m(inp), gt)
+            loss.backward()
+            if step == 0:
+                gl = [(p.grad if p.grad is not None else torch.zeros_like(p)).detach().reshape(-1).numpy()
+                      for p in params]
+                grad1 = np.concatenate(gl)
+                gsums = np.array([[g.astype(np.float64).sum(), np.abs(g).astype(np.float64).sum()] for g in gl])
+                used = np.array([p.grad is not None for p in params], np.uint8)
+            norms.append(float(torch.nn.utils.clip_grad_norm_(params, TRAIN_CLIP)))
+            opt.step()
+            losses.append(float(loss))
+        keys = [k for k, _ in m.named_parameters()]
+        params2 = np.concatenate([p.detach().reshape(-1).numpy() for p in params]).astype(np.float64)
+        d = dict(img=img, rate=rate, gt_hq=gt_hq, gt_sr=gt_sr, loss=np.array(losses, np.float64),
+                 norm=np.array(norms, np.float64), grad1_sub=grad1[::TRAIN_SUB].astype(np.float32), grad_sums=gsums,
+                 used=used, delta2_sub=(params2 - params0)[::TRAIN_SUB].astype(np.float32),
+                 keys=np.frombuffer(json.dumps(keys).encode(), dtype=np.uint8),
+                 cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8),
+                 opt=np.frombuffer(json.dumps(dict(TRAIN_OPT, clip=TRAIN_CLIP)).encode(), dtype=np.uint8))
+        np.savez_compressed(os.path.join(out, f"{name}.npz"), **d)
+        print(name, losses, norms, grad1.shape, f"{time.time() - t0:.1f}s")
+
+
 def main():
     KM, AM = _import_ref()
     out = HERE
-    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512"]
+    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512", "train"]
+    if "train" in which:
+        train_goldens(KM, out)
     if "teacher" in which:
         teacher_goldens(KM, out)
     if "student" in which:
