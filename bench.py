@@ -178,10 +178,90 @@ def bench_secondary(args, world, rank, dev, distributed):
         dist.destroy_process_group()
 
 
+def bench_train(args, world, rank, dev, distributed):
+    """KDLAE-T training iterations: ImageCleanModel.optimize_parameters with the
+    KDLAET.yml fixed-patch setting (batch_size_per_gpu 6, gt_size 128, AdamW lr 1e-5 wd 5e-5 betas
+    (0.2, 0.999), clip_grad_norm_ 0.01, L1LossSr); for N>1 every step all-reduces the flat gradient
+    (107.5 MB) over RCCL, as DDP does.  One step = forward + loss + backward + all-reduce + clip + AdamW."""
+    from rethink_acoustic_image_enhancement_amd.train import KDLAETrainer
+
+    B = args.batch or 6
+    H = W = args.size or 128
+    model = KDLAE_teacher(**KW)
+    load_hash_weights(model)
+    model = model.to(dev)
+    img, rate = make_inputs(1000 + rank * B, B, H, W)
+    gt_hq = torch.from_numpy(np.stack([hash_images(f"train_gt:{rank * B + i}", (3, H, W)) for i in range(B)]))
+    gt_sr = torch.from_numpy(np.stack([hash_images(f"train_gtsr:{rank * B + i}", (3, 2 * H, 2 * W))
+                                       for i in range(B)]))
+    batch = {"img": img.to(dev), "denoise_rate": rate.to(dev)}
+    gt = {"hq": gt_hq.to(dev), "sr": gt_sr.to(dev)}
+    trainer = KDLAETrainer(model)
+
+    loss = None
+    for _ in range(args.warmup):
+        loss = trainer.optimize_parameters(batch, gt)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        loss = trainer.optimize_parameters(batch, gt)
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1)
+    if distributed:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # SURVEY §8d forward FLOPs (1.9177 TFLOP per 512^2 image, linear in pixels) x 3 for fwd + dX + dW
+    flops = 3 * 1.9177e12 * (H * W) / (512 * 512) * B
+    ach = flops * args.steps / (dev_ms / 1e3) / 1e12
+    total = world * B * args.steps
+    res = {"metric": "images/sec KDLAE-T training step 128x128 patches fp32 (KDLAET.yml, SURVEY 8f rank 1)",
+           "value": round(total / elapsed, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic (hash-uniform images and targets, hash weights of the real architecture)",
+           "config": {"workload": f"KDLAE-T train step bs={B}/GPU {H}x{W} (+sr {2 * H}x{2 * W}), L1LossSr, "
+                                  "clip_grad_norm_ 0.01, AdamW", "global_batch": world * B, "per_gpu_batch": B,
+                      "parallelism": f"dp{world}" + (" (RCCL all-reduce of the flat gradient every step)"
+                                                     if distributed else "")},
+           "roofline": {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                        "kernel": "whole training step (all launches, algorithmic 3x forward FLOPs)",
+                        "algorithmic_flops_per_step": flops},
+           "final_loss": float(loss)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.kdlae_oracle import TeacherCfg
+        from oracle.train_oracle import TrainStep
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        torch.set_num_threads(threads)
+        sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        st = TrainStep(sd, TeacherCfg(**KW))
+        t0 = time.perf_counter()
+        st.step(batch["img"][:1].cpu(), batch["denoise_rate"][:1].cpu(),
+                {"hq": gt["hq"][:1].cpu(), "sr": gt["sr"][:1].cpu()})
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(1.0 / dt, 5), "unit": "images/s", "cores": threads, "kind": "port",
+                               "sample": f"1 image of the batch, one optimize_parameters step of the torch-CPU "
+                                         f"training oracle, {threads} threads, {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["t16", "s8", "a64"], default="t16",
-                    help="t16 = KDLAE-T bs16 512^2 (headline); s8 = KDLAE-S; a64 = ASDQE")
+    ap.add_argument("--workload", choices=["t16", "s8", "a64", "train"], default="t16",
+                    help="t16 = KDLAE-T bs16 512^2 (headline); s8 = KDLAE-S; a64 = ASDQE; train = KDLAE-T "
+                         "training step (KDLAET.yml 6x128^2)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -203,6 +283,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    if args.workload == "train":
+        return bench_train(args, world, rank, dev, distributed)
     if args.workload != "t16":
         return bench_secondary(args, world, rank, dev, distributed)
     H = W = args.size or 512

@@ -349,7 +349,7 @@ int block_fwd(Ctx& c, BlockRec& r) {
 
 int dw_wgrad(Ctx& c, const float* dy, const float* x, int C, int Bn, int H, int W, const std::string& n) {
   const long long P = (long long)Bn * H * W;
-  const int nb = nblk_for(P, 10LL * C, 512);
+  const int nb = tr::dw_wgrad_blocks(C, Bn, H, W, nblk_for(P, 10LL * C, 256));
   LAUNCH(tr::launch_dw_wgrad(dy, C, x, C, C, Bn, H, W, c.red, nb, c.s));
   const bool has_b = c.G(n + ".bias") != nullptr;
   LAUNCH(tr::launch_part_reduce(c.red, nb, has_b ? 10 * C : 9 * C, 1, c.G(n + ".weight"), 0, 1.f, c.s, 10 * C));

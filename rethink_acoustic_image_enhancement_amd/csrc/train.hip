@@ -8,6 +8,7 @@
 // :112-145), Train/basicsr/models/losses/losses.py:135-194 (L1LossSr),
 // Train/basicsr/models/image_restoration_model.py:198-218 (clip_grad_norm_ 0.01, optimizer step).
 #include <math.h>
+#include <stdint.h>
 
 #include "train_kernels.h"
 
@@ -33,7 +34,7 @@ static inline int grid_for(long long n, int threads, int cap = 1 << 20) {
 }
 
 // ---------------------------------------------------------------------------------------------- GEMM
-constexpr int BM = 64, BN = 64, BK = 16, LDP = BM + 4;
+constexpr int BM = 64, BN = 64, BK = 32, LDP = BM + 4;
 
 struct Pix { int b, y, x; };
 
@@ -55,6 +56,16 @@ __device__ __forceinline__ float a_at(const TGemm& g, const float* A, int m, int
   const int yy = pm.y + (tap / 3 - 1) * g.dil, xx = pm.x + (tap % 3 - 1) * g.dil;
   if (yy < 0 || yy >= g.H || xx < 0 || xx >= g.W) return 0.f;
   return A[(((long long)pm.b * g.H + yy) * g.W + xx) * g.lda + c];
+}
+
+// address of A(m, k..k+3) when those four are contiguous (null -> out of image: zeros)
+template <int AM>
+__device__ __forceinline__ const float* a_vec_ptr(const TGemm& g, const float* A, int m, int k, const Pix& pm) {
+  if (AM == 0) return A + (long long)m * g.sam + k;
+  const int tap = k / g.Cg, c = k - tap * g.Cg;
+  const int yy = pm.y + (tap / 3 - 1) * g.dil, xx = pm.x + (tap % 3 - 1) * g.dil;
+  if (yy < 0 || yy >= g.H || xx < 0 || xx >= g.W) return nullptr;
+  return A + (((long long)pm.b * g.H + yy) * g.W + xx) * g.lda + c;
 }
 
 template <int BMODE>
@@ -81,10 +92,19 @@ __device__ __forceinline__ float epi(const TGemm& g, float acc, int m, int n, co
   return v;
 }
 
+__device__ __forceinline__ void put4(float* d, const float4& v) { *reinterpret_cast<float4*>(d) = v; }
+__device__ __forceinline__ float4 get4(const float* s) { return *reinterpret_cast<const float4*>(s); }
+
+// 64x64 block tile, BK = 32, 4 waves of 32x32 (2x2 v_mfma_f32_16x16x4_f32 tiles).  Global -> register
+// prefetch of the next k-tile overlaps the MFMAs of the current one; 8 consecutive elements per thread
+// along the contiguous operand dimension, as two float4 loads when `vec` flags say they are aligned.
+// The C tile is staged through LDS so stores go out as whole 256 B rows.
+// flags: 1 = A vector loads, 2 = B vector loads, 4 = C row stores (scn == 1, aligned)
 template <int AM, int BMODE>
-__global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk) {
-  __shared__ float As[BK][LDP];
-  __shared__ float Bs[BK][LDP];
+__global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int flags) {
+  __shared__ float smem[2 * BK * LDP];
+  float (*As)[LDP] = reinterpret_cast<float (*)[LDP]>(smem);
+  float (*Bs)[LDP] = reinterpret_cast<float (*)[LDP]>(smem + BK * LDP);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv & 1, wn = wv >> 1;
   const int tiles_n = (g.N + BN - 1) / BN;
@@ -94,37 +114,83 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk) {
   const float* B = g.B + (BMODE == 1 ? z1 * g.bB1 : z1 * g.bB1 + z2 * g.bB2);
   const int ks = blockIdx.y;
   const int kbeg = ks * kchunk, kend = min(g.K, kbeg + kchunk);
+  const bool vecA = flags & 1, vecB = flags & 2;
 
-  // load mappings (uniform per launch)
-  const bool a_kc = (AM == 1) || (g.sak == 1);           // k contiguous in memory
+  // per-thread 8-element runs: a_kc -> (row m, k..k+7); else (k, m..m+7).  Same for B.
+  const bool a_kc = (AM == 1) || (g.sak == 1);
   const bool b_nc = (BMODE == 1) || (BMODE == 0 && g.sbn == 1);
-  const int a_m = a_kc ? (tid >> 2) : (tid & 15) * 4;
-  const int a_k = a_kc ? (tid & 3) * 4 : (tid >> 4);
-  const int b_k = b_nc ? (tid >> 4) : (tid & 3) * 4;
-  const int b_n = b_nc ? (tid & 15) * 4 : (tid >> 2);
+  const int a_m = a_kc ? (tid >> 2) : (tid & 7) * 8;
+  const int a_k = a_kc ? (tid & 3) * 8 : (tid >> 3);
+  const int b_k = b_nc ? (tid >> 3) : (tid & 3) * 8;
+  const int b_n = b_nc ? (tid & 7) * 8 : (tid >> 2);
   Pix pa{0, 0, 0};
   if (AM == 1 && m0 + a_m < g.M) pa = decompose(m0 + a_m, g.H, g.W);
 
-  float ra[4], rb[4];
+  float ra[8], rb[8];
   auto load = [&](int k0) {
+    if (a_kc) {
+      const int m = m0 + a_m;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = a_kc ? m0 + a_m : m0 + a_m + e;
-      const int k = a_kc ? k0 + a_k + e : k0 + a_k;
-      Pix pm = pa;
-      if (AM == 1 && !a_kc) pm = decompose(m, g.H, g.W);
-      ra[e] = (k < kend) ? a_at<AM>(g, A, m, k, pm) : 0.f;
-    }
-    Pix pk{0, 0, 0};
-    if (BMODE == 1) {
-      const int k = k0 + b_k;  // b_nc: one k per thread
-      if (k < kend) pk = decompose(k, g.H, g.W);
-    }
+      for (int h = 0; h < 2; ++h) {
+        const int k = k0 + a_k + 4 * h;
+        if (vecA && m < g.M && k + 3 < kend) {
+          const float* ptr = a_vec_ptr<AM>(g, A, m, k, pa);
+          const float4 v = ptr ? get4(ptr) : make_float4(0.f, 0.f, 0.f, 0.f);
+          ra[4 * h] = v.x; ra[4 * h + 1] = v.y; ra[4 * h + 2] = v.z; ra[4 * h + 3] = v.w;
+        } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = b_nc ? k0 + b_k : k0 + b_k + e;
-      const int n = b_nc ? n0 + b_n + e : n0 + b_n;
-      rb[e] = (k < kend) ? b_at<BMODE>(g, B, k, n, pk, z2) : 0.f;
+          for (int e = 0; e < 4; ++e) ra[4 * h + e] = (k + e < kend) ? a_at<AM>(g, A, m, k + e, pa) : 0.f;
+        }
+      }
+    } else {
+      const int k = k0 + a_k;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = m0 + a_m + 4 * h;
+        if (vecA && k < kend && m + 3 < g.M) {
+          const float4 v = get4(A + (long long)k * g.sak + m);
+          ra[4 * h] = v.x; ra[4 * h + 1] = v.y; ra[4 * h + 2] = v.z; ra[4 * h + 3] = v.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ra[4 * h + e] = (k < kend) ? a_at<AM>(g, A, m + e, k, pa) : 0.f;
+        }
+      }
+    }
+    if (b_nc) {
+      const int k = k0 + b_k;
+      Pix pk{0, 0, 0};
+      if (BMODE == 1 && k < kend) pk = decompose(k, g.H, g.W);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int n = n0 + b_n + 4 * h;
+        if (vecB && k < kend && n + 3 < g.N) {
+          const float* ptr = nullptr;
+          if (BMODE == 0) ptr = B + (long long)k * g.sbk + n;
+          else {
+            const int yy = pk.y + (z2 / 3 - 1) * g.dil, xx = pk.x + (z2 % 3 - 1) * g.dil;
+            if (yy >= 0 && yy < g.H && xx >= 0 && xx < g.W) ptr = B + (((long long)pk.b * g.H + yy) * g.W + xx) * g.ldb + n;
+          }
+          const float4 v = ptr ? get4(ptr) : make_float4(0.f, 0.f, 0.f, 0.f);
+          rb[4 * h] = v.x; rb[4 * h + 1] = v.y; rb[4 * h + 2] = v.z; rb[4 * h + 3] = v.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rb[4 * h + e] = (k < kend) ? b_at<BMODE>(g, B, k, n + e, pk, z2) : 0.f;
+        }
+      }
+    } else {
+      const int n = n0 + b_n;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = k0 + b_k + 4 * h;
+        if (BMODE == 0 && vecB && n < g.N && k + 3 < kend) {
+          const float4 v = get4(B + (long long)n * g.sbn + k);
+          rb[4 * h] = v.x; rb[4 * h + 1] = v.y; rb[4 * h + 2] = v.z; rb[4 * h + 3] = v.w;
+        } else {
+          Pix pk{0, 0, 0};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rb[4 * h + e] = (k + e < kend) ? b_at<BMODE>(g, B, k + e, n, pk, z2) : 0.f;
+        }
+      }
     }
   };
 
@@ -138,7 +204,7 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk) {
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < 8; ++e) {
       if (a_kc) As[a_k + e][a_m] = ra[e];
       else As[a_k][a_m + e] = ra[e];
       if (b_nc) Bs[b_k][b_n + e] = rb[e];
@@ -147,7 +213,7 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk) {
     __syncthreads();
     if (k0 + BK < kend) load(k0 + BK);
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
+    for (int kk = 0; kk < BK / 4; ++kk) {
       const int kr = kk * 4 + (lane >> 4);
       float av[2], bv[2];
 #pragma unroll
@@ -167,6 +233,48 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk) {
   const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
   const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
   float* part = split ? g.partial + ((long long)z * g.splits + ks) * g.M * g.N : nullptr;
+  if (flags & 4) {
+    // stage the 64x64 tile in LDS, then each thread writes 16 consecutive columns of one row
+    constexpr int LDC = BN + 4;
+    float* Cs = smem;  // 64 x 68 floats <= 2 * BK * LDP
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wm * 32 + i * 16 + 4 * (lane >> 4) + r) * LDC + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    const int row = tid >> 2, cb = (tid & 3) * 16;
+    const int m = m0 + row;
+    if (m < g.M) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + cb + 4 * q;
+        if (n >= g.N) break;
+        float4 v = get4(Cs + row * LDC + cb + 4 * q);
+        if (n + 3 < g.N) {
+          if (split) {
+            put4(part + (long long)m * g.N + n, v);
+          } else {
+            v.x = epi(g, v.x, m, n, R, rs);
+            v.y = epi(g, v.y, m, n + 1, R, rs);
+            v.z = epi(g, v.z, m, n + 2, R, rs);
+            v.w = epi(g, v.w, m, n + 3, R, rs);
+            put4(C + (long long)m * g.scm + n, v);
+          }
+        } else {
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+          for (int e = 0; e < 4 && n + e < g.N; ++e) {
+            if (split) part[(long long)m * g.N + n + e] = vv[e];
+            else C[(long long)m * g.scm + n + e] = epi(g, vv[e], m, n + e, R, rs);
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -181,29 +289,48 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk) {
       }
 }
 
-__global__ void tgemm_reduce_kernel(TGemm g) {
+// split-K reduce: a block owns 64 consecutive outputs of one batch entry; 16 waves each sum every 16th
+// split (4 independent chains), combined in fixed order, then the epilogue -> deterministic
+__global__ __launch_bounds__(1024) void tgemm_reduce_kernel(TGemm g) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long long MN = (long long)g.M * g.N;
-  const long long total = MN * g.nz1 * g.nz2;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const int z = (int)(idx / MN);
-    const long long mn = idx - (long long)z * MN;
-    const int m = (int)(mn / g.N), n = (int)(mn - (long long)m * g.N);
-    const int z1 = z / g.nz2, z2 = z - z1 * g.nz2;
+  const long long mn = (long long)blockIdx.x * 64 + lane;
+  const int z = blockIdx.y;
+  float a = 0.f;
+  if (mn < MN) {
     const float* part = g.partial + (long long)z * g.splits * MN + mn;
-    float s = 0.f;
-    for (int k = 0; k < g.splits; ++k) s += part[(long long)k * MN];
-    float* C = g.C + z1 * g.bC1 + z2 * g.bC2;
-    const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
-    const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
-    C[(long long)m * g.scm + (long long)n * g.scn] = epi(g, s, m, n, R, rs);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int k = wv;
+    for (; k + 48 < g.splits; k += 64) {
+      a0 += part[(long long)k * MN];
+      a1 += part[(long long)(k + 16) * MN];
+      a2 += part[(long long)(k + 32) * MN];
+      a3 += part[(long long)(k + 48) * MN];
+    }
+    for (; k < g.splits; k += 16) a0 += part[(long long)k * MN];
+    a = (a0 + a1) + (a2 + a3);
   }
+  red[wv][lane] = a;
+  __syncthreads();
+  if (wv != 0 || mn >= MN) return;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += red[k][lane];
+  const int m = (int)(mn / g.N), n = (int)(mn - (long long)m * g.N);
+  const int z1 = z / g.nz2, z2 = z - z1 * g.nz2;
+  float* C = g.C + z1 * g.bC1 + z2 * g.bC2;
+  const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
+  const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
+  C[(long long)m * g.scm + (long long)n * g.scn] = epi(g, s, m, n, R, rs);
 }
 
 template <int AM, int BMODE>
-static void launch_t(const TGemm& g, int kchunk, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((tgemm_kernel<AM, BMODE>), grid, dim3(256), 0, s, g, kchunk);
+static void launch_t(const TGemm& g, int kchunk, int flags, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((tgemm_kernel<AM, BMODE>), grid, dim3(256), 0, s, g, kchunk, flags);
 }
+
+static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
@@ -225,15 +352,33 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   splits = (g.K + kchunk - 1) / kchunk;
   if (splits < 1) splits = 1;
   g.splits = splits;
+  // vector-load / row-store eligibility (all offsets multiples of 4 floats, bases 16 B aligned)
+  auto m4 = [](long long v) { return (v & 3) == 0; };
+  int flags = 0;
+  const bool a_kc = g.amode == 1 || g.sak == 1;
+  if (g.amode == 1) {
+    if (al16(g.A) && m4(g.lda) && g.Cg % 4 == 0 && m4(g.bA1) && m4(g.bA2)) flags |= 1;
+  } else if (al16(g.A) && m4(g.bA1) && m4(g.bA2) && (a_kc ? m4(g.sam) : (g.sam == 1 && m4(g.sak)))) {
+    flags |= 1;
+  }
+  if (g.bmode == 1) {
+    if (al16(g.B) && m4(g.ldb) && m4(g.bB1)) flags |= 2;
+  } else if (g.bmode == 0 && al16(g.B) && m4(g.bB1) && m4(g.bB2) &&
+             ((g.sbn == 1 && m4(g.sbk)) || (g.sbk == 1 && m4(g.sbn)))) {
+    flags |= 2;
+  }
+  if (splits > 1 ? (g.N % 4 == 0 && al16(g.partial))
+                 : (g.scn == 1 && al16(g.C) && m4(g.scm) && m4(g.bC1) && m4(g.bC2)))
+    flags |= 4;
   dim3 grid(tiles, splits, (unsigned)batch);
-  if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, grid, s);
-  else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, grid, s);
-  else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, grid, s);
-  else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, grid, s);
+  if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, flags, grid, s);
+  else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, flags, grid, s);
+  else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, grid, s);
+  else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, flags, grid, s);
   else return hipErrorInvalidValue;
   if (splits > 1) {
-    const long long total = (long long)g.M * g.N * batch;
-    hipLaunchKernelGGL(tgemm_reduce_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, s, g);
+    const long long MN = (long long)g.M * g.N;
+    hipLaunchKernelGGL(tgemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64), (unsigned)batch), dim3(1024), 0, s, g);
   }
   return hipGetLastError();
 }
@@ -352,126 +497,213 @@ hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, cons
 }
 
 // ---------------------------------------------------------------------------------------------- depthwise 3x3
-__global__ void dw_fwd_kernel(const float* __restrict__ in, int ldi, const float* __restrict__ w,
-                              const float* __restrict__ b, int flip, int C, int Bn, int H, int W,
-                              float* __restrict__ out, int ldo) {
-  const long long total = (long long)Bn * H * W * C;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const long long p = idx / C;
-    const int c = (int)(idx - p * C);
-    const int x = (int)(p % W);
-    const long long t = p / W;
-    const int y = (int)(t % H);
-    const long long rowbase = (t - y) * W;  // first pixel of this image
-    float acc = b ? b[c] : 0.f;
+// Row sweep: a wave owns 64 channels (one per lane, 256 B coalesced per pixel) of a 64-pixel row
+// segment and slides a 3x3 register window along x, so each output costs 3 new loads instead of 9.
+constexpr int DW_SEG = 64;
+
+struct DwWin {
+  float v[3][3];  // [column x-1, x, x+1][row y-1, y, y+1]
+};
+
+__device__ __forceinline__ void dw_load_col(const float* __restrict__ in, int ldi, long long img0, int y, int x, int H,
+                                            int W, int c, bool live, float (&col)[3]) {
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int yy = y + dy;
-      if (yy < 0 || yy >= H) continue;
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int xx = x + dx;
-        if (xx < 0 || xx >= W) continue;
-        const int tap = (dy + 1) * 3 + (dx + 1);
-        acc += w[c * 9 + (flip ? 8 - tap : tap)] * in[(rowbase + (long long)yy * W + xx) * ldi + c];
-      }
-    }
-    out[p * ldo + c] = acc;
+  for (int r = 0; r < 3; ++r) {
+    const int yy = y + r - 1;
+    col[r] = (live && x >= 0 && x < W && yy >= 0 && yy < H) ? in[(img0 + (long long)yy * W + x) * ldi + c] : 0.f;
   }
 }
 
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(const float* __restrict__ dy, int ldd,
-                                                       const float* __restrict__ in, int ldi, int C, int Bn, int H,
-                                                       int W, float* __restrict__ part) {
-  const long long P = (long long)Bn * H * W;
-  const long long per = (P + gridDim.x - 1) / gridDim.x;
-  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a[10];
+__global__ __launch_bounds__(256) void dw_row_fwd_kernel(const float* __restrict__ in, int ldi,
+                                                         const float* __restrict__ w, const float* __restrict__ b,
+                                                         int flip, int C, int Bn, int H, int W, int nrs,
+                                                         float* __restrict__ out, int ldo) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrs) return;
+  const int c = blockIdx.y * 64 + lane;
+  const bool live = c < C;
+  const int nsx = (W + DW_SEG - 1) / DW_SEG;
+  const int xs = r % nsx, row = r / nsx;
+  const int y = row % H, bi = row / H;
+  const long long img0 = (long long)bi * H * W;
+  const int x0 = xs * DW_SEG, x1 = min(W, x0 + DW_SEG);
+  float wr[9];
 #pragma unroll
-    for (int t = 0; t < 10; ++t) a[t] = 0.f;
-    for (long long p = p0; p < p1; ++p) {
-      const float d = dy[p * ldd + c];
-      const int x = (int)(p % W);
-      const long long t = p / W;
-      const int y = (int)(t % H);
-      const long long rowbase = (t - y) * W;
-      a[9] += d;
+  for (int k = 0; k < 9; ++k) wr[k] = live ? w[c * 9 + (flip ? 8 - k : k)] : 0.f;
+  const float bias = (live && b) ? b[c] : 0.f;
+  DwWin win;
+  dw_load_col(in, ldi, img0, y, x0 - 1, H, W, c, live, win.v[0]);
+  dw_load_col(in, ldi, img0, y, x0, H, W, c, live, win.v[1]);
+  for (int x = x0; x < x1; ++x) {
+    dw_load_col(in, ldi, img0, y, x + 1, H, W, c, live, win.v[2]);
+    float acc = bias;
 #pragma unroll
-      for (int ty = 0; ty < 3; ++ty) {
-        const int yy = y + ty - 1;
-        if (yy < 0 || yy >= H) continue;
+    for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-        for (int tx = 0; tx < 3; ++tx) {
-          const int xx = x + tx - 1;
-          if (xx < 0 || xx >= W) continue;
-          a[ty * 3 + tx] += d * in[(rowbase + (long long)yy * W + xx) * ldi + c];
-        }
-      }
+      for (int tx = 0; tx < 3; ++tx) acc += wr[ty * 3 + tx] * win.v[tx][ty];
+    if (live) out[(img0 + (long long)y * W + x) * ldo + c] = acc;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      win.v[0][k] = win.v[1][k];
+      win.v[1][k] = win.v[2][k];
     }
-    float* o = part + (long long)blockIdx.x * 10 * C;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) o[c * 9 + t] = a[t];
-    o[9 * C + c] = a[9];
   }
 }
+
+// dW partials: block (chunk, channel group) sums dy[p,c] * in[p + off_t, c] (t < 9) and dy[p,c] (bias)
+// over its row segments; 4 waves combined in fixed order -> part[chunk][c*9 + t], part[chunk][9C + c].
+__global__ __launch_bounds__(256) void dw_row_wgrad_kernel(const float* __restrict__ dy, int ldd,
+                                                           const float* __restrict__ in, int ldi, int C, int Bn,
+                                                           int H, int W, int nrs, int per,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4][10][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane;
+  const bool live = c < C;
+  const int nsx = (W + DW_SEG - 1) / DW_SEG;
+  float acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0.f;
+  const int r0 = blockIdx.x * per, r1 = min(nrs, r0 + per);
+  for (int r = r0 + wv; r < r1; r += 4) {
+    const int xs = r % nsx, row = r / nsx;
+    const int y = row % H, bi = row / H;
+    const long long img0 = (long long)bi * H * W;
+    const int x0 = xs * DW_SEG, x1 = min(W, x0 + DW_SEG);
+    DwWin win;
+    dw_load_col(in, ldi, img0, y, x0 - 1, H, W, c, live, win.v[0]);
+    dw_load_col(in, ldi, img0, y, x0, H, W, c, live, win.v[1]);
+    for (int x = x0; x < x1; ++x) {
+      dw_load_col(in, ldi, img0, y, x + 1, H, W, c, live, win.v[2]);
+      const float d = live ? dy[(img0 + (long long)y * W + x) * ldd + c] : 0.f;
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) acc[ty * 3 + tx] += d * win.v[tx][ty];
+      acc[9] += d;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        win.v[0][k] = win.v[1][k];
+        win.v[1][k] = win.v[2][k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) red[wv][k][lane] = acc[k];
+  __syncthreads();
+  if (wv == 0 && live) {
+    float* o = part + (long long)blockIdx.x * 10 * C;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const float s = ((red[0][k][lane] + red[1][k][lane]) + red[2][k][lane]) + red[3][k][lane];
+      if (k < 9) o[c * 9 + k] = s;
+      else o[9 * C + c] = s;
+    }
+  }
+}
+
+static int dw_rowsegs(int Bn, int H, int W) { return Bn * H * ((W + DW_SEG - 1) / DW_SEG); }
 
 hipError_t launch_dw_fwd(const float* in, int ldi, const float* w, const float* b, int flip, int C, int Bn, int H,
                          int W, float* out, int ldo, hipStream_t s) {
-  const long long total = (long long)Bn * H * W * C;
-  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, in, ldi, w, b, flip, C, Bn, H,
-                     W, out, ldo);
+  const int nrs = dw_rowsegs(Bn, H, W);
+  hipLaunchKernelGGL(dw_row_fwd_kernel, dim3((nrs + 3) / 4, (C + 63) / 64), dim3(256), 0, s, in, ldi, w, b, flip, C,
+                     Bn, H, W, nrs, out, ldo);
   return hipGetLastError();
+}
+
+int dw_wgrad_blocks(int C, int Bn, int H, int W, int max_blocks) {
+  const int nrs = dw_rowsegs(Bn, H, W);
+  int nb = (nrs + 3) / 4;  // at least 4 row segments (one per wave) per block
+  if (nb > max_blocks) nb = max_blocks;
+  if (nb < 1) nb = 1;
+  const int per = (nrs + nb - 1) / nb;
+  return (nrs + per - 1) / per;
 }
 
 hipError_t launch_dw_wgrad(const float* dy, int ldd, const float* in, int ldi, int C, int Bn, int H, int W,
                            float* part, int nblk, hipStream_t s) {
-  hipLaunchKernelGGL(dw_wgrad_kernel, dim3(nblk), dim3(256), 0, s, dy, ldd, in, ldi, C, Bn, H, W, part);
+  const int nrs = dw_rowsegs(Bn, H, W);
+  const int per = (nrs + nblk - 1) / nblk;
+  if ((nrs + per - 1) / per != nblk) return hipErrorInvalidValue;  // nblk must come from dw_wgrad_blocks
+  hipLaunchKernelGGL(dw_row_wgrad_kernel, dim3(nblk, (C + 63) / 64), dim3(256), 0, s, dy, ldd, in, ldi, C, Bn, H, W,
+                     nrs, per, part);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------- column reductions
+// block (column group of 64, row chunk, segment): 4 waves take every 4th row, combined in fixed order
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, int ldx, int ncols,
                                                      long long rows_per_seg, int square, float* __restrict__ part) {
-  const int seg = blockIdx.y, nblk = gridDim.x;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, seg = blockIdx.z, nblk = gridDim.y;
   const long long per = (rows_per_seg + nblk - 1) / nblk;
-  const long long r0 = blockIdx.x * per, r1 = min(rows_per_seg, r0 + per);
+  const long long r0 = blockIdx.y * per, r1 = min(rows_per_seg, r0 + per);
   const float* xs = x + (long long)seg * rows_per_seg * ldx;
-  for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
-    float a = 0.f;
-    for (long long r = r0; r < r1; ++r) {
-      const float v = xs[r * ldx + c];
-      a += square ? v * v : v;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < ncols) {
+    long long r = r0 + wv;
+    for (; r + 4 < r1; r += 8) {
+      const float v0 = xs[r * ldx + c], v1 = xs[(r + 4) * ldx + c];
+      a0 += square ? v0 * v0 : v0;
+      a1 += square ? v1 * v1 : v1;
     }
-    part[((long long)seg * nblk + blockIdx.x) * ncols + c] = a;
+    for (; r < r1; r += 4) {
+      const float v = xs[r * ldx + c];
+      a0 += square ? v * v : v;
+    }
   }
+  red[wv][lane] = a0 + a1;
+  __syncthreads();
+  if (wv == 0 && c < ncols)
+    part[((long long)seg * nblk + blockIdx.y) * ncols + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
-__global__ void part_reduce_kernel(const float* __restrict__ part, int nblk, int ncols, int pstride, int nseg,
-                                   float* out, int accumulate, float scale) {
-  const long long total = (long long)nseg * ncols;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const int seg = (int)(idx / ncols), c = (int)(idx - (long long)seg * ncols);
+__global__ __launch_bounds__(1024) void part_reduce_kernel(const float* __restrict__ part, int nblk, int ncols,
+                                                           int pstride, int nseg, float* out, int accumulate,
+                                                           float scale) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, seg = blockIdx.y;
+  float a = 0.f;
+  if (c < ncols) {
     const float* p = part + (long long)seg * nblk * pstride + c;
-    float a = 0.f;
-    for (int b = 0; b < nblk; ++b) a += p[(long long)b * pstride];
-    a *= scale;
-    out[idx] = accumulate ? out[idx] + a : a;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int b = wv;
+    for (; b + 48 < nblk; b += 64) {
+      a0 += p[(long long)b * pstride];
+      a1 += p[(long long)(b + 16) * pstride];
+      a2 += p[(long long)(b + 32) * pstride];
+      a3 += p[(long long)(b + 48) * pstride];
+    }
+    for (; b < nblk; b += 16) a0 += p[(long long)b * pstride];
+    a = (a0 + a1) + (a2 + a3);
+  }
+  red[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0 && c < ncols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][lane];
+    s *= scale;
+    const long long o = (long long)seg * ncols + c;
+    out[o] = accumulate ? out[o] + s : s;
   }
 }
 
 hipError_t launch_colsum(const float* x, int ldx, int ncols, long long rows_per_seg, int nseg, int square, float* part,
                          int nblk, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_kernel, dim3(nblk, nseg), dim3(256), 0, s, x, ldx, ncols, rows_per_seg, square, part);
+  hipLaunchKernelGGL(colsum_kernel, dim3((ncols + 63) / 64, nblk, nseg), dim3(256), 0, s, x, ldx, ncols,
+                     rows_per_seg, square, part);
   return hipGetLastError();
 }
 
 hipError_t launch_part_reduce(const float* part, int nblk, int ncols, int nseg, float* out, int accumulate,
                               float scale, hipStream_t s, int pstride) {
-  hipLaunchKernelGGL(part_reduce_kernel, dim3(grid_for((long long)nseg * ncols, 256, 4096)), dim3(256), 0, s, part,
-                     nblk, ncols, pstride > 0 ? pstride : ncols, nseg, out, accumulate, scale);
+  hipLaunchKernelGGL(part_reduce_kernel, dim3((ncols + 63) / 64, nseg), dim3(1024), 0, s, part, nblk, ncols,
+                     pstride > 0 ? pstride : ncols, nseg, out, accumulate, scale);
   return hipGetLastError();
 }
 

@@ -54,7 +54,9 @@ hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, cons
 // w[c][8-t] (dX of the same conv).
 hipError_t launch_dw_fwd(const float* in, int ldi, const float* w, const float* b, int flip, int C, int Bn, int H,
                          int W, float* out, int ldo, hipStream_t s);
-// dW partials: part[blk][c][10] = (sum_p dy[p,c] in[p+off_t,c] for t<9, sum_p dy[p,c]) over the block's rows
+// dW partials over nblk = dw_wgrad_blocks(...) row chunks: part[blk][c*9 + t] = sum dy[p,c] in[p+off_t,c],
+// part[blk][9C + c] = sum dy[p,c]
+int dw_wgrad_blocks(int C, int Bn, int H, int W, int max_blocks);
 hipError_t launch_dw_wgrad(const float* dy, int ldd, const float* in, int ldi, int C, int Bn, int H, int W,
                            float* part, int nblk, hipStream_t s);
 
