@@ -34,7 +34,7 @@ static inline int grid_for(long long n, int threads, int cap = 1 << 20) {
 }
 
 // ---------------------------------------------------------------------------------------------- GEMM
-constexpr int BM = 64, BN = 64, BK = 32, LDP = BM + 4;
+constexpr int BN = 64, BK = 32, LDP = BN + 4;
 
 struct Pix { int b, y, x; };
 
@@ -95,20 +95,23 @@ __device__ __forceinline__ float epi(const TGemm& g, float acc, int m, int n, co
 __device__ __forceinline__ void put4(float* d, const float4& v) { *reinterpret_cast<float4*>(d) = v; }
 __device__ __forceinline__ float4 get4(const float* s) { return *reinterpret_cast<const float4*>(s); }
 
-// 64x64 block tile, BK = 32, 4 waves of 32x32 (2x2 v_mfma_f32_16x16x4_f32 tiles).  Global -> register
-// prefetch of the next k-tile overlaps the MFMAs of the current one; 8 consecutive elements per thread
-// along the contiguous operand dimension, as two float4 loads when `vec` flags say they are aligned.
-// The C tile is staged through LDS so stores go out as whole 256 B rows.
+// (64*RM)x64 block tile, BK = 32, 4 waves of (32*RM)x32 (2RM x 2 v_mfma_f32_16x16x4_f32 tiles).
+// Global -> register prefetch of the next k-tile overlaps the MFMAs of the current one; 8 consecutive
+// elements per thread along the contiguous operand dimension, as two float4 loads when the `flags`
+// say they are aligned.  The C tile is staged through LDS so stores go out as whole 256 B rows.
+// RM = 2 (128-row tiles) halves the B-operand LDS traffic per MFMA on the tall activation GEMMs.
 // flags: 1 = A vector loads, 2 = B vector loads, 4 = C row stores (scn == 1, aligned)
-template <int AM, int BMODE>
+template <int AM, int BMODE, int RM>
 __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int flags) {
-  __shared__ float smem[2 * BK * LDP];
-  float (*As)[LDP] = reinterpret_cast<float (*)[LDP]>(smem);
-  float (*Bs)[LDP] = reinterpret_cast<float (*)[LDP]>(smem + BK * LDP);
+  constexpr int BMr = 64 * RM, LDA_S = BMr + 4, LDC = BN + 4;
+  constexpr int SM_LOOP = BK * LDA_S + BK * LDP, SM_EPI = BMr * LDC;
+  __shared__ float smem[SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI];
+  float (*As)[LDA_S] = reinterpret_cast<float (*)[LDA_S]>(smem);
+  float (*Bs)[LDP] = reinterpret_cast<float (*)[LDP]>(smem + BK * LDA_S);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv & 1, wn = wv >> 1;
   const int tiles_n = (g.N + BN - 1) / BN;
-  const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
+  const int m0 = (blockIdx.x / tiles_n) * BMr, n0 = (blockIdx.x % tiles_n) * BN;
   const int z = blockIdx.z, z1 = z / g.nz2, z2 = z - z1 * g.nz2;
   const float* A = g.A + z1 * g.bA1 + z2 * g.bA2;
   const float* B = g.B + (BMODE == 1 ? z1 * g.bB1 : z1 * g.bB1 + z2 * g.bB2);
@@ -123,36 +126,44 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
   const int a_k = a_kc ? (tid & 3) * 8 : (tid >> 3);
   const int b_k = b_nc ? (tid >> 3) : (tid & 3) * 8;
   const int b_n = b_nc ? (tid & 7) * 8 : (tid >> 2);
-  Pix pa{0, 0, 0};
-  if (AM == 1 && m0 + a_m < g.M) pa = decompose(m0 + a_m, g.H, g.W);
+  Pix pa[RM];
+#pragma unroll
+  for (int rr = 0; rr < RM; ++rr) {
+    pa[rr] = Pix{0, 0, 0};
+    if (AM == 1 && m0 + 64 * rr + a_m < g.M) pa[rr] = decompose(m0 + 64 * rr + a_m, g.H, g.W);
+  }
 
-  float ra[8], rb[8];
+  float ra[8 * RM], rb[8];
   auto load = [&](int k0) {
-    if (a_kc) {
-      const int m = m0 + a_m;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = k0 + a_k + 4 * h;
-        if (vecA && m < g.M && k + 3 < kend) {
-          const float* ptr = a_vec_ptr<AM>(g, A, m, k, pa);
-          const float4 v = ptr ? get4(ptr) : make_float4(0.f, 0.f, 0.f, 0.f);
-          ra[4 * h] = v.x; ra[4 * h + 1] = v.y; ra[4 * h + 2] = v.z; ra[4 * h + 3] = v.w;
-        } else {
+    for (int rr = 0; rr < RM; ++rr) {
+      float* r8 = ra + 8 * rr;
+      if (a_kc) {
+        const int m = m0 + 64 * rr + a_m;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) ra[4 * h + e] = (k + e < kend) ? a_at<AM>(g, A, m, k + e, pa) : 0.f;
+        for (int h = 0; h < 2; ++h) {
+          const int k = k0 + a_k + 4 * h;
+          if (vecA && m < g.M && k + 3 < kend) {
+            const float* ptr = a_vec_ptr<AM>(g, A, m, k, pa[rr]);
+            const float4 v = ptr ? get4(ptr) : make_float4(0.f, 0.f, 0.f, 0.f);
+            r8[4 * h] = v.x; r8[4 * h + 1] = v.y; r8[4 * h + 2] = v.z; r8[4 * h + 3] = v.w;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r8[4 * h + e] = (k + e < kend) ? a_at<AM>(g, A, m, k + e, pa[rr]) : 0.f;
+          }
         }
-      }
-    } else {
-      const int k = k0 + a_k;
+      } else {
+        const int k = k0 + a_k;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int m = m0 + a_m + 4 * h;
-        if (vecA && k < kend && m + 3 < g.M) {
-          const float4 v = get4(A + (long long)k * g.sak + m);
-          ra[4 * h] = v.x; ra[4 * h + 1] = v.y; ra[4 * h + 2] = v.z; ra[4 * h + 3] = v.w;
-        } else {
+        for (int h = 0; h < 2; ++h) {
+          const int m = m0 + 64 * rr + a_m + 4 * h;
+          if (vecA && k < kend && m + 3 < g.M) {
+            const float4 v = get4(A + (long long)k * g.sak + m);
+            r8[4 * h] = v.x; r8[4 * h + 1] = v.y; r8[4 * h + 2] = v.z; r8[4 * h + 3] = v.w;
+          } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) ra[4 * h + e] = (k < kend) ? a_at<AM>(g, A, m + e, k, pa) : 0.f;
+            for (int e = 0; e < 4; ++e) r8[4 * h + e] = (k < kend) ? a_at<AM>(g, A, m + e, k, pa[rr]) : 0.f;
+          }
         }
       }
     }
@@ -194,9 +205,9 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
     }
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[2 * RM][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2 * RM; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -204,9 +215,14 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
 #pragma unroll
+    for (int rr = 0; rr < RM; ++rr)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (a_kc) As[a_k + e][64 * rr + a_m] = ra[8 * rr + e];
+        else As[a_k][64 * rr + a_m + e] = ra[8 * rr + e];
+      }
+#pragma unroll
     for (int e = 0; e < 8; ++e) {
-      if (a_kc) As[a_k + e][a_m] = ra[e];
-      else As[a_k][a_m + e] = ra[e];
       if (b_nc) Bs[b_k][b_n + e] = rb[e];
       else Bs[b_k + e][b_n] = rb[e];
     }
@@ -215,13 +231,13 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
       const int kr = kk * 4 + (lane >> 4);
-      float av[2], bv[2];
+      float av[2 * RM], bv[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) av[i] = As[kr][wm * 32 + i * 16 + (lane & 15)];
+      for (int i = 0; i < 2 * RM; ++i) av[i] = As[kr][wm * 32 * RM + i * 16 + (lane & 15)];
 #pragma unroll
       for (int j = 0; j < 2; ++j) bv[j] = Bs[kr][wn * 32 + j * 16 + (lane & 15)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2 * RM; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
     }
@@ -234,21 +250,22 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
   const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
   float* part = split ? g.partial + ((long long)z * g.splits + ks) * g.M * g.N : nullptr;
   if (flags & 4) {
-    // stage the 64x64 tile in LDS, then each thread writes 16 consecutive columns of one row
-    constexpr int LDC = BN + 4;
-    float* Cs = smem;  // 64 x 68 floats <= 2 * BK * LDP
+    // stage the tile in LDS, then each thread writes 16 consecutive columns of one row per round
+    float* Cs = smem;
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2 * RM; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          Cs[(wm * 32 + i * 16 + 4 * (lane >> 4) + r) * LDC + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+          Cs[(wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r) * LDC + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
     __syncthreads();
-    const int row = tid >> 2, cb = (tid & 3) * 16;
-    const int m = m0 + row;
-    if (m < g.M) {
+#pragma unroll
+    for (int rr = 0; rr < RM; ++rr) {
+      const int row = 64 * rr + (tid >> 2), cb = (tid & 3) * 16;
+      const int m = m0 + row;
+      if (m >= g.M) continue;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n = n0 + cb + 4 * q;
@@ -276,12 +293,12 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
     return;
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2 * RM; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
+        const int m = m0 + wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r;
         const int n = n0 + wn * 32 + j * 16 + (lane & 15);
         if (m >= g.M || n >= g.N) continue;
         if (split) part[(long long)m * g.N + n] = acc[i][j][r];
@@ -326,16 +343,19 @@ __global__ __launch_bounds__(1024) void tgemm_reduce_kernel(TGemm g) {
 }
 
 template <int AM, int BMODE>
-static void launch_t(const TGemm& g, int kchunk, int flags, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((tgemm_kernel<AM, BMODE>), grid, dim3(256), 0, s, g, kchunk, flags);
+static void launch_t(const TGemm& g, int kchunk, int flags, int rm, dim3 grid, hipStream_t s) {
+  if (rm == 2) hipLaunchKernelGGL((tgemm_kernel<AM, BMODE, 2>), grid, dim3(256), 0, s, g, kchunk, flags);
+  else hipLaunchKernelGGL((tgemm_kernel<AM, BMODE, 1>), grid, dim3(256), 0, s, g, kchunk, flags);
 }
 
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
-  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   const long long batch = (long long)g.nz1 * g.nz2;
+  // 128-row tiles when the grid still holds >= 2 blocks per CU with them (tall activation GEMMs)
+  const int rm = ((long long)((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * batch >= 512) ? 2 : 1;
+  const int tiles = ((g.M + 64 * rm - 1) / (64 * rm)) * ((g.N + BN - 1) / BN);
   int splits = 1;
   if (g.partial && partial_cap > 0) {
     // fill ~2048 blocks, each split at least 256 deep
@@ -371,10 +391,10 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
                  : (g.scn == 1 && al16(g.C) && m4(g.scm) && m4(g.bC1) && m4(g.bC2)))
     flags |= 4;
   dim3 grid(tiles, splits, (unsigned)batch);
-  if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, flags, grid, s);
-  else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, flags, grid, s);
-  else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, grid, s);
-  else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, flags, grid, s);
+  if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, flags, rm, grid, s);
+  else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, flags, rm, grid, s);
+  else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, rm, grid, s);
+  else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, flags, rm, grid, s);
   else return hipErrorInvalidValue;
   if (splits > 1) {
     const long long MN = (long long)g.M * g.N;
@@ -384,115 +404,150 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------- LayerNorm
-constexpr int LN_MAXV = 8;  // C <= 512
+// One wave per pixel, channel c = lane + 64 i (V values per lane), wavefront-shuffle sums; NP pixels
+// per iteration so their loads are in flight together (the per-pixel chain is latency bound).
+constexpr int LN_NP = 4;
 
+template <int V>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ w,
                                                      const float* __restrict__ b, int C, long long P, int biasfree,
                                                      float* __restrict__ y, int ldy, float* __restrict__ stats) {
   const int lane = threadIdx.x & 63;
   const long long nw = (long long)gridDim.x * 4;
-  for (long long p = blockIdx.x * 4LL + (threadIdx.x >> 6); p < P; p += nw) {
-    float v[LN_MAXV];
-    float s = 0.f;
+  for (long long p0 = blockIdx.x * 4LL + (threadIdx.x >> 6); p0 < P; p0 += nw * LN_NP) {
+    float v[LN_NP][V];
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      const int c = lane + 64 * i;
-      v[i] = c < C ? x[p * ldx + c] : 0.f;
-      s += v[i];
-    }
-    const float mu = wave_sum(s) / C;
-    float q = 0.f;
+    for (int q = 0; q < LN_NP; ++q) {
+      const long long p = p0 + q * nw;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < C) q += (v[i] - mu) * (v[i] - mu);
+      for (int i = 0; i < V; ++i) {
+        const int c = lane + 64 * i;
+        v[q][i] = (p < P && c < C) ? x[p * ldx + c] : 0.f;
+      }
     }
-    const float var = wave_sum(q) / C;
-    const float sd = sqrtf(var + 1e-5f);
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < C) y[p * ldy + c] = biasfree ? v[i] / sd * w[c] : (v[i] - mu) / sd * w[c] + b[c];
-    }
-    if (lane == 0) {
-      stats[2 * p] = mu;
-      stats[2 * p + 1] = 1.f / sd;
+    for (int q = 0; q < LN_NP; ++q) {
+      const long long p = p0 + q * nw;
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < V; ++i) s += v[q][i];
+      const float mu = wave_sum(s) / C;
+      float qq = 0.f;
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = lane + 64 * i;
+        if (c < C) qq += (v[q][i] - mu) * (v[q][i] - mu);
+      }
+      const float var = wave_sum(qq) / C;
+      const float sd = sqrtf(var + 1e-5f);
+      if (p >= P) continue;
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = lane + 64 * i;
+        if (c < C) y[p * ldy + c] = biasfree ? v[q][i] / sd * w[c] : (v[q][i] - mu) / sd * w[c] + b[c];
+      }
+      if (lane == 0) {
+        stats[2 * p] = mu;
+        stats[2 * p + 1] = 1.f / sd;
+      }
     }
   }
 }
 
+template <int V>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, int ldd, const float* __restrict__ x,
                                                      int ldx, const float* __restrict__ w,
                                                      const float* __restrict__ stats, int C, long long P, int biasfree,
                                                      const float* R, int ldr, float* dx, int lddx,
                                                      float* __restrict__ part) {
-  __shared__ float red[4][2 * 64 * LN_MAXV];
+  __shared__ float red[4][2 * 64 * V];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float aw[LN_MAXV], ab[LN_MAXV];
+  float aw[V], ab[V], wr[V];
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) aw[i] = ab[i] = 0.f;
+  for (int i = 0; i < V; ++i) {
+    aw[i] = ab[i] = 0.f;
+    const int c = lane + 64 * i;
+    wr[i] = c < C ? w[c] : 0.f;
+  }
   const long long nw = (long long)gridDim.x * 4;
-  for (long long p = blockIdx.x * 4LL + wv; p < P; p += nw) {
-    const float mu = stats[2 * p], r = stats[2 * p + 1];
-    float xv[LN_MAXV], gv[LN_MAXV];
-    float s1 = 0.f, s2 = 0.f;
+  for (long long p0 = blockIdx.x * 4LL + wv; p0 < P; p0 += nw * LN_NP) {
+    float xv[LN_NP][V], dv[LN_NP][V], rv[LN_NP][V], mu[LN_NP], r[LN_NP];
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      const int c = lane + 64 * i;
-      float d = 0.f, xx = 0.f, ww = 0.f;
-      if (c < C) {
-        d = dy[p * ldd + c];
-        xx = x[p * ldx + c];
-        ww = w[c];
+    for (int q = 0; q < LN_NP; ++q) {
+      const long long p = p0 + q * nw;
+      const bool ok = p < P;
+      mu[q] = ok ? stats[2 * p] : 0.f;
+      r[q] = ok ? stats[2 * p + 1] : 0.f;
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = lane + 64 * i;
+        const bool live = ok && c < C;
+        dv[q][i] = live ? dy[p * ldd + c] : 0.f;
+        xv[q][i] = live ? x[p * ldx + c] : 0.f;
+        rv[q][i] = (live && R) ? R[p * ldr + c] : 0.f;
       }
-      const float xh = biasfree ? xx * r : (xx - mu) * r;
-      aw[i] += d * xh;
-      ab[i] += d;
-      gv[i] = d * ww;
-      xv[i] = xx;
-      s1 += gv[i] * (biasfree ? xx : xh);
-      s2 += gv[i];
     }
-    s1 = wave_sum(s1) / C;
-    s2 = wave_sum(s2) / C;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      const int c = lane + 64 * i;
-      if (c >= C) continue;
-      float d;
-      if (biasfree) d = r * gv[i] - r * r * r * (xv[i] - mu) * s1;
-      else d = r * (gv[i] - s2 - (xv[i] - mu) * r * s1);
-      if (R) d += R[p * ldr + c];
-      dx[p * lddx + c] = d;
+    for (int q = 0; q < LN_NP; ++q) {
+      const long long p = p0 + q * nw;
+      float s1 = 0.f, s2 = 0.f, gv[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const float xh = biasfree ? xv[q][i] * r[q] : (xv[q][i] - mu[q]) * r[q];
+        aw[i] += dv[q][i] * xh;
+        ab[i] += dv[q][i];
+        gv[i] = dv[q][i] * wr[i];
+        s1 += gv[i] * (biasfree ? xv[q][i] : xh);
+        s2 += gv[i];
+      }
+      s1 = wave_sum(s1) / C;
+      s2 = wave_sum(s2) / C;
+      if (p >= P) continue;
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = lane + 64 * i;
+        if (c >= C) continue;
+        const float rq = r[q];
+        float d;
+        if (biasfree) d = rq * gv[i] - rq * rq * rq * (xv[q][i] - mu[q]) * s1;
+        else d = rq * (gv[i] - s2 - (xv[q][i] - mu[q]) * rq * s1);
+        dx[p * lddx + c] = d + rv[q][i];
+      }
     }
   }
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < V; ++i) {
     red[wv][64 * i + lane] = aw[i];
-    red[wv][64 * LN_MAXV + 64 * i + lane] = ab[i];
+    red[wv][64 * V + 64 * i + lane] = ab[i];
   }
   __syncthreads();
   const int ncol = biasfree ? C : 2 * C;
   for (int c = threadIdx.x; c < ncol; c += blockDim.x) {
-    const int off = c < C ? c : 64 * LN_MAXV + (c - C);
+    const int off = c < C ? c : 64 * V + (c - C);
     part[(long long)blockIdx.x * ncol + c] = ((red[0][off] + red[1][off]) + red[2][off]) + red[3][off];
   }
 }
 
+#define LN_DISPATCH(KERNEL, grid, ...)                                                           \
+  do {                                                                                            \
+    if (C <= 64) hipLaunchKernelGGL((KERNEL<1>), grid, dim3(256), 0, s, __VA_ARGS__);               \
+    else if (C <= 128) hipLaunchKernelGGL((KERNEL<2>), grid, dim3(256), 0, s, __VA_ARGS__);         \
+    else if (C <= 256) hipLaunchKernelGGL((KERNEL<4>), grid, dim3(256), 0, s, __VA_ARGS__);         \
+    else hipLaunchKernelGGL((KERNEL<8>), grid, dim3(256), 0, s, __VA_ARGS__);                       \
+  } while (0)
+
 hipError_t launch_ln_fwd(const float* x, int ldx, const float* w, const float* b, int C, long long P, int biasfree,
                          float* y, int ldy, float* stats, hipStream_t s) {
-  if (C > 64 * LN_MAXV) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3(grid_for(P, 4, 16384)), dim3(256), 0, s, x, ldx, w, b, C, P, biasfree, y,
-                     ldy, stats);
+  if (C > 512) return hipErrorInvalidValue;
+  LN_DISPATCH(ln_fwd_kernel, dim3(grid_for(P, 4 * LN_NP, 16384)), x, ldx, w, b, C, P, biasfree, y, ldy, stats);
   return hipGetLastError();
 }
 
 hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, const float* w, const float* stats, int C,
                          long long P, int biasfree, const float* R, int ldr, float* dx, int lddx, float* part, int nblk,
                          hipStream_t s) {
-  if (C > 64 * LN_MAXV) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nblk), dim3(256), 0, s, dy, ldd, x, ldx, w, stats, C, P, biasfree, R, ldr,
-                     dx, lddx, part);
+  if (C > 512) return hipErrorInvalidValue;
+  LN_DISPATCH(ln_bwd_kernel, dim3(nblk), dy, ldd, x, ldx, w, stats, C, P, biasfree, R, ldr, dx, lddx, part);
   return hipGetLastError();
 }
 
@@ -514,6 +569,8 @@ __device__ __forceinline__ void dw_load_col(const float* __restrict__ in, int ld
   }
 }
 
+constexpr int DW_U = 4;  // output columns per iteration: 3*DW_U loads in flight together
+
 __global__ __launch_bounds__(256) void dw_row_fwd_kernel(const float* __restrict__ in, int ldi,
                                                          const float* __restrict__ w, const float* __restrict__ b,
                                                          int flip, int C, int Bn, int H, int W, int nrs,
@@ -532,21 +589,25 @@ __global__ __launch_bounds__(256) void dw_row_fwd_kernel(const float* __restrict
 #pragma unroll
   for (int k = 0; k < 9; ++k) wr[k] = live ? w[c * 9 + (flip ? 8 - k : k)] : 0.f;
   const float bias = (live && b) ? b[c] : 0.f;
-  DwWin win;
-  dw_load_col(in, ldi, img0, y, x0 - 1, H, W, c, live, win.v[0]);
-  dw_load_col(in, ldi, img0, y, x0, H, W, c, live, win.v[1]);
-  for (int x = x0; x < x1; ++x) {
-    dw_load_col(in, ldi, img0, y, x + 1, H, W, c, live, win.v[2]);
-    float acc = bias;
+  float col[DW_U + 2][3];  // columns x-1 .. x+DW_U
+  dw_load_col(in, ldi, img0, y, x0 - 1, H, W, c, live, col[0]);
+  dw_load_col(in, ldi, img0, y, x0, H, W, c, live, col[1]);
+  for (int x = x0; x < x1; x += DW_U) {
 #pragma unroll
-    for (int ty = 0; ty < 3; ++ty)
+    for (int u = 0; u < DW_U; ++u) dw_load_col(in, ldi, img0, y, x + 1 + u, H, W, c, live, col[2 + u]);
 #pragma unroll
-      for (int tx = 0; tx < 3; ++tx) acc += wr[ty * 3 + tx] * win.v[tx][ty];
-    if (live) out[(img0 + (long long)y * W + x) * ldo + c] = acc;
+    for (int u = 0; u < DW_U; ++u) {
+      float acc = bias;
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) acc += wr[ty * 3 + tx] * col[u + tx][ty];
+      if (live && x + u < x1) out[(img0 + (long long)y * W + x + u) * ldo + c] = acc;
+    }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      win.v[0][k] = win.v[1][k];
-      win.v[1][k] = win.v[2][k];
+      col[0][k] = col[DW_U][k];
+      col[1][k] = col[DW_U + 1][k];
     }
   }
 }
@@ -571,21 +632,28 @@ __global__ __launch_bounds__(256) void dw_row_wgrad_kernel(const float* __restri
     const int y = row % H, bi = row / H;
     const long long img0 = (long long)bi * H * W;
     const int x0 = xs * DW_SEG, x1 = min(W, x0 + DW_SEG);
-    DwWin win;
-    dw_load_col(in, ldi, img0, y, x0 - 1, H, W, c, live, win.v[0]);
-    dw_load_col(in, ldi, img0, y, x0, H, W, c, live, win.v[1]);
-    for (int x = x0; x < x1; ++x) {
-      dw_load_col(in, ldi, img0, y, x + 1, H, W, c, live, win.v[2]);
-      const float d = live ? dy[(img0 + (long long)y * W + x) * ldd + c] : 0.f;
+    float col[DW_U + 2][3];
+    dw_load_col(in, ldi, img0, y, x0 - 1, H, W, c, live, col[0]);
+    dw_load_col(in, ldi, img0, y, x0, H, W, c, live, col[1]);
+    for (int x = x0; x < x1; x += DW_U) {
+      float d[DW_U];
 #pragma unroll
-      for (int ty = 0; ty < 3; ++ty)
+      for (int u = 0; u < DW_U; ++u) {
+        dw_load_col(in, ldi, img0, y, x + 1 + u, H, W, c, live, col[2 + u]);
+        d[u] = (live && x + u < x1) ? dy[(img0 + (long long)y * W + x + u) * ldd + c] : 0.f;
+      }
 #pragma unroll
-        for (int tx = 0; tx < 3; ++tx) acc[ty * 3 + tx] += d * win.v[tx][ty];
-      acc[9] += d;
+      for (int u = 0; u < DW_U; ++u) {
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) acc[ty * 3 + tx] += d[u] * col[u + tx][ty];
+        acc[9] += d[u];
+      }
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        win.v[0][k] = win.v[1][k];
-        win.v[1][k] = win.v[2][k];
+        col[0][k] = col[DW_U][k];
+        col[1][k] = col[DW_U + 1][k];
       }
     }
   }
