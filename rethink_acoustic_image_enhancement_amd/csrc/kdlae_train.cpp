@@ -186,6 +186,8 @@ struct Ctx {
     if (r_ != KDLAE_OK) return r_; \
   } while (0)
 
+inline int ld4(int n) { return (n + 3) / 4 * 4; }
+
 int nblk_for(long long rows, long long ncols, int maxb = 1024) {
   long long nb = rows / 128;
   if (nb > maxb) nb = maxb;
@@ -335,22 +337,24 @@ int block_fwd(Ctx& c, BlockRec& r) {
   r.st2 = c.alloc(2 * P);
   LAUNCH(tr::launch_ln_fwd(r.x1, C, c.W(p + ".norm2.body.weight"), c.W(p + ".norm2.body.bias"), C, P, bf, r.xn2, C,
                            r.st2, c.s));
-  r.y = c.alloc(P * 2 * hid);
-  TRY(conv1(c, p + ".ffn.project_in", {r.xn2, C}, C, 2 * hid, P, {r.y, 2 * hid}));
-  r.yd = c.alloc(P * 2 * hid);
-  LAUNCH(tr::launch_dw_fwd(r.y, 2 * hid, c.W(p + ".ffn.dwconv.weight"), c.W(p + ".ffn.dwconv.bias"), 0, 2 * hid, Bn,
-                           r.H, r.W, r.yd, 2 * hid, c.s));
-  r.g = c.alloc(P * hid);
-  LAUNCH(tr::launch_gate_fwd(r.yd, 2 * hid, hid, P, r.g, hid, c.s));
+  // hidden-width buffers get a pixel stride rounded up to 4 floats so GEMM rows stay float4-aligned
+  const int L2 = ld4(2 * hid), L1 = ld4(hid);
+  r.y = c.alloc(P * L2);
+  TRY(conv1(c, p + ".ffn.project_in", {r.xn2, C}, C, 2 * hid, P, {r.y, L2}));
+  r.yd = c.alloc(P * L2);
+  LAUNCH(tr::launch_dw_fwd(r.y, L2, c.W(p + ".ffn.dwconv.weight"), c.W(p + ".ffn.dwconv.bias"), 0, 2 * hid, Bn,
+                           r.H, r.W, r.yd, L2, c.s));
+  r.g = c.alloc(P * L1);
+  LAUNCH(tr::launch_gate_fwd(r.yd, L2, hid, P, r.g, L1, c.s));
   r.out = c.alloc(P * C);
-  TRY(conv1(c, p + ".ffn.project_out", {r.g, hid}, hid, C, P, {r.out, C}, r.x1, C));
+  TRY(conv1(c, p + ".ffn.project_out", {r.g, L1}, hid, C, P, {r.out, C}, r.x1, C));
   return KDLAE_OK;
 }
 
-int dw_wgrad(Ctx& c, const float* dy, const float* x, int C, int Bn, int H, int W, const std::string& n) {
+int dw_wgrad(Ctx& c, const float* dy, const float* x, int ld, int C, int Bn, int H, int W, const std::string& n) {
   const long long P = (long long)Bn * H * W;
   const int nb = tr::dw_wgrad_blocks(C, Bn, H, W, nblk_for(P, 10LL * C, 256));
-  LAUNCH(tr::launch_dw_wgrad(dy, C, x, C, C, Bn, H, W, c.red, nb, c.s));
+  LAUNCH(tr::launch_dw_wgrad(dy, ld, x, ld, C, Bn, H, W, c.red, nb, c.s));
   const bool has_b = c.G(n + ".bias") != nullptr;
   LAUNCH(tr::launch_part_reduce(c.red, nb, has_b ? 10 * C : 9 * C, 1, c.G(n + ".weight"), 0, 1.f, c.s, 10 * C));
   return KDLAE_OK;
@@ -373,16 +377,16 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   const std::string& p = r.p;
   const size_t mark = c.off;
   // ffn (KDLAE_model.py:101-106)
-  float* dg = c.alloc(P * hid);
-  TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, hid}, {d, C}, hid, C, P, {dg, hid}));
-  float* dyd = c.alloc(P * 2 * hid);
-  LAUNCH(tr::launch_gate_bwd(dg, hid, r.yd, 2 * hid, hid, P, dyd, 2 * hid, c.s));
-  float* dy = c.alloc(P * 2 * hid);
-  LAUNCH(tr::launch_dw_fwd(dyd, 2 * hid, c.W(p + ".ffn.dwconv.weight"), nullptr, 1, 2 * hid, Bn, r.H, r.W, dy,
-                           2 * hid, c.s));
-  TRY(dw_wgrad(c, dyd, r.y, 2 * hid, Bn, r.H, r.W, p + ".ffn.dwconv"));
+  const int L2 = ld4(2 * hid), L1 = ld4(hid);
+  float* dg = c.alloc(P * L1);
+  TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, L1}, {d, C}, hid, C, P, {dg, L1}));
+  float* dyd = c.alloc(P * L2);
+  LAUNCH(tr::launch_gate_bwd(dg, L1, r.yd, L2, hid, P, dyd, L2, c.s));
+  float* dy = c.alloc(P * L2);
+  LAUNCH(tr::launch_dw_fwd(dyd, L2, c.W(p + ".ffn.dwconv.weight"), nullptr, 1, 2 * hid, Bn, r.H, r.W, dy, L2, c.s));
+  TRY(dw_wgrad(c, dyd, r.y, L2, 2 * hid, Bn, r.H, r.W, p + ".ffn.dwconv"));
   float* dxn2 = c.alloc(P * C);
-  TRY(conv1_bwd(c, p + ".ffn.project_in", {r.xn2, C}, {dy, 2 * hid}, C, 2 * hid, P, {dxn2, C}));
+  TRY(conv1_bwd(c, p + ".ffn.project_in", {r.xn2, C}, {dy, L2}, C, 2 * hid, P, {dxn2, C}));
   float* dx1 = c.alloc(P * C);
   TRY(ln_bwd(c, dxn2, r.x1, r.st2, C, P, p + ".norm2.body", d, dx1));
   // attention (KDLAE_model.py:124-145)
@@ -432,7 +436,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   }
   float* dqkv = c.alloc(P * C3);
   LAUNCH(tr::launch_dw_fwd(dqkvd, C3, c.W(p + ".attn.qkv_dwconv.weight"), nullptr, 1, C3, Bn, r.H, r.W, dqkv, C3, c.s));
-  TRY(dw_wgrad(c, dqkvd, r.qkv, C3, Bn, r.H, r.W, p + ".attn.qkv_dwconv"));
+  TRY(dw_wgrad(c, dqkvd, r.qkv, C3, C3, Bn, r.H, r.W, p + ".attn.qkv_dwconv"));
   float* dxn1 = c.alloc(P * C);
   TRY(conv1_bwd(c, p + ".attn.qkv", {r.xn1, C}, {dqkv, C3}, C, C3, P, {dxn1, C}));
   TRY(ln_bwd(c, dxn1, r.x, r.st1, C, P, p + ".norm1.body", dx1, d));
