@@ -196,11 +196,19 @@ def bench_train(args, world, rank, dev, distributed):
                                        for i in range(B)]))
     batch = {"img": img.to(dev), "denoise_rate": rate.to(dev)}
     gt = {"hq": gt_hq.to(dev), "sr": gt_sr.to(dev)}
-    trainer = KDLAETrainer(model)
+    # KDLAET.yml: mixing_augs {mixup: true, mixup_beta: 1.2, use_identity: true}; feed_train_data mixes
+    trainer = KDLAETrainer(model, mixing_augs={"mixup": True, "mixup_beta": 1.2, "use_identity": True})
+    import random
+    random.seed(rank)
+    torch.manual_seed(rank)
+
+    def train_step():
+        lq_m, gt_m = trainer.feed_train_data(batch, gt)
+        return trainer.optimize_parameters(lq_m, gt_m)
 
     loss = None
     for _ in range(args.warmup):
-        loss = trainer.optimize_parameters(batch, gt)
+        loss = train_step()
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -209,7 +217,7 @@ def bench_train(args, world, rank, dev, distributed):
     t0 = time.perf_counter()
     ev0.record()
     for _ in range(args.steps):
-        loss = trainer.optimize_parameters(batch, gt)
+        loss = train_step()
     ev1.record()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -229,7 +237,7 @@ def bench_train(args, world, rank, dev, distributed):
            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
            "data": "synthetic (hash-uniform images and targets, hash weights of the real architecture)",
            "config": {"workload": f"KDLAE-T train step bs={B}/GPU {H}x{W} (+sr {2 * H}x{2 * W}), L1LossSr, "
-                                  "clip_grad_norm_ 0.01, AdamW", "global_batch": world * B, "per_gpu_batch": B,
+                                  "clip_grad_norm_ 0.01, AdamW, mixup", "global_batch": world * B, "per_gpu_batch": B,
                       "parallelism": f"dp{world}" + (" (RCCL all-reduce of the flat gradient every step)"
                                                      if distributed else "")},
            "roofline": {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",

@@ -232,6 +232,13 @@ int kdlae_train_clip_adamw(float* theta, const float* grad, float* exp_avg, floa
                            float gscale, float max_norm, float lr, float beta1, float beta2, float eps,
                            float weight_decay, int step, const int64_t* ranges, int nranges, float* scratch,
                            void* stream);
+/* replaces Mixing_Augment.mixup (image_restoration_model.py:25-61, KDLAET.yml mixing_augs):
+ * out[b] = lam * in[b] + (1 - lam) * in[perm[b]] over B samples of per_sample floats; perm is a
+ * device int[B]; lam and perm are drawn on the host exactly as the reference draws them. */
+int kdlae_train_mixup(const float* in, float* out, int B, int64_t per_sample, const int* perm, float lam,
+                      void* stream);
+/* replaces BaseModel.model_ema(decay) (Train/basicsr/models/base_model.py:54-62) over the flat buffers. */
+int kdlae_train_ema(float* ema, const float* theta, int64_t n, float decay, void* stream);
 
 #ifdef __cplusplus
 }

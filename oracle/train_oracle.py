@@ -75,3 +75,36 @@ class TrainStep:
 
     def state_dict(self):
         return {k: v.detach() for k, v in self.params.items()}
+
+
+class MixingAugmentRef:
+    """Mixing_Augment (image_restoration_model.py:25-61) restated on CPU tensors, same host RNG calls
+    in the same order (Beta rsample, randperm, random.randint) as the reference."""
+
+    def __init__(self, mixup_beta=1.2, use_identity=False):
+        import random as _random
+        self._random = _random
+        self.dist = torch.distributions.beta.Beta(torch.tensor([mixup_beta]), torch.tensor([mixup_beta]))
+        self.use_identity = use_identity
+        self.augments = [self.mixup]
+
+    def mixup(self, target, input_):
+        lam = self.dist.rsample((1, 1)).item()
+        first = next(iter(target.values())) if isinstance(target, dict) else target
+        r_index = torch.randperm(first.size(0))
+
+        def proc(t):
+            return lam * t + (1 - lam) * t[r_index, :] if t is not None else None
+
+        mt = {k: proc(v) for k, v in target.items()} if isinstance(target, dict) else proc(target)
+        mi = {k: proc(v) for k, v in input_.items()} if isinstance(input_, dict) else proc(input_)
+        return mt, mi
+
+    def __call__(self, target, input_):
+        if self.use_identity:
+            idx = self._random.randint(0, len(self.augments))
+        else:
+            idx = self._random.randint(0, len(self.augments) - 1)
+        if idx < len(self.augments):
+            target, input_ = self.augments[idx](target, input_)
+        return target, input_

@@ -32,7 +32,7 @@ EXPORTS = (
     "kdlae_tt_create", "kdlae_tt_destroy", "kdlae_tt_num_params", "kdlae_tt_param_info", "kdlae_tt_num_floats",
     "kdlae_tt_workspace_bytes", "kdlae_tt_forward", "kdlae_tt_backward",
     "kdlae_train_l1sr_scratch_floats", "kdlae_train_l1sr", "kdlae_train_adamw_scratch_floats",
-    "kdlae_train_clip_adamw",
+    "kdlae_train_clip_adamw", "kdlae_train_mixup", "kdlae_train_ema",
 )
 
 
@@ -139,6 +139,8 @@ def lib() -> ctypes.CDLL:
     L.kdlae_train_clip_adamw.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
                                          c_float, c_float, c_float, c_float, c_float, c_int, c_void_p, c_int, c_void_p,
                                          c_void_p]
+    L.kdlae_train_mixup.argtypes = [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_float, c_void_p]
+    L.kdlae_train_ema.argtypes = [c_void_p, c_void_p, c_int64, c_float, c_void_p]
     for name in EXPORTS:
         if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes", "_padded_size", "_num_floats",
                               "_scratch_floats")):

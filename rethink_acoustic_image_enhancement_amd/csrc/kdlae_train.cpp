@@ -802,4 +802,19 @@ int kdlae_train_clip_adamw(float* theta, const float* grad, float* exp_avg, floa
   return KDLAE_OK;
 }
 
+int kdlae_train_mixup(const float* in, float* out, int B, int64_t per_sample, const int* perm, float lam,
+                      void* stream) {
+  if (!in || !out || !perm || B <= 0 || per_sample <= 0 || in == out) return fail(KDLAE_EINVAL_CONFIG, "bad argument");
+  hipError_t e = tr::launch_mixup(in, out, B, per_sample, perm, lam, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
+  return KDLAE_OK;
+}
+
+int kdlae_train_ema(float* ema, const float* theta, int64_t n, float decay, void* stream) {
+  if (!ema || !theta || n <= 0) return fail(KDLAE_EINVAL_CONFIG, "bad argument");
+  hipError_t e = tr::launch_ema(ema, theta, n, decay, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
+  return KDLAE_OK;
+}
+
 }  // extern "C"

@@ -1116,5 +1116,35 @@ hipError_t launch_adamw(float* p, const float* g, float* m, float* v, long long 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------- mixup, EMA
+// Mixing_Augment.mixup (image_restoration_model.py:32-34): out[b] = lam * in[b] + (1 - lam) * in[perm[b]]
+__global__ void mixup_kernel(const float* __restrict__ in, float* __restrict__ out, int B, long long per,
+                             const int* __restrict__ perm, float lam) {
+  const long long total = (long long)B * per;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / per);
+    const long long e = i - (long long)b * per;
+    out[i] = lam * in[i] + (1.f - lam) * in[(long long)perm[b] * per + e];
+  }
+}
+
+// BaseModel.model_ema (base_model.py:54-62): ema = decay * ema + (1 - decay) * theta
+__global__ void ema_kernel(float* __restrict__ ema, const float* __restrict__ theta, long long n, float decay) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    ema[i] = ema[i] * decay + theta[i] * (1.f - decay);
+}
+
+hipError_t launch_mixup(const float* in, float* out, int B, long long per, const int* perm, float lam, hipStream_t s) {
+  hipLaunchKernelGGL(mixup_kernel, dim3(grid_for((long long)B * per, 256, 65536)), dim3(256), 0, s, in, out, B, per,
+                     perm, lam);
+  return hipGetLastError();
+}
+
+hipError_t launch_ema(float* ema, const float* theta, long long n, float decay, hipStream_t s) {
+  hipLaunchKernelGGL(ema_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, ema, theta, n, decay);
+  return hipGetLastError();
+}
+
 }  // namespace train
 }  // namespace kdlae

@@ -112,5 +112,10 @@ hipError_t launch_clip_coef(const float* part, int nblk, float gscale, float max
 hipError_t launch_adamw(float* p, const float* g, float* m, float* v, long long n, const float* state, float lr,
                         float beta1, float beta2, float eps, float wd, int step, hipStream_t s);
 
+// Mixing_Augment.mixup (image_restoration_model.py:32-34) on a [B][per] tensor, perm on device; out != in
+hipError_t launch_mixup(const float* in, float* out, int B, long long per, const int* perm, float lam, hipStream_t s);
+// BaseModel.model_ema (Train/basicsr/models/base_model.py:54-62)
+hipError_t launch_ema(float* ema, const float* theta, long long n, float decay, hipStream_t s);
+
 }  // namespace train
 }  // namespace kdlae

@@ -18,13 +18,14 @@ There is no CPU fallback: every entry point raises on CPU tensors or a missing l
 from __future__ import annotations
 
 import ctypes
+import random
 
 import torch
 import torch.distributed as dist
 
 from . import _lib
 
-__all__ = ["TrainEngine", "TeacherTrainFn", "L1LossSr", "KDLAETrainer", "sync_gradients"]
+__all__ = ["TrainEngine", "TeacherTrainFn", "L1LossSr", "KDLAETrainer", "MixingAugment", "sync_gradients"]
 
 
 def _vp(t):
@@ -214,6 +215,53 @@ class L1LossSr(torch.nn.Module):
                                  is not None else None, float(self.loss_weight))
 
 
+def _mix(t, perm, lam):
+    t = t.to(torch.float32).contiguous()
+    out = torch.empty_like(t)
+    per = t.numel() // t.shape[0]
+    rc = _lib.lib().kdlae_train_mixup(_vp(t), _vp(out), t.shape[0], per, _vp(perm), float(lam), _stream(t.device))
+    _lib.check(rc, "kdlae_train_mixup")
+    return out
+
+
+class MixingAugment:
+    """Mixing_Augment (Train/basicsr/models/image_restoration_model.py:25-61), blend on the GPU.
+
+    lam ~ Beta(mixup_beta, mixup_beta) and the batch permutation are drawn on the host exactly as the
+    reference draws them (torch.distributions / torch.randperm / random.randint), so a seeded run
+    picks the same mixes; the blend lam * x + (1 - lam) * x[perm] is ``kdlae_train_mixup``."""
+
+    def __init__(self, mixup_beta=1.2, use_identity=False, device=None):
+        self.dist = torch.distributions.beta.Beta(torch.tensor([mixup_beta]), torch.tensor([mixup_beta]))
+        self.device = device
+        self.use_identity = use_identity
+        self.augments = [self.mixup]
+
+    def mixup(self, target, input_):
+        lam = self.dist.rsample((1, 1)).item()
+        first = next(iter(target.values())) if isinstance(target, dict) else target
+        if first.device.type != "cuda":
+            raise RuntimeError("MixingAugment (MI355X build) blends ROCm tensors only")
+        r_index = torch.randperm(first.size(0))
+        perm = r_index.to(device=first.device, dtype=torch.int32)
+
+        def blend(v):
+            return _mix(v, perm, lam) if v is not None else None
+
+        mixed_target = {k: blend(v) for k, v in target.items()} if isinstance(target, dict) else blend(target)
+        mixed_input = {k: blend(v) for k, v in input_.items()} if isinstance(input_, dict) else blend(input_)
+        return mixed_target, mixed_input
+
+    def __call__(self, target, input_):
+        if self.use_identity:
+            augment_idx = random.randint(0, len(self.augments))  # includes "no augmentation"
+        else:
+            augment_idx = random.randint(0, len(self.augments) - 1)
+        if augment_idx < len(self.augments):
+            target, input_ = self.augments[augment_idx](target, input_)
+        return target, input_
+
+
 def sync_gradients(grad: torch.Tensor, group=None) -> float:
     """DDP gradient averaging (base_model.py:76-82) as ONE all-reduce over the flat gradient buffer.
 
@@ -235,7 +283,7 @@ class KDLAETrainer:
     weight_decay 5e-5, betas (0.2, 0.999); use_grad_clip -> clip_grad_norm_(0.01); L1LossSr."""
 
     def __init__(self, model, lr=1e-5, weight_decay=0.5e-4, betas=(0.2, 0.999), eps=1e-8, use_grad_clip=True,
-                 max_norm=0.01, loss_weight=1.0, group=None):
+                 max_norm=0.01, loss_weight=1.0, group=None, mixing_augs=None, ema_decay=0.0):
         params = list(model.parameters())
         if not params or params[0].device.type != "cuda":
             raise RuntimeError("KDLAETrainer: move the model to a ROCm device first (no CPU fallback)")
@@ -265,6 +313,26 @@ class KDLAETrainer:
         self._l1_scratch = torch.empty(int(L.kdlae_train_l1sr_scratch_floats()), dtype=torch.float32, device=dev)
         self._opt_scratch = torch.empty(int(L.kdlae_train_adamw_scratch_floats()), dtype=torch.float32, device=dev)
         self._loss = torch.zeros((), dtype=torch.float32, device=dev)
+        # KDLAET.yml train.mixing_augs ({mixup, mixup_beta, use_identity}); ImageCleanModel.__init__ :83-87
+        m = mixing_augs or {}
+        self.mixing = (MixingAugment(m.get("mixup_beta", 1.2), m.get("use_identity", False), dev)
+                       if m.get("mixup", False) else None)
+        # train.ema_decay (ImageCleanModel.__init__: net_g_ema starts as a copy of net_g, model_ema(0))
+        self.ema_decay = float(ema_decay)
+        self.theta_ema = self.theta.clone() if self.ema_decay > 0 else None
+
+    def feed_train_data(self, lq: dict, gt: dict):
+        """ImageCleanModel.feed_train_data (:161-186): the optional mixup of (gt, lq)."""
+        if self.mixing is not None:
+            gt, lq = self.mixing(gt, lq)
+        return lq, gt
+
+    def ema_state_dict(self):
+        """net_g_ema's parameters (``params_ema`` in BasicSR checkpoints) as views of the EMA buffer."""
+        if self.theta_ema is None:
+            raise RuntimeError("ema_decay is 0: there is no EMA copy")
+        return {k: self.theta_ema[off:off + n].view(p.shape)
+                for (k, n, off), p in zip(self.engine.keys, self.model.parameters())}
 
     def forward_backward(self, lq: dict, gt: dict):
         """preds = net_g(lq); l_pix = cri_pix(preds, gt); l_pix.backward()  (:198-213)."""
@@ -299,6 +367,10 @@ class KDLAETrainer:
         _lib.check(rc, "kdlae_train_clip_adamw")
         for eng in getattr(self.model, "_engines", {}).values():
             eng.signature = None  # inference handles re-pack the updated weights on next use
+        if self.theta_ema is not None:  # model_ema(decay) after the step (:221-222)
+            rc = _lib.lib().kdlae_train_ema(_vp(self.theta_ema), _vp(self.theta), self.engine.numel,
+                                            self.ema_decay, _stream(self.theta.device))
+            _lib.check(rc, "kdlae_train_ema")
 
     def optimize_parameters(self, lq: dict, gt: dict):
         """One full iteration: forward, L1LossSr, backward, DDP all-reduce, clip, AdamW."""
