@@ -111,7 +111,15 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv & 1, wn = wv >> 1;
   const int tiles_n = (g.N + BN - 1) / BN;
-  const int m0 = (blockIdx.x / tiles_n) * BMr, n0 = (blockIdx.x % tiles_n) * BN;
+  // XCD-aware order: dispatch id d runs on XCD d % 8; logical tiles [x*per, (x+1)*per) go to XCD x, so
+  // the n-tiles of one row block (consecutive logical ids) share that XCD's L2 copy of their A rows.
+  // The grid is padded to a multiple of 8; the padding blocks exit.
+  // (flags & 8: remap on; only for single-split grids of >= 64 tiles, where every XCD gets work)
+  const int tiles_m = (g.M + BMr - 1) / BMr;
+  const int per = (int)(gridDim.x >> 3);
+  const int tile = (flags & 8) ? (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  if (tile >= tiles_m * tiles_n) return;
+  const int m0 = (tile / tiles_n) * BMr, n0 = (tile % tiles_n) * BN;
   const int z = blockIdx.z, z1 = z / g.nz2, z2 = z - z1 * g.nz2;
   const float* A = g.A + z1 * g.bA1 + z2 * g.bA2;
   const float* B = g.B + (BMODE == 1 ? z1 * g.bB1 : z1 * g.bB1 + z2 * g.bB2);
@@ -390,7 +398,9 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   if (splits > 1 ? (g.N % 4 == 0 && al16(g.partial))
                  : (g.scn == 1 && al16(g.C) && m4(g.scm) && m4(g.bC1) && m4(g.bC2)))
     flags |= 4;
-  dim3 grid(tiles, splits, (unsigned)batch);
+  const bool xcd = splits == 1 && batch == 1 && tiles >= 64;
+  if (xcd) flags |= 8;
+  dim3 grid(xcd ? (tiles + 7) / 8 * 8 : tiles, splits, (unsigned)batch);
   if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, rm, grid, s);
