@@ -1,0 +1,107 @@
+// KDLAE-S 16 -> 16 channel Conv3d 3x3x3 + bias + ReLU (KDLAE/KDLAE_model.py:386-393, the full-resolution
+// encoder / decoder convs) as an LDS-tiled implicit GEMM for gfx950.
+//
+// With 16 output channels the generic implicit GEMM (gemm.hip) gets one MFMA per activation fragment
+// it loads through L1 (27 taps re-read every input pixel from cache), which caps it near 40% of the
+// MFMA rate.  Here a block stages its input halo once in LDS — 3 frames x (TR+2) rows x (TC+2) columns
+// x 16 channels, 64 B per pixel — and each wave keeps all 27 weight fragments in VGPRs for the whole
+// block, so the inner loop is one conflict-free ds_read_b128 (16 pixels x 64 B) per 4 MFMAs.
+//
+// MFMA roles as in gemm.hip: A = weights (rows = output channels), B = pixels, k = 4 consecutive input
+// channels of one tap; lane (li, lq) ends with pixel li, output channels 4 lq .. 4 lq + 3.
+#include "kernels.h"
+
+namespace kdlae {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TR = 4;             // output rows per block (one per wave)
+constexpr int TC = 64;            // output columns per block (4 pixel tiles of 16 per wave)
+constexpr int HR = TR + 2, HC = TC + 2;
+constexpr int HALO_PX = 3 * HR * HC;  // 1188 pixels x 16 channels = 74.25 KiB
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256, 2) void conv3d_c16_kernel(Conv3dC16Params p) {
+  __shared__ __attribute__((aligned(16))) f32x4 tile[HALO_PX * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int tx_n = (p.W + TC - 1) / TC, ty_n = (p.H + TR - 1) / TR;
+  int bid = blockIdx.x;
+  const int txi = bid % tx_n;
+  bid /= tx_n;
+  const int tyi = bid % ty_n;
+  bid /= ty_n;
+  const int fr = bid % p.F;
+  const int b = bid / p.F;
+  const int x0 = txi * TC, y0 = tyi * TR;
+  const long long fhw = (long long)p.H * p.W;
+  const float* inb = p.in + (long long)b * p.F * fhw * p.ldi;
+
+  // stage the halo: item i = (pixel, channel quad)
+  for (int i = tid; i < HALO_PX * 4; i += 256) {
+    const int q = i & 3, px = i >> 2;
+    const int c = px % HC, r = (px / HC) % HR, f = px / (HC * HR);
+    const int ff = fr + f - 1, yy = y0 + r - 1, xx = x0 + c - 1;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)ff < (unsigned)p.F && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W)
+      v = *reinterpret_cast<const f32x4*>(inb + ((long long)ff * fhw + (long long)yy * p.W + xx) * p.ldi + 4 * q);
+    tile[i] = v;
+  }
+  // the 27 weight fragments (record g = tap of the fragment-order pack, NT = 1, Cin_pad = 16)
+  f32x4 w[27];
+#pragma unroll
+  for (int g = 0; g < 27; ++g) w[g] = *reinterpret_cast<const f32x4*>(p.wp + ((size_t)g * 64 + lane) * 4);
+  const f32x4 bias = *reinterpret_cast<const f32x4*>(p.bias + 4 * lq);
+  __syncthreads();
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tap = 0; tap < 27; ++tap) {
+    const int df = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
+    const f32x4* row = tile + ((df * HR + wave + dy) * HC + dx + li) * 4 + lq;
+    f32x4 xv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) xv[t] = row[t * 16 * 4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = mfma4(w[tap][s], xv[t][s], acc[t]);
+  }
+
+  const int y = y0 + wave;
+  if (y >= p.H) return;
+  float* outb = p.out + ((long long)b * p.F * fhw + (long long)fr * fhw + (long long)y * p.W) * p.ldo;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int x = x0 + t * 16 + li;
+    if (x >= p.W) continue;
+    f32x4 v = acc[t] + bias;
+    if (p.relu) {
+      v.x = fmaxf(v.x, 0.f);
+      v.y = fmaxf(v.y, 0.f);
+      v.z = fmaxf(v.z, 0.f);
+      v.w = fmaxf(v.w, 0.f);
+    }
+    *reinterpret_cast<f32x4*>(outb + (long long)x * p.ldo + 4 * lq) = v;
+  }
+}
+
+hipError_t launch_conv3d_c16(const Conv3dC16Params& p, hipStream_t s) {
+  if (p.ldi % 4 || p.ldo % 4 || p.ldi < 16 || p.ldo < 16 || p.F <= 0 || p.H <= 0 || p.W <= 0 || p.Bn <= 0)
+    return hipErrorInvalidValue;
+  const long long blocks = (long long)p.Bn * p.F * ((p.H + TR - 1) / TR) * ((p.W + TC - 1) / TC);
+  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv3d_c16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace kdlae

@@ -12,6 +12,7 @@
 // stores through the PixelShuffle map and adds the skip tensor in place.  Channel counts are padded
 // to 16 with zero weights (ReLU keeps pad channels at 0).
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -279,7 +280,25 @@ int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int 
   float* tB = buf(pl.tB);
   const DeviceWeights& D = h->dw;
   int rc;
+  static const bool no_c16 = getenv("KDLAE_NO_C16") != nullptr;
   auto conv = [&](const Gemm& g, View in, View o, int Hh, int Ww, int relu) {
+    if (!no_c16 && g.kt == 3 && g.ntiles == 1 && g.cg_per_tap == 1 && g.kgroups == 27) {
+      // 16 -> 16 channels: LDS-tiled kernel with the weights held in VGPRs (conv3d_c16.hip)
+      Conv3dC16Params q{};
+      q.in = in.p;
+      q.ldi = in.ld;
+      q.wp = D.P(g.w);
+      q.bias = D.P(g.bias);
+      q.out = o.p;
+      q.ldo = o.ld;
+      q.Bn = B;
+      q.F = F;
+      q.H = Hh;
+      q.W = Ww;
+      q.relu = relu;
+      HIPCHK(launch_conv3d_c16(q, s));
+      return (int)KDLAE_OK;
+    }
     GemmCall c;
     c.g = &g;
     c.W = D.P(g.w);
