@@ -1,3 +1,4 @@
+#include <cstdlib>
 // ASDQE host runtime: DenoiseRatePredictor forward in eval mode (ASDQE/ASDQE_model.py:123-171).
 //
 //   pad_to_multiple(lq / gt, dim) (:113-121, :159-160)   -> zero-extent bounds in the first convs
@@ -284,7 +285,27 @@ int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int 
   const int d = h->cfg.dim, m = 3 * d, ci = h->cfg.in_channels;
   const int Hp = pl.Hp, Wp = pl.Wp;
   int rc;
+  static const bool no_c16 = getenv("KDLAE_NO_C16") != nullptr;
   auto conv = [&](const Gemm& g, View in, View o, int Hh, int Ww, int relu) {
+    if (!no_c16 && g.kt == 1 && g.ksize == 3 && g.ntiles == 1 && g.cg_per_tap == 1 && g.kgroups == 9 &&
+        g.out_mode == 0) {
+      // 16 -> 16 channels: LDS-tiled kernel with VGPR-resident weights (conv3d_c16.hip)
+      Conv3dC16Params q{};
+      q.in = in.p;
+      q.ldi = in.ld;
+      q.wp = D.P(g.w);
+      q.bias = D.P(g.bias);
+      q.out = o.p;
+      q.ldo = o.ld;
+      q.Bn = B;
+      q.F = 1;
+      q.H = Hh;
+      q.W = Ww;
+      q.relu = relu;
+      q.kt = 1;
+      HIPCHK(launch_conv3d_c16(q, s));
+      return (int)KDLAE_OK;
+    }
     GemmCall c;
     c.g = &g;
     c.W = D.P(g.w);

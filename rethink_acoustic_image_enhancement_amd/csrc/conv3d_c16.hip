@@ -1,5 +1,6 @@
-// KDLAE-S 16 -> 16 channel Conv3d 3x3x3 + bias + ReLU (KDLAE/KDLAE_model.py:386-393, the full-resolution
-// encoder / decoder convs) as an LDS-tiled implicit GEMM for gfx950.
+// 16 -> 16 channel 3x3x3 Conv3d (KT = 3: KDLAE-S full-resolution encoder / decoder convs,
+// KDLAE/KDLAE_model.py:386-393) and 3x3 Conv2d (KT = 1: the ASDQE extractors' second conv,
+// ASDQE/ASDQE_model.py:131-142) + bias + ReLU as an LDS-tiled implicit GEMM for gfx950.
 //
 // With 16 output channels the generic implicit GEMM (gemm.hip) gets one MFMA per activation fragment
 // it loads through L1 (27 taps re-read every input pixel from cache), which caps it near 40% of the
@@ -20,7 +21,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int TR = 4;             // output rows per block (one per wave)
 constexpr int TC = 64;            // output columns per block (4 pixel tiles of 16 per wave)
 constexpr int HR = TR + 2, HC = TC + 2;
-constexpr int HALO_PX = 3 * HR * HC;  // 1188 pixels x 16 channels = 74.25 KiB
+constexpr int HALO_PX = 3 * HR * HC;  // up to 1188 pixels x 16 channels = 74.25 KiB (KT = 3)
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -28,7 +29,9 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 
 }  // namespace
 
+template <int KT>
 __global__ __launch_bounds__(256, 2) void conv3d_c16_kernel(Conv3dC16Params p) {
+  constexpr int NPX = KT * HR * HC, NTAP = 9 * KT;
   __shared__ __attribute__((aligned(16))) f32x4 tile[HALO_PX * 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
@@ -45,19 +48,19 @@ __global__ __launch_bounds__(256, 2) void conv3d_c16_kernel(Conv3dC16Params p) {
   const float* inb = p.in + (long long)b * p.F * fhw * p.ldi;
 
   // stage the halo: item i = (pixel, channel quad)
-  for (int i = tid; i < HALO_PX * 4; i += 256) {
+  for (int i = tid; i < NPX * 4; i += 256) {
     const int q = i & 3, px = i >> 2;
     const int c = px % HC, r = (px / HC) % HR, f = px / (HC * HR);
-    const int ff = fr + f - 1, yy = y0 + r - 1, xx = x0 + c - 1;
+    const int ff = fr + f - (KT == 3 ? 1 : 0), yy = y0 + r - 1, xx = x0 + c - 1;
     f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
     if ((unsigned)ff < (unsigned)p.F && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W)
       v = *reinterpret_cast<const f32x4*>(inb + ((long long)ff * fhw + (long long)yy * p.W + xx) * p.ldi + 4 * q);
     tile[i] = v;
   }
-  // the 27 weight fragments (record g = tap of the fragment-order pack, NT = 1, Cin_pad = 16)
-  f32x4 w[27];
+  // the 9 KT weight fragments (record g = tap of the fragment-order pack, NT = 1, Cin_pad = 16)
+  f32x4 w[NTAP];
 #pragma unroll
-  for (int g = 0; g < 27; ++g) w[g] = *reinterpret_cast<const f32x4*>(p.wp + ((size_t)g * 64 + lane) * 4);
+  for (int g = 0; g < NTAP; ++g) w[g] = *reinterpret_cast<const f32x4*>(p.wp + ((size_t)g * 64 + lane) * 4);
   const f32x4 bias = *reinterpret_cast<const f32x4*>(p.bias + 4 * lq);
   __syncthreads();
 
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_c16_kernel(Conv3dC16Params p) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int tap = 0; tap < 27; ++tap) {
+  for (int tap = 0; tap < NTAP; ++tap) {
     const int df = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
     const f32x4* row = tile + ((df * HR + wave + dy) * HC + dx + li) * 4 + lq;
     f32x4 xv[4];
@@ -100,7 +103,9 @@ hipError_t launch_conv3d_c16(const Conv3dC16Params& p, hipStream_t s) {
     return hipErrorInvalidValue;
   const long long blocks = (long long)p.Bn * p.F * ((p.H + TR - 1) / TR) * ((p.W + TC - 1) / TC);
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv3d_c16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  if (p.kt == 3) hipLaunchKernelGGL(conv3d_c16_kernel<3>, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  else if (p.kt == 1) hipLaunchKernelGGL(conv3d_c16_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -296,6 +296,7 @@ int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int 
       q.H = Hh;
       q.W = Ww;
       q.relu = relu;
+      q.kt = 3;
       HIPCHK(launch_conv3d_c16(q, s));
       return (int)KDLAE_OK;
     }

@@ -153,7 +153,7 @@ struct HeadParams {
 };
 hipError_t launch_asdqe_head(const HeadParams& p, hipStream_t s);
 
-// KDLAE-S 16 -> 16 channel Conv3d 3x3x3 (+ bias, ReLU) on NDHWC views, LDS-tiled (conv3d_c16.hip).
+// 16 -> 16 channel 3x3x3 Conv3d / 3x3 Conv2d (+ bias, ReLU) on NDHWC views, LDS-tiled (conv3d_c16.hip).
 // wp: fragment-order weights of a Gemm with ntiles = 1, cg_per_tap = 1, kgroups = 27 (runtime.h pack).
 struct Conv3dC16Params {
   const float* in; int ldi;        // [B][F][H][W] pixels, 16 channels at stride ldi
@@ -162,6 +162,7 @@ struct Conv3dC16Params {
   float* out; int ldo;
   int Bn, F, H, W;
   int relu;
+  int kt;                          // temporal taps: 3 (Conv3d) or 1 (Conv2d, F = 1)
 };
 hipError_t launch_conv3d_c16(const Conv3dC16Params& p, hipStream_t s);
 
