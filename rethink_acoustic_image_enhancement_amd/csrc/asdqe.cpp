@@ -286,6 +286,7 @@ int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int 
   const int Hp = pl.Hp, Wp = pl.Wp;
   int rc;
   static const bool no_c16 = getenv("KDLAE_NO_C16") != nullptr;
+  static const bool no_lds = getenv("KDLAE_NO_CONV_LDS") != nullptr;
   auto conv = [&](const Gemm& g, View in, View o, int Hh, int Ww, int relu) {
     if (!no_c16 && g.kt == 1 && g.ksize == 3 && g.ntiles == 1 && g.cg_per_tap == 1 && g.kgroups == 9 &&
         g.out_mode == 0) {
@@ -304,6 +305,27 @@ int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int 
       q.relu = relu;
       q.kt = 1;
       HIPCHK(launch_conv3d_c16(q, s));
+      return (int)KDLAE_OK;
+    }
+    if (!no_lds && g.ksize == 3 && g.out_mode == 0 && g.kt == 1 && conv_lds_supported(g.kt, g.ntiles, g.cg_per_tap * 16)) {
+      // LDS-tiled implicit GEMM (conv_lds.hip): halo staged once, no per-tap L1 re-reads
+      ConvLdsParams q{};
+      q.in = in.p;
+      q.ldi = in.ld;
+      q.cin_pad = g.cg_per_tap * 16;
+      q.wp = D.P(g.w);
+      q.ntiles = g.ntiles;
+      q.kgroups = g.kgroups;
+      q.bias = D.P(g.bias);
+      q.out = o.p;
+      q.ldo = o.ld;
+      q.Bn = B;
+      q.F = 1;
+      q.H = Hh;
+      q.W = Ww;
+      q.kt = g.kt;
+      q.relu = relu;
+      HIPCHK(launch_conv_lds(q, s));
       return (int)KDLAE_OK;
     }
     GemmCall c;

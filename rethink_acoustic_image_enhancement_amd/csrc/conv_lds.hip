@@ -1,0 +1,170 @@
+// LDS-tiled implicit-GEMM 3x3 Conv2d / 3x3x3 Conv3d (+ bias, ReLU) for the small-image U-Nets: the
+// ASDQE DoubleConvs (ASDQE/ASDQE_model.py:20-34, 64 to 256 output channels) and the KDLAE-S 32- and
+// 64-channel levels (KDLAE/KDLAE_model.py:386-393).  Output channels beyond 64 run as more blocks
+// along grid.y (4 channel tiles each), every one staging the same halo.
+//
+// The generic implicit GEMM (gemm.hip) re-reads every input pixel through L1 for each of the 9 (27)
+// taps.  Here a block owns a 4-row x 64-column output tile of one frame and NT x 16 output channels.
+// It stages the input halo of CC channels at a time in LDS, channel-group-major
+// ([16-ch group][frame][6 rows][66 cols][16 ch], so one wave's 16-pixel x 64-B fragment read is a
+// contiguous, conflict-free 1 KiB), and walks the k-groups (tap, 16-ch group) with the NT weight
+// fragments of the next k-group prefetched from global memory (fragment order, L2-resident) while the
+// 16 NT MFMAs of the current one run.  Wave w computes output row w: 4 pixel tiles x NT channel tiles.
+//
+// MFMA roles as in gemm.hip: A = weights (rows = output channels), B = pixels; lane (li, lq) ends with
+// pixel li and output channels 4 lq .. 4 lq + 3 of each channel tile.
+#include "kernels.h"
+
+namespace kdlae {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TR = 4, TC = 64, HR = TR + 2, HC = TC + 2;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+}  // namespace
+
+template <int KT, int NT, int CC>
+__global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
+  constexpr int NG = CC / 16;                   // 16-channel groups per staged chunk
+  constexpr int FPX = KT * HR * HC;             // halo pixels per group
+  constexpr int NTAP = 9 * KT;
+  __shared__ __attribute__((aligned(16))) f32x4 tile[NG * FPX * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int tx_n = (p.W + TC - 1) / TC, ty_n = (p.H + TR - 1) / TR;
+  int bid = blockIdx.x;
+  const int txi = bid % tx_n;
+  bid /= tx_n;
+  const int tyi = bid % ty_n;
+  bid /= ty_n;
+  const int fr = bid % p.F;
+  const int b = bid / p.F;
+  const int x0 = txi * TC, y0 = tyi * TR;
+  const int t0 = blockIdx.y * NT;               // first output channel tile of this block
+  const long long fhw = (long long)p.H * p.W;
+  const float* inb = p.in + (long long)b * p.F * fhw * p.ldi;
+  const int cgt = p.cin_pad / 16;               // channel groups per tap
+
+  f32x4 acc[NT][4];
+#pragma unroll
+  for (int n = 0; n < NT; ++n)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[n][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // weight fragment of (channel tile t0 + n, k-group g) for this lane; tiles past ntiles read zeros
+  auto wfrag = [&](int n, int g) -> f32x4 {
+    const int tt = t0 + n;
+    if (tt >= p.ntiles) return f32x4{0.f, 0.f, 0.f, 0.f};
+    return *reinterpret_cast<const f32x4*>(p.wp + (((size_t)tt * p.kgroups + g) * 64 + lane) * 4);
+  };
+
+  for (int c0 = 0; c0 < p.cin_pad; c0 += CC) {
+    __syncthreads();  // previous chunk's reads are done
+    // stage channels [c0, c0 + CC): item = (group, halo pixel, quad)
+    for (int i = tid; i < NG * FPX * 4; i += 256) {
+      const int q = i & 3, gp = i >> 2;
+      const int px = gp % FPX, grp = gp / FPX;
+      const int c = px % HC, r = (px / HC) % HR, f = px / (HC * HR);
+      const int ff = fr + f - (KT == 3 ? 1 : 0), yy = y0 + r - 1, xx = x0 + c - 1;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (c0 + grp * 16 < p.cin_pad && (unsigned)ff < (unsigned)p.F && (unsigned)yy < (unsigned)p.H &&
+          (unsigned)xx < (unsigned)p.W)
+        v = *reinterpret_cast<const f32x4*>(inb + ((long long)ff * fhw + (long long)yy * p.W + xx) * p.ldi + c0 +
+                                             grp * 16 + 4 * q);
+      tile[i] = v;
+    }
+    __syncthreads();
+    const int ngrp = min(NG, (p.cin_pad - c0) / 16);
+    const int nk = NTAP * ngrp;  // k-groups of this chunk: (tap, group) with group fastest
+    f32x4 wc[NT];
+    {
+      const int g = 0 * cgt + c0 / 16;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) wc[n] = wfrag(n, g);
+    }
+    for (int kk = 0; kk < nk; ++kk) {
+      const int tap = kk / ngrp, grp = kk - tap * ngrp;
+      // prefetch the next k-group's weights
+      f32x4 wn[NT];
+      if (kk + 1 < nk) {
+        const int tap1 = (kk + 1) / ngrp, grp1 = (kk + 1) - tap1 * ngrp;
+        const int g1 = tap1 * cgt + c0 / 16 + grp1;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) wn[n] = wfrag(n, g1);
+      }
+      const int df = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
+      const f32x4* row = tile + (((grp * KT + df) * HR + wave + dy) * HC + dx + li) * 4 + lq;
+      f32x4 xv[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) xv[t] = row[t * 16 * 4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int n = 0; n < NT; ++n) acc[n][t] = mfma4(wc[n][s], xv[t][s], acc[n][t]);
+      if (kk + 1 < nk) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) wc[n] = wn[n];
+      }
+    }
+  }
+
+  const int y = y0 + wave;
+  if (y >= p.H) return;
+  float* outb = p.out + ((long long)b * p.F * fhw + (long long)fr * fhw + (long long)y * p.W) * p.ldo;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int tt = t0 + n;
+    if (tt >= p.ntiles) break;
+    const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + tt * 16 + 4 * lq) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int x = x0 + t * 16 + li;
+      if (x >= p.W) continue;
+      f32x4 v = acc[n][t] + bias;
+      if (p.relu) {
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+        v.z = fmaxf(v.z, 0.f);
+        v.w = fmaxf(v.w, 0.f);
+      }
+      *reinterpret_cast<f32x4*>(outb + (long long)x * p.ldo + tt * 16 + 4 * lq) = v;
+    }
+  }
+}
+
+bool conv_lds_supported(int kt, int ntiles, int cin_pad) {
+  if (kt != 1 && kt != 3) return false;
+  if (cin_pad % 16 || cin_pad <= 0) return false;
+  return ntiles >= 2 && ntiles <= 16;
+}
+
+hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s) {
+  if (!conv_lds_supported(p.kt, p.ntiles, p.cin_pad) || p.ldi % 4 || p.ldo % 4 || p.ldi < p.cin_pad ||
+      p.ldo < 16 * p.ntiles || p.kgroups != 9 * p.kt * (p.cin_pad / 16))
+    return hipErrorInvalidValue;
+  const long long blocks = (long long)p.Bn * p.F * ((p.H + TR - 1) / TR) * ((p.W + TC - 1) / TC);
+  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  // 4 channel tiles per block at most: NT = 8 needs 271 VGPRs + AGPRs (one wave per SIMD) and measured
+  // slower than two NT = 4 blocks that stage the same halo (r01, ASDQE 128-channel convs)
+  const int nt = p.ntiles <= 2 ? 2 : 4;
+  dim3 grid((unsigned)blocks, (unsigned)((p.ntiles + nt - 1) / nt));
+  // staged chunk: 32 channels (2-D, 51 KiB) or 16 channels (3-D, 76 KiB) of halo
+  if (p.kt == 1) {
+    if (nt == 2) hipLaunchKernelGGL((conv_lds_kernel<1, 2, 32>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv_lds_kernel<1, 4, 32>), grid, dim3(256), 0, s, p);
+  } else {
+    if (nt == 2) hipLaunchKernelGGL((conv_lds_kernel<3, 2, 16>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv_lds_kernel<3, 4, 16>), grid, dim3(256), 0, s, p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kdlae

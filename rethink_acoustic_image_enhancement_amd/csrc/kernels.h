@@ -166,4 +166,17 @@ struct Conv3dC16Params {
 };
 hipError_t launch_conv3d_c16(const Conv3dC16Params& p, hipStream_t s);
 
+// LDS-tiled implicit-GEMM 3x3 (kt 1) / 3x3x3 (kt 3) conv with 2..8 output tiles of 16 channels (conv_lds.hip):
+// wp = fragment-order weights of a Gemm with k = tap * cin_pad + c (kgroups = 9 kt cin_pad / 16).
+struct ConvLdsParams {
+  const float* in; int ldi; int cin_pad;
+  const float* wp; int ntiles, kgroups;
+  const float* bias;               // [ntiles * 16] or null
+  float* out; int ldo;
+  int Bn, F, H, W;
+  int kt, relu;
+};
+bool conv_lds_supported(int kt, int ntiles, int cin_pad);
+hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s);
+
 }  // namespace kdlae
