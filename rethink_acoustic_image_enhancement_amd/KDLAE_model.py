@@ -241,9 +241,14 @@ class KDLAE_teacher(nn.Module):
         cat = self._cfg["params"] == "cat"
         if cat and tuple(denoise_rate.shape) != (B, 1, H, W):
             raise RuntimeError(f"denoise_rate must be [B,1,H,W]={B, 1, H, W}, got {tuple(denoise_rate.shape)}")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            # training: the HIP training engine behind an autograd node (train.py), so
-            # `l_pix.backward()` (image_restoration_model.py:213) runs the hand-written backward
+        wants_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        if wants_grad and not self.training and not self._warned_grad:
+            warnings.warn("KDLAE_teacher in eval mode with grad enabled: the HIP inference path returns outputs "
+                          "without an autograd graph; call .train() to differentiate through the model")
+            self._warned_grad = True
+        if wants_grad and self.training:
+            # training (BasicSR calls net_g.train()): the HIP training engine behind an autograd node
+            # (train.py), so `l_pix.backward()` (image_restoration_model.py:213) runs the hand-written backward
             if img.requires_grad and not self._warned_grad:
                 warnings.warn("KDLAE_teacher HIP training path: the input image receives no gradient")
                 self._warned_grad = True

@@ -291,3 +291,21 @@ def test_trainer_ema_and_mixup_step():
     assert float((tr.theta_ema.double() - ema).abs().max()) <= 1e-6
     sd = tr.ema_state_dict()
     assert set(sd) == {k for k, _ in m.named_parameters()}
+
+
+def test_eval_mode_uses_inference_path_train_mode_builds_graph():
+    """BasicSR differentiates in train mode (net_g.train()); eval mode keeps the inference kernels."""
+    import warnings
+
+    m = _model(dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, LayerNorm_type="BiasFree"))
+    inp = {"img": torch.from_numpy(hash_images("mode_img", (1, 3, 32, 32))).to(DEV),
+           "denoise_rate": torch.full((1, 1, 32, 32), 0.5, device=DEV)}
+    m.eval()
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        o_eval = m(inp)
+    assert o_eval["hq"].grad_fn is None and any("eval mode" in str(x.message) for x in w)
+    m.train()
+    o_train = m(inp)
+    assert o_train["hq"].grad_fn is not None and o_train["sr"].grad_fn is not None
+    assert float((o_train["hq"] - o_eval["hq"]).abs().max()) <= 1e-4
