@@ -566,10 +566,6 @@ hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, cons
 // segment and slides a 3x3 register window along x, so each output costs 3 new loads instead of 9.
 constexpr int DW_SEG = 64;
 
-struct DwWin {
-  float v[3][3];  // [column x-1, x, x+1][row y-1, y, y+1]
-};
-
 __device__ __forceinline__ void dw_load_col(const float* __restrict__ in, int ldi, long long img0, int y, int x, int H,
                                             int W, int c, bool live, float (&col)[3]) {
 #pragma unroll
