@@ -9,6 +9,7 @@
 // Train/basicsr/models/image_restoration_model.py:198-218 (clip_grad_norm_ 0.01, optimizer step).
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "train_kernels.h"
 
@@ -314,6 +315,194 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
       }
 }
 
+// Lean variant for plain strided operands whose 8-element runs are float4-aligned (amode 0, bmode 0,
+// flags 1|2 — every 1x1 conv forward / dX / dW and every MDTA contraction of the training step): the
+// operand layouts are template parameters (AKC: A k-contiguous, BNC: B n-contiguous), each thread's
+// operand pointers are formed once, and per-element bounds checks run only in edge tiles (the generic
+// kernel spent ~10 VALU/SALU instructions per MFMA on them: r01 PMC, `tools/micro/tgemm_bench.cpp`).
+template <bool AKC, bool BNC, int RM>
+__global__ __launch_bounds__(256) void tgemm_lean_kernel(TGemm g, int kchunk, int flags) {
+  constexpr int BMr = 64 * RM, LDA_S = BMr + 4, LDC = BN + 4;
+  constexpr int SM_LOOP = BK * LDA_S + BK * LDP, SM_EPI = BMr * LDC;
+  __shared__ __attribute__((aligned(16))) float smem[SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI];
+  float (*As)[LDA_S] = reinterpret_cast<float (*)[LDA_S]>(smem);
+  float (*Bs)[LDP] = reinterpret_cast<float (*)[LDP]>(smem + BK * LDA_S);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv & 1, wn = wv >> 1;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int tiles_m = (g.M + BMr - 1) / BMr;
+  const int per = (int)(gridDim.x >> 3);
+  const int tile = (flags & 8) ? (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  if (tile >= tiles_m * tiles_n) return;
+  const int m0 = (tile / tiles_n) * BMr, n0 = (tile % tiles_n) * BN;
+  const int z = blockIdx.z, z1 = z / g.nz2, z2 = z - z1 * g.nz2;
+  const float* A = g.A + z1 * g.bA1 + z2 * g.bA2;
+  const float* B = g.B + z1 * g.bB1 + z2 * g.bB2;
+  const int ks = blockIdx.y;
+  const int kbeg = ks * kchunk, kend = min(g.K, kbeg + kchunk);
+
+  const int a_m = AKC ? (tid >> 2) : (tid & 7) * 8;
+  const int a_k = AKC ? (tid & 3) * 8 : (tid >> 3);
+  const int b_k = BNC ? (tid >> 3) : (tid & 3) * 8;
+  const int b_n = BNC ? (tid & 7) * 8 : (tid >> 2);
+  const float* pa[RM];
+  int mrow[RM];
+#pragma unroll
+  for (int rr = 0; rr < RM; ++rr) {
+    mrow[rr] = m0 + 64 * rr + a_m;
+    pa[rr] = AKC ? A + (long long)mrow[rr] * g.sam + a_k : A + mrow[rr] + (long long)a_k * g.sak;
+  }
+  const int ncol = n0 + b_n;
+  const float* pb = BNC ? B + ncol + (long long)b_k * g.sbk : B + (long long)ncol * g.sbn + b_k;
+
+  float ra[8 * RM], rb[8];
+  auto put8 = [](float* r, const float4& v0, const float4& v1) {
+    r[0] = v0.x; r[1] = v0.y; r[2] = v0.z; r[3] = v0.w;
+    r[4] = v1.x; r[5] = v1.y; r[6] = v1.z; r[7] = v1.w;
+  };
+  auto load = [&](int k0) {
+    const bool kfull = k0 + BK <= kend;  // uniform: only the last k-tile of a split needs k checks
+#pragma unroll
+    for (int rr = 0; rr < RM; ++rr) {
+      float* r = ra + 8 * rr;
+      if (AKC) {
+        const float* q = pa[rr] + k0;
+        if (mrow[rr] < g.M && kfull) {
+          put8(r, get4(q), get4(q + 4));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) r[e] = (mrow[rr] < g.M && k0 + a_k + e < kend) ? q[e] : 0.f;
+        }
+      } else {
+        const float* q = pa[rr] + (long long)k0 * g.sak;
+        const bool kok = k0 + a_k < kend;
+        if (kok && mrow[rr] + 7 < g.M) {
+          put8(r, get4(q), get4(q + 4));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) r[e] = (kok && mrow[rr] + e < g.M) ? q[e] : 0.f;
+        }
+      }
+    }
+    if (BNC) {
+      const float* q = pb + (long long)k0 * g.sbk;
+      const bool kok = k0 + b_k < kend;
+      if (kok && ncol + 7 < g.N) {
+        put8(rb, get4(q), get4(q + 4));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rb[e] = (kok && ncol + e < g.N) ? q[e] : 0.f;
+      }
+    } else {
+      const float* q = pb + k0;
+      if (ncol < g.N && kfull) {
+        put8(rb, get4(q), get4(q + 4));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rb[e] = (ncol < g.N && k0 + b_k + e < kend) ? q[e] : 0.f;
+      }
+    }
+  };
+
+  f32x4 acc[2 * RM][2];
+#pragma unroll
+  for (int i = 0; i < 2 * RM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < RM; ++rr)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (AKC) As[a_k + e][64 * rr + a_m] = ra[8 * rr + e];
+        else As[a_k][64 * rr + a_m + e] = ra[8 * rr + e];
+      }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (BNC) Bs[b_k][b_n + e] = rb[e];
+      else Bs[b_k + e][b_n] = rb[e];
+    }
+    __syncthreads();
+    if (k0 + BK < kend) load(k0 + BK);
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      const int kr = kk * 4 + (lane >> 4);
+      float av[2 * RM], bv[2];
+#pragma unroll
+      for (int i = 0; i < 2 * RM; ++i) av[i] = As[kr][wm * 32 * RM + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[j] = Bs[kr][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2 * RM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+    }
+  }
+
+  const bool split = g.splits > 1;
+  float* C = g.C + z1 * g.bC1 + z2 * g.bC2;
+  const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
+  const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
+  float* part = split ? g.partial + ((long long)z * g.splits + ks) * g.M * g.N : nullptr;
+  if (flags & 4) {
+    float* Cs = smem;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2 * RM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r) * LDC + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < RM; ++rr) {
+      const int row = 64 * rr + (tid >> 2), cb = (tid & 3) * 16;
+      const int m = m0 + row;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + cb + 4 * q;
+        if (n >= g.N) break;
+        float4 v = get4(Cs + row * LDC + cb + 4 * q);
+        if (n + 3 < g.N) {
+          if (split) {
+            put4(part + (long long)m * g.N + n, v);
+          } else {
+            v.x = epi(g, v.x, m, n, R, rs);
+            v.y = epi(g, v.y, m, n + 1, R, rs);
+            v.z = epi(g, v.z, m, n + 2, R, rs);
+            v.w = epi(g, v.w, m, n + 3, R, rs);
+            put4(C + (long long)m * g.scm + n, v);
+          }
+        } else {
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+          for (int e = 0; e < 4 && n + e < g.N; ++e) {
+            if (split) part[(long long)m * g.N + n + e] = vv[e];
+            else C[(long long)m * g.scm + n + e] = epi(g, vv[e], m, n + e, R, rs);
+          }
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 2 * RM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r;
+        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (m >= g.M || n >= g.N) continue;
+        if (split) part[(long long)m * g.N + n] = acc[i][j][r];
+        else C[(long long)m * g.scm + (long long)n * g.scn] = epi(g, acc[i][j][r], m, n, R, rs);
+      }
+}
+
 // split-K reduce: a block owns 64 consecutive outputs of one batch entry; 16 waves each sum every 16th
 // split (4 independent chains), combined in fixed order, then the epilogue -> deterministic
 __global__ __launch_bounds__(1024) void tgemm_reduce_kernel(TGemm g) {
@@ -357,6 +546,11 @@ static void launch_t(const TGemm& g, int kchunk, int flags, int rm, dim3 grid, h
 }
 
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+// KDLAE_TGEMM_GENERIC=1 routes everything through the generic kernel (A/B comparisons)
+static bool getenv_generic() {
+  static const bool on = getenv("KDLAE_TGEMM_GENERIC") != nullptr;
+  return on;
+}
 
 hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
@@ -401,7 +595,18 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   const bool xcd = splits == 1 && batch == 1 && tiles >= 64;
   if (xcd) flags |= 8;
   dim3 grid(xcd ? (tiles + 7) / 8 * 8 : tiles, splits, (unsigned)batch);
-  if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, flags, rm, grid, s);
+  if (g.amode == 0 && g.bmode == 0 && (flags & 3) == 3 && !getenv_generic()) {
+    const bool akc = g.sak == 1, bnc = g.sbn == 1;
+#define LEAN(a, b, r) hipLaunchKernelGGL((tgemm_lean_kernel<a, b, r>), grid, dim3(256), 0, s, g, kchunk, flags)
+    if (rm == 2) {
+      if (akc && bnc) LEAN(true, true, 2); else if (akc) LEAN(true, false, 2);
+      else if (bnc) LEAN(false, true, 2); else LEAN(false, false, 2);
+    } else {
+      if (akc && bnc) LEAN(true, true, 1); else if (akc) LEAN(true, false, 1);
+      else if (bnc) LEAN(false, true, 1); else LEAN(false, false, 1);
+    }
+#undef LEAN
+  } else if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, flags, rm, grid, s);
