@@ -96,6 +96,77 @@ __device__ __forceinline__ float epi(const TGemm& g, float acc, int m, int n, co
 __device__ __forceinline__ void put4(float* d, const float4& v) { *reinterpret_cast<float4*>(d) = v; }
 __device__ __forceinline__ float4 get4(const float* s) { return *reinterpret_cast<const float4*>(s); }
 
+// Shared GEMM epilogue: C/D lane map col = lane & 15, row = 4 * (lane >> 4) + r.  With flags & 4 the
+// (64 RM) x 64 tile is staged in LDS (smem, >= 64 RM x (BN + 4) floats) and each thread writes 16
+// consecutive columns of one row per round; split-K blocks store raw partial sums.
+template <int RM>
+__device__ __forceinline__ void store_tile(const TGemm& g, int flags, float* smem, const f32x4 (&acc)[2 * RM][2],
+                                           int m0, int n0, int z, int z1, int z2, int ks) {
+  constexpr int LDC = BN + 4;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv & 1, wn = wv >> 1;
+  const bool split = g.splits > 1;
+  float* C = g.C + z1 * g.bC1 + z2 * g.bC2;
+  const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
+  const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
+  float* part = split ? g.partial + ((long long)z * g.splits + ks) * g.M * g.N : nullptr;
+  if (flags & 4) {
+    // stage the tile in LDS, then each thread writes 16 consecutive columns of one row per round
+    float* Cs = smem;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2 * RM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r) * LDC + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < RM; ++rr) {
+      const int row = 64 * rr + (tid >> 2), cb = (tid & 3) * 16;
+      const int m = m0 + row;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + cb + 4 * q;
+        if (n >= g.N) break;
+        float4 v = get4(Cs + row * LDC + cb + 4 * q);
+        if (n + 3 < g.N) {
+          if (split) {
+            put4(part + (long long)m * g.N + n, v);
+          } else {
+            v.x = epi(g, v.x, m, n, R, rs);
+            v.y = epi(g, v.y, m, n + 1, R, rs);
+            v.z = epi(g, v.z, m, n + 2, R, rs);
+            v.w = epi(g, v.w, m, n + 3, R, rs);
+            put4(C + (long long)m * g.scm + n, v);
+          }
+        } else {
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+          for (int e = 0; e < 4 && n + e < g.N; ++e) {
+            if (split) part[(long long)m * g.N + n + e] = vv[e];
+            else C[(long long)m * g.scm + n + e] = epi(g, vv[e], m, n + e, R, rs);
+          }
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 2 * RM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r;
+        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (m >= g.M || n >= g.N) continue;
+        if (split) part[(long long)m * g.N + n] = acc[i][j][r];
+        else C[(long long)m * g.scm + (long long)n * g.scn] = epi(g, acc[i][j][r], m, n, R, rs);
+      }
+}
+
 // (64*RM)x64 block tile, BK = 32, 4 waves of (32*RM)x32 (2RM x 2 v_mfma_f32_16x16x4_f32 tiles).
 // Global -> register prefetch of the next k-tile overlaps the MFMAs of the current one; 8 consecutive
 // elements per thread along the contiguous operand dimension, as two float4 loads when the `flags`
@@ -253,66 +324,7 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TGemm g, int kchunk, int fla
   }
 
   // epilogue: C/D lane map col = lane & 15, row = 4 * (lane >> 4) + r
-  const bool split = g.splits > 1;
-  float* C = g.C + z1 * g.bC1 + z2 * g.bC2;
-  const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
-  const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
-  float* part = split ? g.partial + ((long long)z * g.splits + ks) * g.M * g.N : nullptr;
-  if (flags & 4) {
-    // stage the tile in LDS, then each thread writes 16 consecutive columns of one row per round
-    float* Cs = smem;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 2 * RM; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r) * LDC + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
-    __syncthreads();
-#pragma unroll
-    for (int rr = 0; rr < RM; ++rr) {
-      const int row = 64 * rr + (tid >> 2), cb = (tid & 3) * 16;
-      const int m = m0 + row;
-      if (m >= g.M) continue;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = n0 + cb + 4 * q;
-        if (n >= g.N) break;
-        float4 v = get4(Cs + row * LDC + cb + 4 * q);
-        if (n + 3 < g.N) {
-          if (split) {
-            put4(part + (long long)m * g.N + n, v);
-          } else {
-            v.x = epi(g, v.x, m, n, R, rs);
-            v.y = epi(g, v.y, m, n + 1, R, rs);
-            v.z = epi(g, v.z, m, n + 2, R, rs);
-            v.w = epi(g, v.w, m, n + 3, R, rs);
-            put4(C + (long long)m * g.scm + n, v);
-          }
-        } else {
-          const float vv[4] = {v.x, v.y, v.z, v.w};
-          for (int e = 0; e < 4 && n + e < g.N; ++e) {
-            if (split) part[(long long)m * g.N + n + e] = vv[e];
-            else C[(long long)m * g.scm + n + e] = epi(g, vv[e], m, n + e, R, rs);
-          }
-        }
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 2 * RM; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r;
-        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
-        if (m >= g.M || n >= g.N) continue;
-        if (split) part[(long long)m * g.N + n] = acc[i][j][r];
-        else C[(long long)m * g.scm + (long long)n * g.scn] = epi(g, acc[i][j][r], m, n, R, rs);
-      }
+  store_tile<RM>(g, flags, smem, acc, m0, n0, z, z1, z2, ks);
 }
 
 // Lean variant for plain strided operands whose 8-element runs are float4-aligned (amode 0, bmode 0,
@@ -442,65 +454,7 @@ __global__ __launch_bounds__(256) void tgemm_lean_kernel(TGemm g, int kchunk, in
     }
   }
 
-  const bool split = g.splits > 1;
-  float* C = g.C + z1 * g.bC1 + z2 * g.bC2;
-  const float* R = g.R ? g.R + z1 * g.bR1 + z2 * g.bR2 : nullptr;
-  const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
-  float* part = split ? g.partial + ((long long)z * g.splits + ks) * g.M * g.N : nullptr;
-  if (flags & 4) {
-    float* Cs = smem;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 2 * RM; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r) * LDC + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
-    __syncthreads();
-#pragma unroll
-    for (int rr = 0; rr < RM; ++rr) {
-      const int row = 64 * rr + (tid >> 2), cb = (tid & 3) * 16;
-      const int m = m0 + row;
-      if (m >= g.M) continue;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = n0 + cb + 4 * q;
-        if (n >= g.N) break;
-        float4 v = get4(Cs + row * LDC + cb + 4 * q);
-        if (n + 3 < g.N) {
-          if (split) {
-            put4(part + (long long)m * g.N + n, v);
-          } else {
-            v.x = epi(g, v.x, m, n, R, rs);
-            v.y = epi(g, v.y, m, n + 1, R, rs);
-            v.z = epi(g, v.z, m, n + 2, R, rs);
-            v.w = epi(g, v.w, m, n + 3, R, rs);
-            put4(C + (long long)m * g.scm + n, v);
-          }
-        } else {
-          const float vv[4] = {v.x, v.y, v.z, v.w};
-          for (int e = 0; e < 4 && n + e < g.N; ++e) {
-            if (split) part[(long long)m * g.N + n + e] = vv[e];
-            else C[(long long)m * g.scm + n + e] = epi(g, vv[e], m, n + e, R, rs);
-          }
-        }
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 2 * RM; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 * RM + i * 16 + 4 * (lane >> 4) + r;
-        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
-        if (m >= g.M || n >= g.N) continue;
-        if (split) part[(long long)m * g.N + n] = acc[i][j][r];
-        else C[(long long)m * g.scm + (long long)n * g.scn] = epi(g, acc[i][j][r], m, n, R, rs);
-      }
+  store_tile<RM>(g, flags, smem, acc, m0, n0, z, z1, z2, ks);
 }
 
 // split-K reduce: a block owns 64 consecutive outputs of one batch entry; 16 waves each sum every 16th
