@@ -57,6 +57,8 @@ struct kdlae_tt_handle {
   std::unordered_map<std::string, int64_t> off;
   int64_t total = 0;
   Saved sv;
+  int ws_B = -1, ws_H = -1, ws_W = -1;  // last kdlae_tt_workspace_bytes query (its dry run is cached)
+  int64_t ws_bytes = -1;
 };
 
 namespace {
@@ -693,6 +695,8 @@ static int check_shape(int B, int H, int W) {
 int64_t kdlae_tt_workspace_bytes(kdlae_tt_handle* h, int B, int H, int W) {
   if (!h) return -1;
   if (check_shape(B, H, W)) return -1;
+  // the dry run walks the whole step on the host: cache it per shape (every training step asks)
+  if (h->ws_B == B && h->ws_H == H && h->ws_W == W) return h->ws_bytes;
   Saved keep = h->sv;
   Ctx c;
   ctx_init(c, h, nullptr, 0, true, nullptr);
@@ -701,7 +705,12 @@ int64_t kdlae_tt_workspace_bytes(kdlae_tt_handle* h, int B, int H, int W) {
   int rc = net_fwd(c, nullptr, nullptr, nullptr, nullptr);
   if (rc == KDLAE_OK) rc = net_bwd(c, nullptr, nullptr, h->cfg.static_train != 0);
   h->sv = keep;
-  return rc == KDLAE_OK ? (int64_t)c.peak : -1;
+  if (rc != KDLAE_OK) return -1;
+  h->ws_B = B;
+  h->ws_H = H;
+  h->ws_W = W;
+  h->ws_bytes = (int64_t)c.peak;
+  return h->ws_bytes;
 }
 
 int kdlae_tt_forward(kdlae_tt_handle* h, const float* theta, const float* img, const float* rate, int B, int H, int W,
