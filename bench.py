@@ -259,6 +259,19 @@ def bench_train(args, world, rank, dev, distributed):
         res["cpu_baseline"] = {"value": round(1.0 / dt, 5), "unit": "images/s", "cores": threads, "kind": "port",
                                "sample": f"1 image of the batch, one optimize_parameters step of the torch-CPU "
                                          f"training oracle, {threads} threads, {dt:.1f} s"}
+        # parity of the trained weights' loss and gradients on image 0 (the oracle step above ran on the
+        # same weights before its update; recompute its gradients without stepping)
+        from oracle.train_oracle import loss_and_grads
+        one = {"img": batch["img"][:1], "denoise_rate": batch["denoise_rate"][:1]}
+        gt1 = {"hq": gt["hq"][:1], "sr": gt["sr"][:1]}
+        l_gpu = float(trainer.forward_backward(one, gt1))
+        g_gpu = trainer.grad.detach().cpu()
+        l_ref, g_ref = loss_and_grads(sd, one["img"].cpu(), one["denoise_rate"].cpu(),
+                                      {k: v.cpu() for k, v in gt1.items()}, TeacherCfg(**KW))
+        g_ref = torch.cat([g_ref[k].reshape(-1) for k, _ in model.named_parameters()])
+        res["parity"] = {"vs": "torch-CPU training oracle, image 0, current weights",
+                         "loss_rel_err": abs(l_gpu - float(l_ref)) / abs(float(l_ref)),
+                         "grad_max_abs_err_rel_to_max": float((g_gpu - g_ref).abs().max() / g_ref.abs().max())}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if distributed:
@@ -382,7 +395,8 @@ def main():
         ips = imgs_total / elapsed / world
         res["per_gpu"] = {"images_per_s": round(ips, 3),
                           "hbm_roof_frac_survey_def": round(ips * 150.70e9 / 8.0e12, 4),
-                          "fp32_compute_frac": round(ips * 1.9177e12 / 157.3e12, 4)}
+                          "fp32_compute_frac": round(ips * 1.9177e12 / 157.3e12, 4),
+                          "sigma_max_roof_frac": round(ips / 41.8, 4)}  # SURVEY §8d per-op Σmax roof
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"], res["parity"] = cpu_baseline(model, batch, out, args.cpu_threads)
