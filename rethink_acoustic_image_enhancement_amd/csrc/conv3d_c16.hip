@@ -11,6 +11,7 @@
 // MFMA roles as in gemm.hip: A = weights (rows = output channels), B = pixels, k = 4 consecutive input
 // channels of one tap; lane (li, lq) ends with pixel li, output channels 4 lq .. 4 lq + 3.
 #include "kernels.h"
+#include "lds_dma.h"
 
 namespace kdlae {
 
@@ -48,15 +49,14 @@ __global__ __launch_bounds__(256, 2) void conv3d_c16_kernel(Conv3dC16Params p) {
   const float* inb = p.in + (long long)b * p.F * fhw * p.ldi;
 
   // stage the halo: item i = (pixel, channel quad)
-  for (int i = tid; i < NPX * 4; i += 256) {
+  dma::stage_batched<NPX * 4, 8>(tile, tid, [&](int i) -> f32x4 {
     const int q = i & 3, px = i >> 2;
     const int c = px % HC, r = (px / HC) % HR, f = px / (HC * HR);
     const int ff = fr + f - (KT == 3 ? 1 : 0), yy = y0 + r - 1, xx = x0 + c - 1;
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
     if ((unsigned)ff < (unsigned)p.F && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W)
-      v = *reinterpret_cast<const f32x4*>(inb + ((long long)ff * fhw + (long long)yy * p.W + xx) * p.ldi + 4 * q);
-    tile[i] = v;
-  }
+      return *reinterpret_cast<const f32x4*>(inb + ((long long)ff * fhw + (long long)yy * p.W + xx) * p.ldi + 4 * q);
+    return f32x4{0.f, 0.f, 0.f, 0.f};
+  });
   // the 9 KT weight fragments (record g = tap of the fragment-order pack, NT = 1, Cin_pad = 16)
   f32x4 w[NTAP];
 #pragma unroll

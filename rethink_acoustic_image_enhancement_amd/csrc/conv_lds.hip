@@ -14,6 +14,7 @@
 // MFMA roles as in gemm.hip: A = weights (rows = output channels), B = pixels; lane (li, lq) ends with
 // pixel li and output channels 4 lq .. 4 lq + 3 of each channel tile.
 #include "kernels.h"
+#include "lds_dma.h"
 
 namespace kdlae {
 
@@ -67,18 +68,17 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
   for (int c0 = 0; c0 < p.cin_pad; c0 += CC) {
     __syncthreads();  // previous chunk's reads are done
     // stage channels [c0, c0 + CC): item = (group, halo pixel, quad)
-    for (int i = tid; i < NG * FPX * 4; i += 256) {
+    dma::stage_batched<NG * FPX * 4, 8>(tile, tid, [&](int i) -> f32x4 {
       const int q = i & 3, gp = i >> 2;
       const int px = gp % FPX, grp = gp / FPX;
       const int c = px % HC, r = (px / HC) % HR, f = px / (HC * HR);
       const int ff = fr + f - (KT == 3 ? 1 : 0), yy = y0 + r - 1, xx = x0 + c - 1;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
       if (c0 + grp * 16 < p.cin_pad && (unsigned)ff < (unsigned)p.F && (unsigned)yy < (unsigned)p.H &&
           (unsigned)xx < (unsigned)p.W)
-        v = *reinterpret_cast<const f32x4*>(inb + ((long long)ff * fhw + (long long)yy * p.W + xx) * p.ldi + c0 +
-                                             grp * 16 + 4 * q);
-      tile[i] = v;
-    }
+        return *reinterpret_cast<const f32x4*>(inb + ((long long)ff * fhw + (long long)yy * p.W + xx) * p.ldi + c0 +
+                                               grp * 16 + 4 * q);
+      return f32x4{0.f, 0.f, 0.f, 0.f};
+    });
     __syncthreads();
     const int ngrp = min(NG, (p.cin_pad - c0) / 16);
     const int nk = NTAP * ngrp;  // k-groups of this chunk: (tap, group) with group fastest

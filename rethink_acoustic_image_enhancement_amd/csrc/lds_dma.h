@@ -52,5 +52,27 @@ __device__ __forceinline__ void barrier_lds() {
   asm volatile("" ::: "memory");
 }
 
+// Register-staged tile fill for a 256-thread block: item i = tid + 256 k of an N-item f32x4 tile,
+// fetched SB items per thread at a time — all SB loads are issued before the first LDS write, so a
+// fill costs ceil(N / (256 SB)) memory latencies instead of one per item (a plain strided loop
+// compiles to load / s_waitcnt vmcnt(0) / ds_write per item).
+template <int N, int SB, typename Fetch>
+__device__ __forceinline__ void stage_batched(f32x4* tile, int tid, Fetch&& fetch) {
+#pragma unroll 1
+  for (int base = 0; base < N; base += 256 * SB) {
+    f32x4 v[SB];
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const int i = base + tid + 256 * k;
+      v[k] = i < N ? fetch(i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const int i = base + tid + 256 * k;
+      if (i < N) tile[i] = v[k];
+    }
+  }
+}
+
 }  // namespace dma
 }  // namespace kdlae

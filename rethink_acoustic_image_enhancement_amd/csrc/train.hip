@@ -838,8 +838,102 @@ __global__ __launch_bounds__(256) void dw_row_wgrad_kernel(const float* __restri
 
 static int dw_rowsegs(int Bn, int H, int W) { return Bn * H * ((W + DW_SEG - 1) / DW_SEG); }
 
+// LDS-tiled version for views with ldi, ldo % 4 == 0: a block owns TY = 8 rows x TX pixel columns x
+// QB channel quads (QB * TX = 256 threads) of one image, stages the (TY + 2) x (TX + 2) halo of float4
+// quads in LDS with every load issued up front, then thread (x, q) walks its column of TY outputs with
+// a 3 x 3 float4 window read from LDS (consecutive lanes = consecutive quads: conflict-free b128).
+// Same accumulation order (bias, then taps row-major) as dw_row_fwd_kernel.
+constexpr int DWT_TY = 8;
+
+template <int QB>
+__global__ __launch_bounds__(256) void dw_tile_fwd_kernel(const float* __restrict__ in, int ldi,
+                                                          const float* __restrict__ w, const float* __restrict__ b,
+                                                          int flip, int C, int H, int W, int tiles_x,
+                                                          float* __restrict__ out, int ldo) {
+  constexpr int TX = 256 / QB, HX = TX + 2, HY = DWT_TY + 2;
+  __shared__ f32x4 tile[HY * HX * QB];
+  const int Cq = (C + 3) >> 2, ngrp = (Cq + QB - 1) / QB;
+  // channel group fastest: the blocks sharing a pixel tile run together, so each pixel's channels
+  // reach HBM as whole lines at about the same time
+  const int q0 = (blockIdx.x % ngrp) * QB, tile_i = blockIdx.x / ngrp;
+  const int tx0 = (tile_i % tiles_x) * TX, ty0 = (tile_i / tiles_x) * DWT_TY;
+  const long long img0 = (long long)blockIdx.z * H * W;
+  const float* src = in + img0 * ldi;
+  // all of a thread's halo loads are issued before the first LDS write (one HBM latency per block)
+  constexpr int NLD = (HY * HX * QB + 255) / 256;
+  f32x4 v[NLD];
+#pragma unroll
+  for (int k = 0; k < NLD; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    const int q = i % QB, px = i / QB;
+    const int xx = tx0 + px % HX - 1, yy = ty0 + px / HX - 1;
+    v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (i < HY * HX * QB && q0 + q < Cq && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+      v[k] = *reinterpret_cast<const f32x4*>(src + ((long long)yy * W + xx) * ldi + 4 * (q0 + q));
+  }
+#pragma unroll
+  for (int k = 0; k < NLD; ++k)
+    if (threadIdx.x + 256 * k < HY * HX * QB) tile[threadIdx.x + 256 * k] = v[k];
+  const int q = threadIdx.x % QB, xl = threadIdx.x / QB;
+  const int c0 = 4 * (q0 + q), x = tx0 + xl;
+  f32x4 wr[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[k][e] = c0 + e < C ? w[(c0 + e) * 9 + (flip ? 8 - k : k)] : 0.f;
+  f32x4 bias = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (b)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[e] = c0 + e < C ? b[c0 + e] : 0.f;
+  __syncthreads();
+  if (c0 >= C || x >= W) return;
+  const f32x4* t = tile + xl * QB + q;
+  f32x4 r0[3], r1[3], r2[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    r0[dx] = t[dx * QB];
+    r1[dx] = t[(HX + dx) * QB];
+  }
+  const bool full = c0 + 4 <= C;
+  float* dst = out + (img0 + (long long)ty0 * W + x) * ldo + c0;
+#pragma unroll
+  for (int r = 0; r < DWT_TY; ++r) {
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) r2[dx] = t[((r + 2) * HX + dx) * QB];
+    f32x4 acc = bias;
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx) acc += wr[tx] * r0[tx];
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx) acc += wr[3 + tx] * r1[tx];
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx) acc += wr[6 + tx] * r2[tx];
+    if (ty0 + r < H) {
+      float* o = dst + (long long)r * W * ldo;
+      if (full) *reinterpret_cast<f32x4*>(o) = acc;
+      else
+        for (int e = 0; e < C - c0; ++e) o[e] = acc[e];
+    }
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      r0[dx] = r1[dx];
+      r1[dx] = r2[dx];
+    }
+  }
+}
+
 hipError_t launch_dw_fwd(const float* in, int ldi, const float* w, const float* b, int flip, int C, int Bn, int H,
                          int W, float* out, int ldo, hipStream_t s) {
+  if (ldi % 4 == 0 && ldo % 4 == 0 && ldi >= (C + 3) / 4 * 4 && !getenv("KDLAE_DW_ROW")) {
+    // QB = 8 quads (32 channels) when 16-quad groups would leave more dead lanes
+    const int Cq = (C + 3) / 4;
+    const bool q8 = ((Cq + 7) / 8) * 8 < ((Cq + 15) / 16) * 16;
+    const int TX = q8 ? 32 : 16, QB = q8 ? 8 : 16;
+    const int tiles_x = (W + TX - 1) / TX;
+    const dim3 grid(tiles_x * ((H + DWT_TY - 1) / DWT_TY) * ((Cq + QB - 1) / QB), 1, Bn);
+    if (q8) hipLaunchKernelGGL(dw_tile_fwd_kernel<8>, grid, dim3(256), 0, s, in, ldi, w, b, flip, C, H, W, tiles_x, out, ldo);
+    else hipLaunchKernelGGL(dw_tile_fwd_kernel<16>, grid, dim3(256), 0, s, in, ldi, w, b, flip, C, H, W, tiles_x, out, ldo);
+    return hipGetLastError();
+  }
   const int nrs = dw_rowsegs(Bn, H, W);
   hipLaunchKernelGGL(dw_row_fwd_kernel, dim3((nrs + 3) / 4, (C + 63) / 64), dim3(256), 0, s, in, ldi, w, b, flip, C,
                      Bn, H, W, nrs, out, ldo);
@@ -984,86 +1078,102 @@ hipError_t launch_gate_bwd(const float* dg, int ldg, const float* y, int ldy, in
 // ---------------------------------------------------------------------------------------------- MDTA core
 constexpr float kNormEps = 1e-12f;  // F.normalize eps (KDLAE_model.py:135-136)
 
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// One wave per attention row i (Ch <= 128: lane owns columns lane and lane + 64), four rows per block,
+// grid (B * heads, ceil(Ch / 4)).
 __global__ __launch_bounds__(256) void attn_softmax_kernel(const float* __restrict__ G, const float* __restrict__ sumsq,
                                                            const float* __restrict__ temp, int C, int heads,
                                                            float* __restrict__ Attn) {
   const int bh = blockIdx.x, b = bh / heads, h = bh - b * heads;
   const int Ch = C / heads;
+  const int lane = threadIdx.x & 63, i = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= Ch) return;
   const float t = temp[h];
-  const float* g = G + (long long)bh * Ch * Ch;
-  float* a = Attn + (long long)bh * Ch * Ch;
+  const float* g = G + (long long)bh * Ch * Ch + (long long)i * Ch;
+  float* a = Attn + (long long)bh * Ch * Ch + (long long)i * Ch;
   const float* sq = sumsq + (long long)b * 2 * C + h * Ch;
   const float* sk = sumsq + (long long)b * 2 * C + C + h * Ch;
-  for (int i = threadIdx.x; i < Ch; i += blockDim.x) {
-    const float nq = fmaxf(sqrtf(sq[i]), kNormEps);
-    float mx = -INFINITY;
-    for (int j = 0; j < Ch; ++j) {
-      const float v = g[i * Ch + j] / (nq * fmaxf(sqrtf(sk[j]), kNormEps)) * t;
-      a[i * Ch + j] = v;
-      mx = fmaxf(mx, v);
-    }
-    float sum = 0.f;
-    for (int j = 0; j < Ch; ++j) {
-      const float e = expf(a[i * Ch + j] - mx);
-      a[i * Ch + j] = e;
-      sum += e;
-    }
-    const float inv = 1.f / sum;
-    for (int j = 0; j < Ch; ++j) a[i * Ch + j] *= inv;
-  }
+  const float nq = fmaxf(sqrtf(sq[i]), kNormEps);
+  const int j0 = lane, j1 = lane + 64;
+  const float v0 = j0 < Ch ? g[j0] / (nq * fmaxf(sqrtf(sk[j0]), kNormEps)) * t : -INFINITY;
+  const float v1 = j1 < Ch ? g[j1] / (nq * fmaxf(sqrtf(sk[j1]), kNormEps)) * t : -INFINITY;
+  const float mx = wave_max(fmaxf(v0, v1));
+  const float e0 = j0 < Ch ? expf(v0 - mx) : 0.f, e1 = j1 < Ch ? expf(v1 - mx) : 0.f;
+  const float inv = 1.f / wave_sum(e0 + e1);
+  if (j0 < Ch) a[j0] = e0 * inv;
+  if (j1 < Ch) a[j1] = e1 * inv;
 }
 
+// One block per (image, head): wave w walks rows w, w + 4, ... with the row's columns across lanes
+// (dS, Mq, the E = dGhat * Ghat row and its row sum), then one thread per column sums E's column.
 __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__ G, const float* __restrict__ sumsq,
                                                        const float* __restrict__ temp, const float* __restrict__ Attn,
                                                        const float* __restrict__ dAttn, int C, int heads,
                                                        float* __restrict__ Mq, float* __restrict__ cq,
                                                        float* __restrict__ ck, float* __restrict__ dtemp_part) {
-  extern __shared__ float E[];  // [Ch][Ch] = dGhat * Ghat, then [256] for the dt reduction
+  extern __shared__ float E[];  // [Ch][Ch] = dGhat * Ghat, then [4] per-wave dt partials
   const int bh = blockIdx.x, b = bh / heads, h = bh - b * heads;
   const int Ch = C / heads;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float t = temp[h];
   const long long mo = (long long)bh * Ch * Ch;
   const float* sq = sumsq + (long long)b * 2 * C + h * Ch;
   const float* sk = sumsq + (long long)b * 2 * C + C + h * Ch;
   float* red = E + Ch * Ch;
+  const int j0 = lane, j1 = lane + 64;
+  const float nk0 = j0 < Ch ? fmaxf(sqrtf(sk[j0]), kNormEps) : 1.f;
+  const float nk1 = j1 < Ch ? fmaxf(sqrtf(sk[j1]), kNormEps) : 1.f;
   float dt = 0.f;
-  for (int i = threadIdx.x; i < Ch; i += blockDim.x) {
+  for (int i = wave; i < Ch; i += 4) {
+    const long long ro = mo + (long long)i * Ch;
     const float nq = fmaxf(sqrtf(sq[i]), kNormEps);
-    float rd = 0.f;
-    for (int j = 0; j < Ch; ++j) rd += dAttn[mo + i * Ch + j] * Attn[mo + i * Ch + j];
-    for (int j = 0; j < Ch; ++j) {
-      const float nk = fmaxf(sqrtf(sk[j]), kNormEps);
-      const float a = Attn[mo + i * Ch + j];
-      const float dS = a * (dAttn[mo + i * Ch + j] - rd);
-      const float gh = G[mo + i * Ch + j] / (nq * nk);
+    const float a0 = j0 < Ch ? Attn[ro + j0] : 0.f, d0 = j0 < Ch ? dAttn[ro + j0] : 0.f;
+    const float a1 = j1 < Ch ? Attn[ro + j1] : 0.f, d1 = j1 < Ch ? dAttn[ro + j1] : 0.f;
+    const float rd = wave_sum(a0 * d0 + a1 * d1);
+    float rs = 0.f;
+    if (j0 < Ch) {
+      const float dS = a0 * (d0 - rd), gh = G[ro + j0] / (nq * nk0), dgh = t * dS;
       dt += dS * gh;
-      const float dgh = t * dS;
-      Mq[mo + i * Ch + j] = dgh / (nq * nk);
-      E[i * Ch + j] = dgh * gh;
+      Mq[ro + j0] = dgh / (nq * nk0);
+      E[i * Ch + j0] = dgh * gh;
+      rs += dgh * gh;
+    }
+    if (j1 < Ch) {
+      const float dS = a1 * (d1 - rd), gh = G[ro + j1] / (nq * nk1), dgh = t * dS;
+      dt += dS * gh;
+      Mq[ro + j1] = dgh / (nq * nk1);
+      E[i * Ch + j1] = dgh * gh;
+      rs += dgh * gh;
+    }
+    rs = wave_sum(rs);
+    if (lane == 0) {
+      const float s = sqrtf(sq[i]);
+      cq[(long long)bh * Ch + i] = s >= kNormEps ? -rs / (s * s) : 0.f;
     }
   }
-  red[threadIdx.x] = dt;
+  dt = wave_sum(dt);
+  if (lane == 0) red[wave] = dt;
   __syncthreads();
-  for (int i = threadIdx.x; i < Ch; i += blockDim.x) {
-    const float s = sqrtf(sq[i]);
-    float rsum = 0.f;
-    for (int j = 0; j < Ch; ++j) rsum += E[i * Ch + j];
-    cq[(long long)bh * Ch + i] = s >= kNormEps ? -rsum / (s * s) : 0.f;
-    const float sj = sqrtf(sk[i]);
+  for (int j = threadIdx.x; j < Ch; j += blockDim.x) {
+    const float sj = sqrtf(sk[j]);
     float csum = 0.f;
-    for (int r = 0; r < Ch; ++r) csum += E[r * Ch + i];
-    ck[(long long)bh * Ch + i] = sj >= kNormEps ? -csum / (sj * sj) : 0.f;
+    for (int r = 0; r < Ch; ++r) csum += E[r * Ch + j];
+    ck[(long long)bh * Ch + j] = sj >= kNormEps ? -csum / (sj * sj) : 0.f;
   }
-  if (threadIdx.x == 0) {
-    float a = 0.f;
-    for (int k = 0; k < (int)blockDim.x; ++k) a += red[k];
-    dtemp_part[bh] = a;
-  }
+  if (threadIdx.x == 0) dtemp_part[bh] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 hipError_t launch_attn_softmax(const float* G, const float* sumsq, const float* temp, int Bn, int C, int heads,
                                float* Attn, hipStream_t s) {
-  hipLaunchKernelGGL(attn_softmax_kernel, dim3(Bn * heads), dim3(128), 0, s, G, sumsq, temp, C, heads, Attn);
+  const int Ch = C / heads;
+  if (Ch > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(attn_softmax_kernel, dim3(Bn * heads, (Ch + 3) / 4), dim3(256), 0, s, G, sumsq, temp, C, heads,
+                     Attn);
   return hipGetLastError();
 }
 
@@ -1071,7 +1181,8 @@ hipError_t launch_attn_bwd(const float* G, const float* sumsq, const float* temp
                            int Bn, int C, int heads, float* Mq, float* cq, float* ck, float* dtemp_part,
                            hipStream_t s) {
   const int Ch = C / heads;
-  const size_t lds = ((size_t)Ch * Ch + 256) * sizeof(float);
+  if (Ch > 128) return hipErrorInvalidValue;
+  const size_t lds = ((size_t)Ch * Ch + 4) * sizeof(float);
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(Bn * heads), dim3(256), lds, s, G, sumsq, temp, Attn, dAttn, C, heads, Mq,
                      cq, ck, dtemp_part);
   return hipGetLastError();
