@@ -3,6 +3,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <tuple>
 
 namespace kdlae {
 
@@ -176,12 +178,52 @@ int run_gemm(const GemmCall& c, hipStream_t s) {
     p.stats = c.stats_buf;
   }
   const int gy = g.group_tiles ? (int)ceil_div(g.ntiles, g.group_tiles) : (int)ceil_div(g.ntiles, g.NT);
-  int gx = (int)std::min<long long>(p.total_tiles,
-                                    std::max<long long>(1, ceil_div(g.group_tiles ? 256 * g.WPE : 1024, gy)));
-  p.tiles_per_block = (int)ceil_div(p.total_tiles, gx);
-  gx = (int)ceil_div(p.total_tiles, p.tiles_per_block);
+  p.tiles_per_block = gemm_tiles_per_block(p.total_tiles, gy, g.group_tiles != 0, g.WPE);
+  const int gx = (int)ceil_div(p.total_tiles, p.tiles_per_block);
   HIPCHK(launch_gemm(p, g.NT, g.KG, g.WPE, gx, s));
   return KDLAE_OK;
+}
+
+int device_cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      return 256;
+    return v;
+  }();
+  return n;
+}
+
+// Tiles per block for a GEMM grid of ceil(T / tpb) x gy equal-work blocks.  One 8-wave block fills
+// a CU at 2 waves/SIMD (two at 4), so the launch runs in ceil(blocks / slots) rounds and its
+// makespan is rounds x tpb tile-times.  The old "about 512 blocks" rule could land a handful of
+// blocks past a round (C192 project_in: 516 blocks = 3 rounds of 12 tiles for 24 tiles of work per
+// CU).  Resident blocks also restage their weight group once (about half a tile-time, from L2).
+int gemm_tiles_per_block(int total_tiles, int gy, bool resident, int wpe) {
+  thread_local std::map<std::tuple<int, int, bool, int>, int> memo;  // a forward repeats ~30 shapes
+  const auto key = std::make_tuple(total_tiles, gy, resident, wpe);
+  auto it = memo.find(key);
+  if (it != memo.end()) return it->second;
+  const long long slots = (long long)device_cu_count() * (wpe == 4 ? 2 : 1);
+  const int target = resident ? 256 * wpe : 1024;  // previous heuristic: the tie-break
+  const int gx0 = (int)std::min<long long>(total_tiles, std::max<long long>(1, ceil_div(target, gy)));
+  int best = (int)ceil_div(total_tiles, gx0);
+  auto cost = [&](int tpb) {
+    const long long blocks = ceil_div(total_tiles, tpb) * gy;
+    const long long rounds = ceil_div(blocks, slots);
+    return (double)rounds * (tpb + (resident ? 0.5 : 0.0));
+  };
+  double best_cost = cost(best);
+  for (int tpb = 1; tpb <= total_tiles; ++tpb) {
+    const double c = cost(tpb);
+    if (c < best_cost * 0.98) {
+      best_cost = c;
+      best = tpb;
+    }
+  }
+  memo[key] = best;
+  return best;
 }
 
 }  // namespace kdlae

@@ -112,5 +112,8 @@ struct GemmCall {
   float* stats_buf = nullptr;  // scratch [P][2] used when LN needs precomputed row stats
 };
 int run_gemm(const GemmCall& c, hipStream_t s);
+// Compute units of the current device (256 on MI355X) and the tail-aware GEMM grid split.
+int device_cu_count();
+int gemm_tiles_per_block(int total_tiles, int gy, bool resident, int wpe);
 
 }  // namespace kdlae
