@@ -379,6 +379,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
   X(6, 12, true, 1, false, 2, false) X(12, 3, true, 1, false, 2, false) X(12, 6, true, 1, false, 2, false) \
   X(3, 3, true, 2, false, 2, false) X(3, 6, true, 2, false, 2, false) X(6, 6, true, 2, false, 2, false) \
   X(6, 12, true, 2, false, 2, false) X(12, 3, true, 2, false, 2, false) X(12, 6, true, 2, false, 2, false) \
+  X(2, 6, true, 2, false, 2, false) X(2, 6, true, 1, false, 2, false) \
   X(1, 9, true, 0, false, 2, false) X(2, 9, true, 0, false, 2, false) X(4, 9, true, 0, false, 2, false) \
   X(8, 6, true, 0, false, 2, false) X(4, 6, true, 0, false, 2, false) X(2, 6, true, 0, false, 2, false) \
   X(1, 3, false, 0, false, 2, false) X(3, 4, false, 0, false, 2, false) X(4, 4, false, 2, false, 2, false) \

@@ -76,8 +76,12 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
       if (!gemm_has_variant(nt, kg, g.ksize == 3, 2, false, g.out_mode)) continue;
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
-      // every k-chunk restages weights behind two barriers; every n-chunk re-reads A
-      double cost = waste * (1.0 + 0.04 * (nch - 1) + (g.ksize == 3 ? 0.0 : 0.08 * (kch - 1)));
+      // every k-chunk restages weights behind two barriers; every n-chunk re-reads A.
+      // 3x3 (r01 probe): an n-chunk re-gathers the whole im2col A (12x3 beat 6x12 at N = 384, 768);
+      // with 12-tile chunks, halving the k-chunks (12x6) saved 2%; with 3-tile chunks 3x6 lost 12%
+      const double npen = g.ksize == 3 ? 0.12 : 0.04;
+      const double kpen = g.ksize == 3 ? (nt >= 12 ? 0.01 : 0.0) : 0.08;
+      double cost = waste * (1.0 + npen * (nch - 1) + kpen * (kch - 1));
       if (cost < best - 1e-9) {
         best = cost;
         g.NT = nt;
