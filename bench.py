@@ -19,6 +19,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -410,7 +411,11 @@ def pmc_traffic(cls):
     """HBM bytes per launch of a kernel class from the committed rocprofv3 PMC summary
     (profiles/*pmc_traffic*.json, produced by tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")))
+    def version(path):  # r01_pmc_traffic_v13.json -> (13,): numeric, so v13 sorts after v9
+        m = re.search(r"_v(\d+)\.json$", path)
+        return (int(m.group(1)) if m else -1, path)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), key=version)
     if not files:
         return None
     with open(files[-1]) as f:

@@ -205,6 +205,11 @@ __syncthreads();
 __host__ __device__ constexpr int gram_waves(int ct) {
   return ct == 1 ? 3 : ct == 2 ? 6 : ct == 3 ? 9 : ct == 4 ? 12 : ct == 5 ? 15 : ct == 6 ? 9 : ct == 7 ? 7 : 12;
 }
+#ifndef KDLAE_RING6_WAVES
+#define KDLAE_RING6_WAVES 9
+#endif
+// waves per block for the LDS-DMA ring kernel (one block per CU at CT = 6)
+__host__ __device__ constexpr int gram_ring_waves(int ct) { return ct == 6 ? KDLAE_RING6_WAVES : gram_waves(ct); }
 
 template <int CT>
 __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(GramParams p, int nseg, int seg_rows) {
@@ -362,7 +367,7 @@ __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(
 template <int CT>
 struct GramRing {
   static constexpr int Ch = CT * 16;
-  static constexpr int NW = gram_waves(CT);
+  static constexpr int NW = gram_ring_waves(CT);
   static constexpr int NJ = 3 * CT;
   static constexpr int PS4 = 3 * Ch / 4 + 1;          // float4 per ring pixel
   static constexpr int PS = 4 * PS4;                  // floats per ring pixel
@@ -383,7 +388,7 @@ struct GramRing {
 };
 
 template <int CT>
-__global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_ring_kernel(GramParams p, int seg_rows) {
+__global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_kernel(GramParams p, int seg_rows) {
   using R = GramRing<CT>;
   using dma::f32x4;
   constexpr int NW = R::NW, NJ = R::NJ, NDW = R::NDW, PPD = R::PPD;
@@ -575,7 +580,7 @@ static void launch_gram_ct(const GramParams& p, hipStream_t s) {
         (unsigned long long)p.H * p.W * p.ld * 4 < (1ull << 32)) {
       const int nseg = p.nslots / (p.W / 16);
       const int seg_rows = (p.H + nseg - 1) / nseg;
-      hipLaunchKernelGGL(dwconv_gram_ring_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(64 * gram_waves(CT)),
+      hipLaunchKernelGGL(dwconv_gram_ring_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(64 * gram_ring_waves(CT)),
                          R::lds_bytes, s, p, seg_rows);
       return;
     }
