@@ -266,7 +266,7 @@ def bench_train(args, world, rank, dev, distributed):
         one = {"img": batch["img"][:1], "denoise_rate": batch["denoise_rate"][:1]}
         gt1 = {"hq": gt["hq"][:1], "sr": gt["sr"][:1]}
         l_gpu = float(trainer.forward_backward(one, gt1))
-        g_gpu = trainer.grad.detach().cpu()
+        g_gpu = trainer.engine.packed(trainer.grad.detach()).cpu()
         l_ref, g_ref = loss_and_grads(sd, one["img"].cpu(), one["denoise_rate"].cpu(),
                                       {k: v.cpu() for k, v in gt1.items()}, TeacherCfg(**KW))
         g_ref = torch.cat([g_ref[k].reshape(-1) for k, _ in model.named_parameters()])

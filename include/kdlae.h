@@ -187,7 +187,8 @@ int kdlae_postprocess_u8(const float* out, int B, int C, int Hs, int Ws, int h, 
  * (Train/basicsr/models/image_restoration_model.py:198-218): forward with saved activations,
  * L1LossSr (Train/basicsr/models/losses/losses.py:135-194), backward of every layer,
  * clip_grad_norm_(0.01) and AdamW.  Parameters and gradients are two flat caller-owned device
- * buffers of kdlae_tt_num_floats floats in state_dict order (offsets from kdlae_tt_param_info);
+ * buffers of kdlae_tt_num_floats floats in state_dict order (offsets from kdlae_tt_param_info; each key
+ * starts on a 16-byte boundary and the pad floats between keys must be zero);
  * weights are read in their OIHW state_dict layout, so an optimizer update needs no repacking.
  * The DDP gradient all-reduce (base_model.py:76-82) is one collective over the flat gradient
  * buffer, done by the caller between kdlae_tt_backward and kdlae_train_clip_adamw.

@@ -4,7 +4,7 @@
 // (Train/basicsr/models/image_restoration_model.py:198-218).
 //
 // Parameters and their gradients live in two flat caller-owned device buffers laid out in
-// state_dict order (kdlae_tt_param_info gives each key's offset), so the optimizer is one kernel
+// state_dict order, each key 16-byte aligned (kdlae_tt_param_info gives each key's offset), so the optimizer is one kernel
 // over one buffer and the DDP gradient all-reduce is one RCCL call over one buffer.
 //
 // Workspace: [split-K partials][reduction partials][saved forward activations][backward scratch].
@@ -68,10 +68,13 @@ int hid_of(const kdlae_t_config& c, int dim) { return (int)((double)dim * c.ffn_
 // state_dict order of KDLAE_teacher (KDLAE_model.py:220-268; TransformerBlock :150-157)
 void build_keys(kdlae_tt_handle* h) {
   const kdlae_t_config& c = h->cfg;
+  // every key starts on a 16-byte boundary (pad floats stay zero), so the weight operands of the
+  // training GEMMs (temperature [heads] and ffn.dwconv [2 hid * 9] break 4-float alignment
+  // otherwise) qualify for the vectorised kernel
   auto add = [&](const std::string& k, int64_t n) {
     h->off[k] = h->total;
     h->keys.emplace_back(k, n);
-    h->total += n;
+    h->total += (n + 3) & ~int64_t(3);
   };
   auto conv = [&](const std::string& n, int co, int ci, int k, bool b) {
     add(n + ".weight", (int64_t)co * ci * k * k);
@@ -357,8 +360,16 @@ int dw_wgrad(Ctx& c, const float* dy, const float* x, int ld, int C, int Bn, int
   const long long P = (long long)Bn * H * W;
   const int nb = tr::dw_wgrad_blocks(C, Bn, H, W, nblk_for(P, 10LL * C, 256));
   LAUNCH(tr::launch_dw_wgrad(dy, ld, x, ld, C, Bn, H, W, c.red, nb, c.s));
-  const bool has_b = c.G(n + ".bias") != nullptr;
-  LAUNCH(tr::launch_part_reduce(c.red, nb, has_b ? 10 * C : 9 * C, 1, c.G(n + ".weight"), 0, 1.f, c.s, 10 * C));
+  // partial columns: [9 C weights | C bias]; one reduce when the bias key directly follows the
+  // weight key in the flat buffer (keys are 16-byte aligned, so only when 9 C % 4 == 0)
+  float* gw = c.G(n + ".weight");
+  float* gb = c.G(n + ".bias");
+  if (!gb || gb == gw + 9LL * C) {
+    LAUNCH(tr::launch_part_reduce(c.red, nb, gb ? 10 * C : 9 * C, 1, gw, 0, 1.f, c.s, 10 * C));
+  } else {
+    LAUNCH(tr::launch_part_reduce(c.red, nb, 9 * C, 1, gw, 0, 1.f, c.s, 10 * C));
+    LAUNCH(tr::launch_part_reduce(c.red + 9LL * C, nb, C, 1, gb, 0, 1.f, c.s, 10 * C));
+  }
   return KDLAE_OK;
 }
 
@@ -368,7 +379,15 @@ int ln_bwd(Ctx& c, const float* dy, const float* x, const float* st, int C, long
   const int ncol = bf ? C : 2 * C;
   const int nb = nblk_for(P, ncol);
   LAUNCH(tr::launch_ln_bwd(dy, C, x, C, c.W(n + ".weight"), st, C, P, bf, R, C, dx, C, c.red, nb, c.s));
-  LAUNCH(tr::launch_part_reduce(c.red, nb, ncol, 1, c.G(n + ".weight"), 0, 1.f, c.s));
+  // partial columns: [C weight | C bias (WithBias)], split when the keys are not adjacent
+  float* gw = c.G(n + ".weight");
+  float* gb = bf ? nullptr : c.G(n + ".bias");
+  if (!gb || gb == gw + C) {
+    LAUNCH(tr::launch_part_reduce(c.red, nb, ncol, 1, gw, 0, 1.f, c.s));
+  } else {
+    LAUNCH(tr::launch_part_reduce(c.red, nb, C, 1, gw, 0, 1.f, c.s, ncol));
+    LAUNCH(tr::launch_part_reduce(c.red + C, nb, C, 1, gb, 0, 1.f, c.s, ncol));
+  }
   return KDLAE_OK;
 }
 

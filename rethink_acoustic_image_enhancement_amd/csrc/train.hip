@@ -560,7 +560,14 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
       else if (bnc) LEAN(false, true, 1); else LEAN(false, false, 1);
     }
 #undef LEAN
-  } else if (g.amode == 0 && g.bmode == 0) launch_t<0, 0>(g, kchunk, flags, rm, grid, s);
+  } else if (g.amode == 0 && g.bmode == 0) {
+    static const bool log = getenv("KDLAE_TGEMM_LOG") != nullptr;  // shapes that miss the lean kernel
+    if (log)
+      fprintf(stderr, "tgemm-generic M=%d N=%d K=%d batch=%lld sam=%lld sak=%lld sbk=%lld sbn=%lld A%%16=%d B%%16=%d flags=%d splits=%d\n",
+              g.M, g.N, g.K, batch, (long long)g.sam, (long long)g.sak, (long long)g.sbk, (long long)g.sbn,
+              (int)((uintptr_t)g.A & 15), (int)((uintptr_t)g.B & 15), flags, splits);
+    launch_t<0, 0>(g, kchunk, flags, rm, grid, s);
+  }
   else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, flags, rm, grid, s);

@@ -84,14 +84,24 @@ class TrainEngine:
         for (k, n, off), u in zip(self.keys, self.used):
             if not u:
                 continue
+            end = off + ((n + 3) & ~3)  # keys are 16-byte aligned; the zero pad floats ride along
             if out and out[-1][1] == off:
-                out[-1][1] = off + n
+                out[-1][1] = end
             else:
-                out.append([off, off + n])
+                out.append([off, end])
         return out
 
     def flatten(self, tensors) -> torch.Tensor:
-        return torch.cat([t.detach().reshape(-1).to(torch.float32) for t in tensors])
+        """Parameters -> the handle's flat layout (state_dict order, each key 16-byte aligned, pads zero)."""
+        tensors = list(tensors)
+        flat = torch.zeros(self.numel, dtype=torch.float32, device=tensors[0].device)
+        for (k, n, off), t in zip(self.keys, tensors):
+            flat[off:off + n] = t.detach().reshape(-1).to(torch.float32)
+        return flat
+
+    def packed(self, flat) -> torch.Tensor:
+        """The flat layout without its pad floats: torch.cat of the keys in state_dict order."""
+        return torch.cat([flat[off:off + n] for _, n, off in self.keys])
 
     def _workspace(self, B, H, W):
         nbytes = int(self._L.kdlae_tt_workspace_bytes(self.handle, B, H, W))

@@ -119,7 +119,7 @@ def test_training_handle_layout_matches_module(kw):
             name, numel, off = ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_int64()
             assert L.kdlae_tt_param_info(h, i, ctypes.byref(name), ctypes.byref(numel), ctypes.byref(off)) == 0
             assert name.value.decode() == k and numel.value == p.numel() and off.value == off_expect
-            off_expect += p.numel()
+            off_expect += (p.numel() + 3) // 4 * 4  # each key 16-byte aligned
         assert L.kdlae_tt_num_floats(h) == off_expect
         # workspace for the KDLAET.yml patch setting (6 x 128^2) and a ragged-size rejection
         nb = L.kdlae_tt_workspace_bytes(h, 6, 128, 128)

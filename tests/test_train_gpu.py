@@ -59,14 +59,13 @@ def _dev(gt):
     return {k: v.to(DEV) for k, v in gt.items()}
 
 
-def _check_grads(keys, numels, flat_hip, grads_ref, used=None):
-    off = 0
+def _check_grads(keys, layout, flat_hip, grads_ref, used=None):
+    """layout: the engine's (key, numel, offset) list; flat_hip: its flat gradient buffer."""
     worst = (0.0, None)
     for i, k in enumerate(keys):
-        n = numels[i]
+        _, n, off = layout[i]
         g = flat_hip[off:off + n].double()
         r = grads_ref[k].reshape(-1).double()
-        off += n
         if used is not None and not used[i]:
             assert float(g.abs().max()) == 0.0, k
             continue
@@ -88,8 +87,12 @@ def test_trainer_loss_and_grads_match_oracle(name):
     assert abs(float(loss) - float(loss_ref)) <= 1e-5 * abs(float(loss_ref))
     assert abs(float(loss) - d["loss"][0]) <= 1e-5 * abs(d["loss"][0])
     flat = tr.grad.cpu()
-    numels = [n for _, n, _ in tr.engine.keys]
-    _check_grads(keys, numels, flat, grads_ref, tr.engine.used)
+    _check_grads(keys, tr.engine.keys, flat, grads_ref, tr.engine.used)
+    pad = torch.ones(flat.numel(), dtype=torch.bool)  # the 16-byte alignment pads between keys stay zero
+    for _, n, off in tr.engine.keys:
+        pad[off:off + n] = False
+    assert not pad.any() or float(flat[pad].abs().max()) == 0.0
+    flat = tr.engine.packed(flat)
     # against the reference's own gradients (every 5th element of the flat buffer)
     sub = d["grad1_sub"]
     assert np.abs(flat.numpy()[::5] - sub).max() <= 2e-3 * np.abs(sub).max()
@@ -208,7 +211,7 @@ def test_full_config_small_image_matches_oracle():
     torch.cuda.synchronize()
     loss_ref, grads_ref = _oracle(cfg, keys, img, rate, gt)
     assert abs(float(loss) - float(loss_ref)) <= 1e-5 * abs(float(loss_ref))
-    _check_grads(keys, [n for _, n, _ in tr.engine.keys], tr.grad.cpu(), grads_ref)
+    _check_grads(keys, tr.engine.keys, tr.grad.cpu(), grads_ref)
 
 
 def test_full_size_step_properties():
