@@ -34,6 +34,7 @@ struct BlockRec {
   float *x = nullptr, *xn1 = nullptr, *st1 = nullptr, *qkv = nullptr, *qkvd = nullptr, *sumsq = nullptr, *G = nullptr,
         *A = nullptr, *ao = nullptr, *x1 = nullptr, *xn2 = nullptr, *st2 = nullptr, *y = nullptr, *yd = nullptr,
         *g = nullptr, *out = nullptr;
+  float* wpo = nullptr;  // ffn.project_out weight with rows padded to ld4(hid) (odd hid only), zero pads
 };
 
 struct Saved {
@@ -207,11 +208,12 @@ struct V {
   int ld;
 };
 
+// wp (optional): the weight as [Cout][ldw] rows (a padded copy), else the flat buffer's [Cout][Cin]
 int conv1(Ctx& c, const std::string& n, V x, int Cin, int Cout, long long P, V out, const float* R = nullptr,
-          int ldr = 0) {
+          int ldr = 0, V wp = {nullptr, 0}) {
   tr::TGemm g;
   g.A = x.p; g.sam = x.ld; g.sak = 1;
-  g.B = c.W(n + ".weight"); g.sbk = 1; g.sbn = Cin;
+  g.B = wp.p ? wp.p : c.W(n + ".weight"); g.sbk = 1; g.sbn = wp.p ? wp.ld : Cin;
   g.C = out.p; g.scm = out.ld; g.scn = 1;
   g.bias = c.W(n + ".bias");
   g.R = R; g.srm = ldr; g.srn = 1;
@@ -230,7 +232,7 @@ int bias_grad(Ctx& c, V dy, int N, long long P, float* out) {
 
 // dW = dY^T X, db = colsum dY, dX = dY W (+R)
 int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long long P, V dx, const float* R = nullptr,
-              int ldr = 0) {
+              int ldr = 0, V wp = {nullptr, 0}) {
   tr::TGemm g;
   g.A = dy.p; g.sam = 1; g.sak = dy.ld;
   g.B = x.p; g.sbk = x.ld; g.sbn = 1;
@@ -242,7 +244,7 @@ int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long l
   if (dx.p) {
     tr::TGemm d;
     d.A = dy.p; d.sam = dy.ld; d.sak = 1;
-    d.B = c.W(n + ".weight"); d.sbk = Cin; d.sbn = 1;
+    d.B = wp.p ? wp.p : c.W(n + ".weight"); d.sbk = wp.p ? wp.ld : Cin; d.sbn = 1;
     d.C = dx.p; d.scm = dx.ld; d.scn = 1;
     d.R = R; d.srm = ldr; d.srn = 1;
     d.M = (int)P; d.N = Cin; d.K = Cout;
@@ -352,7 +354,14 @@ int block_fwd(Ctx& c, BlockRec& r) {
   r.g = c.alloc(P * L1);
   LAUNCH(tr::launch_gate_fwd(r.yd, L2, hid, P, r.g, L1, c.s));
   r.out = c.alloc(P * C);
-  TRY(conv1(c, p + ".ffn.project_out", {r.g, L1}, hid, C, P, {r.out, C}, r.x1, C));
+  if (hid % 4) {
+    // row stride hid is not a multiple of 4 floats: a zero-padded [C][ld4(hid)] copy lets the forward
+    // and dX GEMMs use the vectorised kernel (kept until the backward: theta is unchanged in between)
+    r.wpo = c.alloc((size_t)C * L1);
+    LAUNCH(hipMemsetAsync(r.wpo, 0, (size_t)C * L1 * sizeof(float), c.s));
+    LAUNCH(tr::launch_copy_cols(c.W(p + ".ffn.project_out.weight"), hid, r.wpo, L1, hid, C, 0, c.s));
+  }
+  TRY(conv1(c, p + ".ffn.project_out", {r.g, L1}, hid, C, P, {r.out, C}, r.x1, C, {r.wpo, L1}));
   return KDLAE_OK;
 }
 
@@ -400,7 +409,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   // ffn (KDLAE_model.py:101-106)
   const int L2 = ld4(2 * hid), L1 = ld4(hid);
   float* dg = c.alloc(P * L1);
-  TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, L1}, {d, C}, hid, C, P, {dg, L1}));
+  TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, L1}, {d, C}, hid, C, P, {dg, L1}, nullptr, 0, {r.wpo, L1}));
   float* dyd = c.alloc(P * L2);
   LAUNCH(tr::launch_gate_bwd(dg, L1, r.yd, L2, hid, P, dyd, L2, c.s));
   float* dy = c.alloc(P * L2);
