@@ -375,6 +375,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
   X(3, 3, false, 0, false, 2, false) X(6, 6, false, 0, false, 2, false) X(9, 12, false, 0, false, 2, false) \
   X(8, 12, false, 0, false, 2, false) X(6, 12, false, 0, false, 2, false) X(3, 12, false, 0, false, 2, false) \
   X(6, 16, false, 0, false, 2, false) X(3, 16, false, 0, false, 2, false) \
+  X(12, 8, false, 0, false, 2, false) \
   X(3, 3, true, 1, false, 2, false) X(3, 6, true, 1, false, 2, false) X(6, 6, true, 1, false, 2, false) \
   X(6, 12, true, 1, false, 2, false) X(12, 3, true, 1, false, 2, false) X(12, 6, true, 1, false, 2, false) \
   X(3, 3, true, 2, false, 2, false) X(3, 6, true, 2, false, 2, false) X(6, 6, true, 2, false, 2, false) \

@@ -77,10 +77,18 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
       // every k-chunk restages weights behind two barriers; every n-chunk re-reads A.
+      // 1x1 (r01 v15 probe): n-chunks cost more than k-chunks; with penalties 0.06 / 0.02 the
+      // K = 510/1021 FFN project_out and the C384 GEMMs take 12x8 chunks (72 -> 85 and 76 -> 90 TF/s)
       // 3x3 (r01 probe): an n-chunk re-gathers the whole im2col A (12x3 beat 6x12 at N = 384, 768);
       // with 12-tile chunks, halving the k-chunks (12x6) saved 2%; with 3-tile chunks 3x6 lost 12%
-      const double npen = g.ksize == 3 ? 0.12 : 0.04;
-      const double kpen = g.ksize == 3 ? (nt >= 12 ? 0.01 : 0.0) : 0.08;
+#ifndef KDLAE_NPEN_1X1
+#define KDLAE_NPEN_1X1 0.06
+#endif
+      const double npen = g.ksize == 3 ? 0.12 : KDLAE_NPEN_1X1;
+#ifndef KDLAE_KPEN_1X1
+#define KDLAE_KPEN_1X1 0.02
+#endif
+      const double kpen = g.ksize == 3 ? (nt >= 12 ? 0.01 : 0.0) : KDLAE_KPEN_1X1;
       double cost = waste * (1.0 + npen * (nch - 1) + kpen * (kch - 1));
       if (cost < best - 1e-9) {
         best = cost;
