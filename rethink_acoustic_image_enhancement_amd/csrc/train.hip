@@ -506,6 +506,12 @@ static bool getenv_generic() {
   return on;
 }
 
+#ifndef KDLAE_SPLITK_BLOCKS
+#define KDLAE_SPLITK_BLOCKS 2048
+#endif
+#ifndef KDLAE_SPLITK_MIN
+#define KDLAE_SPLITK_MIN 256
+#endif
 hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   const long long batch = (long long)g.nz1 * g.nz2;
@@ -514,10 +520,10 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   const int tiles = ((g.M + 64 * rm - 1) / (64 * rm)) * ((g.N + BN - 1) / BN);
   int splits = 1;
   if (g.partial && partial_cap > 0) {
-    // fill ~2048 blocks, each split at least 256 deep
+    // fill ~KDLAE_SPLITK_BLOCKS blocks, each split at least KDLAE_SPLITK_MIN deep
     const long long blocks = tiles * batch;
-    long long want = (2048 + blocks - 1) / blocks;
-    const long long maxk = (g.K + 255) / 256;
+    long long want = (KDLAE_SPLITK_BLOCKS + blocks - 1) / blocks;
+    const long long maxk = (g.K + KDLAE_SPLITK_MIN - 1) / KDLAE_SPLITK_MIN;
     if (want > maxk) want = maxk;
     const long long cap = (long long)(partial_cap / ((size_t)g.M * g.N * batch));
     if (want > cap) want = cap;
