@@ -209,7 +209,12 @@ __host__ __device__ constexpr int gram_waves(int ct) {
 #define KDLAE_RING6_WAVES 9
 #endif
 // waves per block for the LDS-DMA ring kernel (one block per CU at CT = 6)
-__host__ __device__ constexpr int gram_ring_waves(int ct) { return ct == 6 ? KDLAE_RING6_WAVES : gram_waves(ct); }
+#ifndef KDLAE_RING3_WAVES
+#define KDLAE_RING3_WAVES 9
+#endif
+__host__ __device__ constexpr int gram_ring_waves(int ct) {
+  return ct == 6 ? KDLAE_RING6_WAVES : ct == 3 ? KDLAE_RING3_WAVES : gram_waves(ct);
+}
 
 template <int CT>
 __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(GramParams p, int nseg, int seg_rows) {
