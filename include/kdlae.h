@@ -7,8 +7,11 @@
  * beside it.  All pointers are device pointers unless marked host; tensors
  * are fp32, contiguous NCHW exactly as the reference consumes/produces them.
  * `stream` is a hipStream_t (0 = null stream).  Nothing here allocates,
- * frees or synchronises inside *_forward: activations, outputs and the
- * workspace are caller-owned; the handle owns only packed weights.
+ * frees or synchronises inside *_forward / *_pack_device: activations,
+ * outputs, the flat parameter vector and the workspace are caller-owned;
+ * the handle owns only the packed weights and their pack program.  Every
+ * call makes the handle's device current and restores the caller's device
+ * before returning.
  *
  * Error handling: every call returns KDLAE_OK (0) or one of the codes
  * below; kdlae_last_error() returns a thread-local message describing the
@@ -63,12 +66,18 @@ int kdlae_t_create(const kdlae_t_config* cfg, int device, kdlae_t_handle** out);
 int kdlae_t_destroy(kdlae_t_handle* h);
 
 /* state_dict surface (KDLAE_model.py:220-268 key layout; load_state_dict at KDLAE_T.ipynb:1074-1075).
- * kdlae_t_num_params / kdlae_t_param_info enumerate the expected keys and element counts;
- * kdlae_t_set_param stages one entry from HOST memory (strict: unknown key or numel mismatch
- * -> KDLAE_EPARAM); kdlae_t_commit_params packs every staged entry into the device layout
- * (LN weight folded into 1x1 weights, NHWC/MFMA fragment order) and uploads it on `stream`. */
+ * kdlae_t_num_params / kdlae_t_param_info enumerate the expected keys and element counts, in
+ * state_dict order.  The packed device layout (LN weight folded into 1x1 weights, NHWC/MFMA
+ * fragment order) is produced ON THE DEVICE by the handle's pack program from the flat fp32
+ * parameter vector (every key in that order, back to back; kdlae_t_params_numel floats):
+ *   kdlae_t_pack_device(params = DEVICE flat vector) enqueues the pack on `stream` (no sync) and
+ *     is what the nn.Module calls before every forward, so the packed copy never goes stale;
+ *   kdlae_t_set_param stages one entry from HOST memory (strict: unknown key or numel mismatch
+ *     -> KDLAE_EPARAM) and kdlae_t_commit_params packs the staged set (synchronous). */
 int kdlae_t_num_params(const kdlae_t_handle* h);
 int kdlae_t_param_info(const kdlae_t_handle* h, int index, const char** name, int64_t* numel);
+int64_t kdlae_t_params_numel(const kdlae_t_handle* h);
+int kdlae_t_pack_device(kdlae_t_handle* h, const float* params, int64_t numel, void* stream);
 int kdlae_t_set_param(kdlae_t_handle* h, const char* name, const float* host_data, int64_t numel);
 int kdlae_t_commit_params(kdlae_t_handle* h, void* stream);
 
@@ -118,6 +127,8 @@ int kdlae_s_destroy(kdlae_s_handle* h);
  * out_conv (same semantics as the kdlae_t_* calls). */
 int kdlae_s_num_params(const kdlae_s_handle* h);
 int kdlae_s_param_info(const kdlae_s_handle* h, int index, const char** name, int64_t* numel);
+int64_t kdlae_s_params_numel(const kdlae_s_handle* h);
+int kdlae_s_pack_device(kdlae_s_handle* h, const float* params, int64_t numel, void* stream);
 int kdlae_s_set_param(kdlae_s_handle* h, const char* name, const float* host_data, int64_t numel);
 int kdlae_s_commit_params(kdlae_s_handle* h, void* stream);
 int64_t kdlae_s_workspace_bytes(const kdlae_s_handle* h, int B, int F, int H, int W);
@@ -144,9 +155,13 @@ typedef struct asdqe_handle asdqe_handle;
 int asdqe_create(const asdqe_config* cfg, int device, asdqe_handle** out);
 int asdqe_destroy(asdqe_handle* h);
 /* state_dict surface incl. BatchNorm buffers (num_batches_tracked: 1 element, ignored).  The
- * reference loads its checkpoint with strict=False (ASDQE_test.py:79); this surface is strict. */
+ * reference loads its checkpoint with strict=False (ASDQE_test.py:79); this surface is strict.
+ * The BatchNorm fold (W' = W g / sqrt(var + 1e-5), b' = (b - mean) g / sqrt(var + 1e-5) + beta) is
+ * part of the device pack program (asdqe_pack_device, same contract as kdlae_t_pack_device). */
 int asdqe_num_params(const asdqe_handle* h);
 int asdqe_param_info(const asdqe_handle* h, int index, const char** name, int64_t* numel);
+int64_t asdqe_params_numel(const asdqe_handle* h);
+int asdqe_pack_device(asdqe_handle* h, const float* params, int64_t numel, void* stream);
 int asdqe_set_param(asdqe_handle* h, const char* name, const float* host_data, int64_t numel);
 int asdqe_commit_params(asdqe_handle* h, void* stream);
 int64_t asdqe_workspace_bytes(const asdqe_handle* h, int B, int H, int W);

@@ -111,9 +111,14 @@ def _stage(n, dim, heads, ffn, bias, ln):
 
 
 class _Engine:
-    """One C-ABI handle per (module, device); re-packs weights when any parameter changes.
+    """One C-ABI handle per (module, device).
 
-    ``prefix`` selects the handle family: ``kdlae_t`` (teacher) or ``kdlae_s`` (student)."""
+    ``prefix`` selects the handle family: ``kdlae_t`` (teacher), ``kdlae_s`` (student) or ``asdqe``.
+    The packed weights are rebuilt ON THE DEVICE from the module's live parameters at every forward
+    (``<prefix>_pack_device``: one ``torch.cat`` of the state_dict into a flat fp32 buffer, then the
+    handle's pack program, ~0.1 ms for KDLAE-T).  Nothing is cached across forwards, so in-place
+    writes that bypass autograd's version counter (``p.data.mul_()``, BasicSR's ``model_ema``,
+    base_model.py:54-62), optimizer steps and ``load_state_dict`` are always seen."""
 
     def __init__(self, cfg, device_index: int, prefix: str = "kdlae_t"):
         L = _lib.lib()
@@ -123,24 +128,55 @@ class _Engine:
                    prefix + "_create")
         self.handle = h
         self.device_index = device_index
-        self.signature = None
         self.ws = None
+        self.flat = None
+        self._src_sig = None
+        self._srcs = None
         self._fin = weakref.finalize(self, getattr(L, prefix + "_destroy"), h)
+        names = []
+        for i in range(getattr(L, prefix + "_num_params")(h)):
+            name, numel = ctypes.c_char_p(), ctypes.c_int64()
+            _lib.check(getattr(L, prefix + "_param_info")(h, i, ctypes.byref(name), ctypes.byref(numel)),
+                       prefix + "_param_info")
+            names.append((name.value.decode(), int(numel.value)))
+        self.keys = names
+        self.numel = int(getattr(L, prefix + "_params_numel")(h))
+
+    def _sources(self, module: nn.Module, device) -> list:
+        tensors = list(module.parameters()) + list(module.buffers())
+        sig = (len(tensors),) + tuple(t.data_ptr() for t in tensors)  # identity of the storages, not values
+        if sig != self._src_sig:
+            if not tensors and self.keys:
+                raise RuntimeError(f"{type(module).__name__}: the module has no registered parameters (an "
+                                   "nn.DataParallel replica?). The MI355X build runs one process per GPU: use "
+                                   "DistributedDataParallel / torchrun instead of nn.DataParallel")
+            sd = module.state_dict(keep_vars=True)
+            missing = [k for k, _ in self.keys if k not in sd]
+            if missing:
+                raise RuntimeError(f"{type(module).__name__}: state_dict lacks {missing[:4]} "
+                                   f"({len(missing)} missing keys)")
+            srcs = []
+            for k, n in self.keys:
+                t = sd[k].detach()
+                if t.numel() != n:
+                    raise RuntimeError(f"size mismatch for {k}: expected {n} elements, got {t.numel()}")
+                if t.device != device:
+                    raise RuntimeError(f"{k} is on {t.device}, the input on {device}: move the model with .to()")
+                # fp32 contiguous storage: keep an aliasing view (reads the live values every forward)
+                srcs.append(t.view(-1) if t.dtype == torch.float32 and t.is_contiguous() else t)
+            self._srcs, self._src_sig = srcs, sig
+        return [t if t.dim() == 1 and t.dtype == torch.float32 else t.reshape(-1).to(torch.float32)
+                for t in self._srcs]
 
     def sync_params(self, module: nn.Module, stream) -> None:
-        params = list(module.parameters()) + list(module.buffers())
-        sig = tuple((id(p), p._version, p.data_ptr()) for p in params)
-        if sig == self.signature:
-            return
-        L = _lib.lib()
-        for name, t in module.state_dict().items():
-            host = t.detach().to("cpu", torch.float32).contiguous()
-            _lib.check(getattr(L, self.prefix + "_set_param")(self.handle, name.encode(),
-                                                              ctypes.c_void_p(host.data_ptr()), host.numel()),
-                       f"load {name}")
-        _lib.check(getattr(L, self.prefix + "_commit_params")(self.handle, ctypes.c_void_p(stream)),
-                   self.prefix + "_commit_params")
-        self.signature = sig
+        """Pack the module's current parameters into the handle's device arena (on ``stream``)."""
+        device = torch.device("cuda", self.device_index)
+        if self.flat is None or self.flat.device != device:
+            self.flat = torch.empty(self.numel, dtype=torch.float32, device=device)
+        torch.cat(self._sources(module, device), out=self.flat)
+        _lib.check(getattr(_lib.lib(), self.prefix + "_pack_device")(
+            self.handle, ctypes.c_void_p(self.flat.data_ptr()), self.numel, ctypes.c_void_p(stream)),
+            self.prefix + "_pack_device")
 
     def workspace(self, nbytes: int, device) -> torch.Tensor:
         if self.ws is None or self.ws.numel() < nbytes:

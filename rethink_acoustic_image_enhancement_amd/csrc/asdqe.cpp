@@ -24,8 +24,8 @@ struct asdqe_handle {
   asdqe_config cfg{};
   int device = 0;
   ParamStore ps;
-  bool committed = false;
-  DeviceWeights dw;
+  bool built = false, committed = false;
+  DeviceWeights dw;        // packed arena + the pack program that fills it from the parameters
   SmallW ext1[3];
   Gemm ext2[3];
   Gemm inc[2], dn[3][2], upc[3][2];
@@ -42,9 +42,11 @@ const char* kUp[3] = {"unet.up1.conv.double_conv", "unet.up2.conv.double_conv", 
 const int kDownC[3][2] = {{64, 128}, {128, 256}, {256, 256}};
 const int kUpC[3][2] = {{512, 128}, {256, 64}, {128, 64}};
 
-int gap_slots(int B) {
-  int s = (2048 + B - 1) / B;
-  return std::max(1, std::min(256, s));
+// GAP partial slots per image: a function of the padded image size only, so an image's pooled
+// features are summed in the same order whatever the batch (bit-identical batch invariance).
+int gap_slots(long long HW) {
+  long long s = HW / 2048;
+  return (int)std::max<long long>(1, std::min<long long>(256, s));
 }
 
 struct APlan {
@@ -80,7 +82,7 @@ APlan make_aplan(const asdqe_handle* h, int B, int H, int W) {
   pl.p3 = pl.take(P3 * 256);
   pl.t3 = pl.take(P3 * 256);
   pl.x4 = pl.take(P3 * 256);
-  pl.slots = gap_slots(B);
+  pl.slots = gap_slots((long long)pl.Hp * pl.Wp);
   pl.partial = pl.take((long long)B * pl.slots * 64);
   return pl;
 }
@@ -129,7 +131,10 @@ int asdqe_create(const asdqe_config* cfg, int device, asdqe_handle** out) {
 
 int asdqe_destroy(asdqe_handle* h) {
   if (!h) return KDLAE_OK;
-  h->dw.release();
+  {
+    DeviceGuard g(h->device);
+    h->dw.release();
+  }
   delete h;
   return KDLAE_OK;
 }
@@ -141,42 +146,54 @@ int asdqe_param_info(const asdqe_handle* h, int index, const char** name, int64_
   return h->ps.info(index, name, numel);
 }
 
+int64_t asdqe_params_numel(const asdqe_handle* h) { return h ? h->ps.total : -1; }
+
 int asdqe_set_param(asdqe_handle* h, const char* name, const float* host_data, int64_t numel) {
   if (!h || !name || !host_data) return fail(KDLAE_ESTATE, "null argument");
-  int rc = h->ps.set(name, host_data, numel);
-  if (rc == KDLAE_OK) h->committed = false;
-  return rc;
+  return h->ps.set(name, host_data, numel);
 }
 
-int asdqe_commit_params(asdqe_handle* h, void* stream) {
-  if (!h) return fail(KDLAE_ESTATE, "null handle");
-  int rc = h->ps.check_complete();
-  if (rc) return rc;
-  HIPCHK(hipSetDevice(h->device));
-  Arena ar;
+}  // extern "C"
+
+// Records the packed layout (pack program, runtime.h) of this configuration once per handle.
+static int build_program_a(asdqe_handle* h) {
+  if (h->built) return KDLAE_OK;
+  PackProgram ar;
+  ar.nsrc = h->ps.total;
   int err = KDLAE_OK;
-  // BatchNorm2d eval (eps 1e-5) folded into the preceding conv: W' = s W, b' = s (b - rm) + beta
-  auto bn_fold = [&](const std::string& conv, const std::string& bn, int cout, std::vector<float>& s,
-                     std::vector<float>& t) {
-    const std::vector<float>* B = h->ps.get(conv + ".bias", &err);
-    const std::vector<float>* g = h->ps.get(bn + ".weight", &err);
-    const std::vector<float>* be = h->ps.get(bn + ".bias", &err);
-    const std::vector<float>* rm = h->ps.get(bn + ".running_mean", &err);
-    const std::vector<float>* rv = h->ps.get(bn + ".running_var", &err);
-    s.assign(cout, 0.f);
-    t.assign(cout, 0.f);
+  // BatchNorm2d eval (eps 1e-5) folded into the preceding conv: W' = s W, b' = s (b - rm) + beta,
+  // s = gamma / sqrt(rv + eps): s and b' are derived values computed on the device before the gathers
+  auto bn_fold = [&](const std::string& conv, const std::string& bn, int cout, std::vector<int32_t>& sc,
+                     std::vector<int32_t>& sh) {
+    const int32_t B = h->ps.base(conv + ".bias", &err);
+    const int32_t g = h->ps.base(bn + ".weight", &err);
+    const int32_t be = h->ps.base(bn + ".bias", &err);
+    const int32_t rm = h->ps.base(bn + ".running_mean", &err);
+    const int32_t rv = h->ps.base(bn + ".running_var", &err);
+    sc.assign(cout, -1);
+    sh.assign(cout, -1);
     if (err) return;
     for (int n = 0; n < cout; ++n) {
-      s[n] = (*g)[n] / std::sqrt((*rv)[n] + 1e-5f);
-      t[n] = ((*B)[n] - (*rm)[n]) * s[n] + (*be)[n];
+      PDer d0;
+      d0.kind = 0;
+      d0.a = g + n;
+      d0.b = rv + n;
+      sc[n] = ar.derive(d0);
+      PDer d1;
+      d1.kind = 1;
+      d1.a = B + n;
+      d1.b = rm + n;
+      d1.c = sc[n];
+      d1.d = be + n;
+      sh[n] = ar.derive(d1);
     }
   };
   auto conv3 = [&](const std::string& p, int i, int cin, int cout) {
     Gemm g;
     const std::string cv = p + "." + std::to_string(i), bn = p + "." + std::to_string(i + 1);
-    const std::vector<float>* W = h->ps.get(cv + ".weight", &err);
-    std::vector<float> s, t;
-    bn_fold(cv, bn, cout, s, t);
+    const int32_t W = h->ps.base(cv + ".weight", &err);
+    std::vector<int32_t> sc, sh;
+    bn_fold(cv, bn, cout, sc, sh);
     if (err) return g;
     const int cis = ru16(cin), cos = ru16(cout);
     g.ksize = 3;
@@ -187,13 +204,13 @@ int asdqe_commit_params(asdqe_handle* h, void* stream) {
     g.K = 9 * cis;
     g.n_true = cout;
     g.k_true = 9 * cin;
-    g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> float {
+    g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
       const int tap = k / cis, c = k - tap * cis;
-      if (n >= cout || c >= cin) return 0.f;
-      return (*W)[((size_t)n * cin + c) * 9 + tap] * s[n];
+      if (n >= cout || c >= cin) return PEx{};
+      return PEx{W + (n * cin + c) * 9 + tap, sc[n]};
     }));
-    std::vector<float> b((size_t)cos, 0.f);
-    for (int n = 0; n < cout; ++n) b[n] = t[n];
+    std::vector<PEx> b((size_t)cos);
+    for (int n = 0; n < cout; ++n) b[n].a = sh[n];
     g.bias = ar.add(b);
     choose_variant(g);
     return g;
@@ -201,13 +218,15 @@ int asdqe_commit_params(asdqe_handle* h, void* stream) {
   const int d = h->cfg.dim, m = 3 * d, ci = h->cfg.in_channels;
   for (int e = 0; e < 3; ++e) {
     const std::string p = std::string(kExt[e]) + ".double_conv";
-    const std::vector<float>* W = h->ps.get(p + ".0.weight", &err);
-    std::vector<float> s, t;
-    bn_fold(p + ".0", p + ".1", d, s, t);
+    const int32_t W = h->ps.base(p + ".0.weight", &err);
+    std::vector<int32_t> sc, sh;
+    bn_fold(p + ".0", p + ".1", d, sc, sh);
     if (err) return err;
-    std::vector<float> w((size_t)d * ci * 9);
-    for (int n = 0; n < d; ++n)
-      for (int k = 0; k < ci * 9; ++k) w[(size_t)n * ci * 9 + k] = (*W)[(size_t)n * ci * 9 + k] * s[n];
+    std::vector<PEx> w((size_t)d * ci * 9), t((size_t)d);
+    for (int n = 0; n < d; ++n) {
+      for (int k = 0; k < ci * 9; ++k) w[(size_t)n * ci * 9 + k] = PEx{W + n * ci * 9 + k, sc[n]};
+      t[n].a = sh[n];
+    }
     h->ext1[e].w = ar.add(w);
     h->ext1[e].bias = ar.add(t);
     h->ext1[e].Cin = ci;
@@ -223,8 +242,8 @@ int asdqe_commit_params(asdqe_handle* h, void* stream) {
     h->upc[i][1] = conv3(kUp[i], 3, kUpC[i][1], kUpC[i][1]);
   }
   {
-    const std::vector<float>* W = h->ps.get("unet.outc.conv.weight", &err);
-    const std::vector<float>* Bv = h->ps.get("unet.outc.conv.bias", &err);
+    const int32_t W = h->ps.base("unet.outc.conv.weight", &err);
+    const int32_t Bv = h->ps.base("unet.outc.conv.bias", &err);
     if (err) return err;
     Gemm& g = h->outc;
     g.ntiles = ru16(m) / 16;
@@ -233,29 +252,56 @@ int asdqe_commit_params(asdqe_handle* h, void* stream) {
     g.K = 64;
     g.n_true = m;
     g.k_true = 64;
-    g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> float {
-      return n < m ? (*W)[(size_t)n * 64 + k] : 0.f;
+    g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
+      return n < m ? PEx{W + n * 64 + k, -1} : PEx{};
     }));
-    std::vector<float> b((size_t)g.N, 0.f);
-    for (int n = 0; n < m; ++n) b[n] = (*Bv)[n];
+    std::vector<PEx> b((size_t)g.N);
+    for (int n = 0; n < m; ++n) b[n].a = Bv + n;
     g.bias = ar.add(b);
     choose_variant(g);
-    h->wo = ar.add(*W);
-    h->bo = ar.add(*Bv);
+    h->wo = ar.copy(W, (size_t)m * 64);
+    h->bo = ar.copy(Bv, m);
   }
-  auto raw = [&](const char* k) {
-    const std::vector<float>* v = h->ps.get(k, &err);
-    return v ? ar.add(*v) : kNone;
+  auto raw = [&](const char* k, size_t n) {
+    const int32_t b = h->ps.base(k, &err);
+    return b >= 0 ? ar.copy(b, n) : kNone;
   };
-  h->w1 = raw("regressor.2.weight");
-  h->b1 = raw("regressor.2.bias");
-  h->w2 = raw("regressor.5.weight");
-  h->b2 = raw("regressor.5.bias");
-  h->w3 = raw("regressor.8.weight");
-  h->b3 = raw("regressor.8.bias");
+  h->w1 = raw("regressor.2.weight", (size_t)256 * m);
+  h->b1 = raw("regressor.2.bias", 256);
+  h->w2 = raw("regressor.5.weight", 256 * 64);
+  h->b2 = raw("regressor.5.bias", 64);
+  h->w3 = raw("regressor.8.weight", 64);
+  h->b3 = raw("regressor.8.bias", 1);
   if (err) return err;
-  rc = h->dw.upload(ar, reinterpret_cast<hipStream_t>(stream));
+  DeviceGuard dg(h->device);
+  int rc = h->dw.upload_program(ar);
   if (rc) return rc;
+  h->built = true;
+  return KDLAE_OK;
+}
+
+extern "C" {
+
+int asdqe_commit_params(asdqe_handle* h, void* stream) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  int rc = h->ps.check_complete();
+  if (rc) return rc;
+  if ((rc = build_program_a(h))) return rc;
+  DeviceGuard g(h->device);
+  if ((rc = h->dw.run_host(h->ps.flat(), reinterpret_cast<hipStream_t>(stream)))) return rc;
+  h->committed = true;
+  return KDLAE_OK;
+}
+
+int asdqe_pack_device(asdqe_handle* h, const float* params, int64_t numel, void* stream) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  if (numel != h->ps.total)
+    return fail(KDLAE_EPARAM, "flat parameter vector has " + std::to_string(numel) + " floats, expected " +
+                                  std::to_string(h->ps.total));
+  int rc = build_program_a(h);
+  if (rc) return rc;
+  DeviceGuard g(h->device);
+  if ((rc = h->dw.run(params, reinterpret_cast<hipStream_t>(stream)))) return rc;
   h->committed = true;
   return KDLAE_OK;
 }
@@ -272,12 +318,12 @@ int64_t asdqe_workspace_bytes(const asdqe_handle* h, int B, int H, int W) {
 int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int H, int W, float* score, float* feat,
                   void* workspace, int64_t workspace_bytes, void* stream) {
   if (!h) return fail(KDLAE_ESTATE, "null handle");
-  if (!h->committed) return fail(KDLAE_ESTATE, "forward before asdqe_commit_params");
+  if (!h->committed) return fail(KDLAE_ESTATE, "forward before asdqe_commit_params / asdqe_pack_device");
   if (B <= 0 || H <= 0 || W <= 0) return fail(KDLAE_EINVAL_SHAPE, "B, H, W must be positive");
   if (!lq || !gt || !score || !workspace) return fail(KDLAE_ESTATE, "null tensor");
   APlan pl = make_aplan(h, B, H, W);
   if ((int64_t)pl.total > workspace_bytes) return fail(KDLAE_ESTATE, "workspace too small");
-  HIPCHK(hipSetDevice(h->device));
+  DeviceGuard dg(h->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   char* ws = reinterpret_cast<char*>(workspace);
   auto buf = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };

@@ -396,13 +396,16 @@ bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident, int ou
 
 template <int NT, int KG, bool C3, int OUT, bool PF, int WPE, bool RES>
 static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
-  static size_t attr_lds = 0;
-  if (lds > attr_lds) {
+  // the dynamic-LDS attribute is per device: one high-water mark per device id
+  static size_t attr_lds[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (lds > attr_lds[dev]) {
     hipError_t e = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&conv_gemm_kernel<NT, KG, C3, OUT, PF, WPE, RES>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attr_lds = lds;
+    attr_lds[dev] = lds;
   }
   hipLaunchKernelGGL((conv_gemm_kernel<NT, KG, C3, OUT, PF, WPE, RES>), dim3(grid_x, grid_y), dim3(kGemmThreads),
                      lds, s, p);

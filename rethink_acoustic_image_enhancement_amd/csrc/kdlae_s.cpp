@@ -26,8 +26,8 @@ struct kdlae_s_handle {
   int L = 0;               // levels = len(hidden_channels) - 1
   std::vector<int> hc, cs;  // hidden channels, padded to 16
   ParamStore ps;
-  bool committed = false;
-  DeviceWeights dw;
+  bool built = false, committed = false;
+  DeviceWeights dw;        // packed arena + the pack program that fills it from the parameters
   struct Block { Gemm a, b; };
   SmallW first;             // encoders.0.0 (Cin = 1), stored padded [cs0][27]
   std::vector<Block> enc, dec;
@@ -120,7 +120,10 @@ int kdlae_s_create(const kdlae_s_config* cfg, int device, kdlae_s_handle** out) 
 
 int kdlae_s_destroy(kdlae_s_handle* h) {
   if (!h) return KDLAE_OK;
-  h->dw.release();
+  {
+    DeviceGuard g(h->device);
+    h->dw.release();
+  }
   delete h;
   return KDLAE_OK;
 }
@@ -132,23 +135,24 @@ int kdlae_s_param_info(const kdlae_s_handle* h, int index, const char** name, in
   return h->ps.info(index, name, numel);
 }
 
+int64_t kdlae_s_params_numel(const kdlae_s_handle* h) { return h ? h->ps.total : -1; }
+
 int kdlae_s_set_param(kdlae_s_handle* h, const char* name, const float* host_data, int64_t numel) {
   if (!h || !name || !host_data) return fail(KDLAE_ESTATE, "null argument");
-  int rc = h->ps.set(name, host_data, numel);
-  if (rc == KDLAE_OK) h->committed = false;
-  return rc;
+  return h->ps.set(name, host_data, numel);
 }
 
-int kdlae_s_commit_params(kdlae_s_handle* h, void* stream) {
-  if (!h) return fail(KDLAE_ESTATE, "null handle");
-  int rc = h->ps.check_complete();
-  if (rc) return rc;
-  HIPCHK(hipSetDevice(h->device));
-  Arena ar;
+}  // extern "C"
+
+// Records the packed layout (pack program, runtime.h) of this configuration once per handle.
+static int build_program_s(kdlae_s_handle* h) {
+  if (h->built) return KDLAE_OK;
+  PackProgram ar;
+  ar.nsrc = h->ps.total;
   int err = KDLAE_OK;
   auto conv3d = [&](const std::string& name, int cin, int cout) {
-    const std::vector<float>* W = h->ps.get(name + ".weight", &err);
-    const std::vector<float>* Bv = h->ps.get(name + ".bias", &err);
+    const int32_t W = h->ps.base(name + ".weight", &err);
+    const int32_t Bv = h->ps.base(name + ".bias", &err);
     Gemm g;
     if (err) return g;
     const int cis = ru16(cin), cos = ru16(cout);
@@ -161,27 +165,27 @@ int kdlae_s_commit_params(kdlae_s_handle* h, void* stream) {
     g.K = 27 * cis;
     g.n_true = cout;
     g.k_true = 27 * cin;
-    g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> float {
+    g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
       const int tap = k / cis, c = k - tap * cis;
-      if (n >= cout || c >= cin) return 0.f;
-      return (*W)[((size_t)n * cin + c) * 27 + tap];
+      if (n >= cout || c >= cin) return PEx{};
+      return PEx{W + (n * cin + c) * 27 + tap, -1};
     }));
-    std::vector<float> b((size_t)g.ntiles * 16, 0.f);
-    for (int n = 0; n < cout; ++n) b[n] = (*Bv)[n];
+    std::vector<PEx> b((size_t)g.ntiles * 16);
+    for (int n = 0; n < cout; ++n) b[n].a = Bv + n;
     g.bias = ar.add(b);
     choose_variant(g);
     return g;
   };
   // first conv: Cin = 1 direct kernel, weights padded to [cs0][27]
   {
-    const std::vector<float>* W = h->ps.get("encoders.0.0.weight", &err);
-    const std::vector<float>* Bv = h->ps.get("encoders.0.0.bias", &err);
+    const int32_t W = h->ps.base("encoders.0.0.weight", &err);
+    const int32_t Bv = h->ps.base("encoders.0.0.bias", &err);
     if (err) return err;
     const int c0 = h->hc[0], cs0 = h->cs[0];
-    std::vector<float> w((size_t)cs0 * 27, 0.f), b((size_t)cs0, 0.f);
+    std::vector<PEx> w((size_t)cs0 * 27), b((size_t)cs0);
     for (int n = 0; n < c0; ++n) {
-      for (int t = 0; t < 27; ++t) w[(size_t)n * 27 + t] = (*W)[(size_t)n * 27 + t];
-      b[n] = (*Bv)[n];
+      for (int t = 0; t < 27; ++t) w[(size_t)n * 27 + t].a = W + n * 27 + t;
+      b[n].a = Bv + n;
     }
     h->first.w = ar.add(w);
     h->first.bias = ar.add(b);
@@ -202,8 +206,8 @@ int kdlae_s_commit_params(kdlae_s_handle* h, void* stream) {
   h->fusion.b = conv3d("st_fusion.2", h->hc[h->L], h->hc[h->L]);
   for (int j = 0, i = h->L - 1; i >= 0; --i, ++j) {
     const std::string p = "upconv_layers." + std::to_string(j);
-    const std::vector<float>* W = h->ps.get(p + ".weight", &err);  // [cin][cout][1][2][2]
-    const std::vector<float>* Bv = h->ps.get(p + ".bias", &err);
+    const int32_t W = h->ps.base(p + ".weight", &err);  // [cin][cout][1][2][2]
+    const int32_t Bv = h->ps.base(p + ".bias", &err);
     if (err) return err;
     const int cin = (i == h->L - 1) ? h->hc[h->L] : h->hc[i + 1], cout = h->hc[i];
     const int cis = ru16(cin), cos = ru16(cout);
@@ -216,14 +220,14 @@ int kdlae_s_commit_params(kdlae_s_handle* h, void* stream) {
     g.K = cis;
     g.n_true = 4 * cout;
     g.k_true = cin;
-    g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> float {
+    g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
       const int c = n >> 2, ii = (n >> 1) & 1, jj = n & 1;
-      if (c >= cout || k >= cin) return 0.f;
-      return (*W)[(((size_t)k * cout + c) * 2 + ii) * 2 + jj];
+      if (c >= cout || k >= cin) return PEx{};
+      return PEx{W + ((k * cout + c) * 2 + ii) * 2 + jj, -1};
     }));
-    std::vector<float> b((size_t)g.ntiles * 16, 0.f);
+    std::vector<PEx> b((size_t)g.ntiles * 16);
     for (int n = 0; n < 4 * cos; ++n)
-      if ((n >> 2) < cout) b[n] = (*Bv)[n >> 2];
+      if ((n >> 2) < cout) b[n].a = Bv + (n >> 2);
     g.bias = ar.add(b);
     choose_variant(g);
     h->up.push_back(g);
@@ -234,19 +238,46 @@ int kdlae_s_commit_params(kdlae_s_handle* h, void* stream) {
     h->dec.push_back(bl);
   }
   {
-    const std::vector<float>* W = h->ps.get("out_conv.weight", &err);
-    const std::vector<float>* Bv = h->ps.get("out_conv.bias", &err);
+    const int32_t W = h->ps.base("out_conv.weight", &err);
+    const int32_t Bv = h->ps.base("out_conv.bias", &err);
     if (err) return err;
-    std::vector<float> w((size_t)h->cs[0], 0.f);
-    for (int c = 0; c < h->hc[0]; ++c) w[c] = (*W)[c];
+    std::vector<PEx> w((size_t)h->cs[0]);
+    for (int c = 0; c < h->hc[0]; ++c) w[c].a = W + c;
     h->outc.w = ar.add(w);
-    h->outc.bias = ar.add(*Bv);
+    h->outc.bias = ar.copy(Bv, h->cfg.out_channels);
     h->outc.Cin = h->cs[0];
     h->outc.Cout = 1;
   }
   if (err) return err;
-  rc = h->dw.upload(ar, reinterpret_cast<hipStream_t>(stream));
+  DeviceGuard g(h->device);
+  int rc = h->dw.upload_program(ar);
   if (rc) return rc;
+  h->built = true;
+  return KDLAE_OK;
+}
+
+extern "C" {
+
+int kdlae_s_commit_params(kdlae_s_handle* h, void* stream) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  int rc = h->ps.check_complete();
+  if (rc) return rc;
+  if ((rc = build_program_s(h))) return rc;
+  DeviceGuard g(h->device);
+  if ((rc = h->dw.run_host(h->ps.flat(), reinterpret_cast<hipStream_t>(stream)))) return rc;
+  h->committed = true;
+  return KDLAE_OK;
+}
+
+int kdlae_s_pack_device(kdlae_s_handle* h, const float* params, int64_t numel, void* stream) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  if (numel != h->ps.total)
+    return fail(KDLAE_EPARAM, "flat parameter vector has " + std::to_string(numel) + " floats, expected " +
+                                  std::to_string(h->ps.total));
+  int rc = build_program_s(h);
+  if (rc) return rc;
+  DeviceGuard g(h->device);
+  if ((rc = h->dw.run(params, reinterpret_cast<hipStream_t>(stream)))) return rc;
   h->committed = true;
   return KDLAE_OK;
 }
@@ -264,7 +295,7 @@ int64_t kdlae_s_workspace_bytes(const kdlae_s_handle* h, int B, int F, int H, in
 int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int W, float* out, void* workspace,
                     int64_t workspace_bytes, void* stream) {
   if (!h) return fail(KDLAE_ESTATE, "null handle");
-  if (!h->committed) return fail(KDLAE_ESTATE, "forward before kdlae_s_commit_params");
+  if (!h->committed) return fail(KDLAE_ESTATE, "forward before kdlae_s_commit_params / kdlae_s_pack_device");
   const int m = 1 << h->L;
   if (B <= 0 || F <= 0 || H <= 0 || W <= 0 || H % m || W % m)
     return fail(KDLAE_EINVAL_SHAPE, "KDLAE_student needs H and W divisible by 2^(len(hidden_channels)-1) "
@@ -272,7 +303,7 @@ int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int 
   if (!x || !out || !workspace) return fail(KDLAE_ESTATE, "null tensor");
   SPlan pl = make_splan(h, B, F, H, W);
   if ((int64_t)pl.total > workspace_bytes) return fail(KDLAE_ESTATE, "workspace too small");
-  HIPCHK(hipSetDevice(h->device));
+  DeviceGuard dg(h->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   char* ws = reinterpret_cast<char*>(workspace);
   auto buf = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };

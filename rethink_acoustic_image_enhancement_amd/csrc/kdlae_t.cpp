@@ -40,12 +40,10 @@ using namespace kdlae;
 struct kdlae_t_handle {
   kdlae_t_config cfg{};
   int device = 0;
-  std::vector<std::pair<std::string, int64_t>> keys;  // expected state_dict keys (ordered)
-  std::unordered_map<std::string, int> key_index;
-  std::unordered_map<std::string, std::vector<float>> staged;
-  bool committed = false;
-  float* dev = nullptr;  // weight arena
-  size_t dev_floats = 0;
+  ParamStore ps;           // expected state_dict keys (ordered, flat offsets) + host-staged values
+  bool built = false;      // pack program uploaded (depends on the config only)
+  bool committed = false;  // arena filled from parameters at least once
+  DeviceWeights dw;        // packed arena + pack program
   // model
   std::vector<BlockW> enc1, enc2, enc3, latent, dec3, dec2, dec1, refinement, refinement_out, enhance;
   SmallW patch_embed, output, output_param, output2, cen, outputen;
@@ -60,17 +58,14 @@ struct kdlae_t_handle {
   struct ProbeRec { std::string tag; double bytes, flops; };
   std::vector<ProbeRec> probe_recs;
 
-  const float* P(size_t off) const { return off == kNone ? nullptr : dev + off; }
+  const float* P(size_t off) const { return dw.P(off); }
 };
 
 namespace kdlae {
 
 static int hid_of(const kdlae_t_config& c, int dim) { return (int)((double)dim * c.ffn_expansion_factor); }
 
-static void add_key(kdlae_t_handle* h, const std::string& k, int64_t n) {
-  h->key_index[k] = (int)h->keys.size();
-  h->keys.emplace_back(k, n);
-}
+static void add_key(kdlae_t_handle* h, const std::string& k, int64_t n) { h->ps.add(k, n); }
 
 // Expected state_dict (KDLAE_model.py:220-268, TransformerBlock :150-157, Attention :113-120,
 // FeedForward :90-99, LayerNorm :73-79).
@@ -161,32 +156,19 @@ static int validate(const kdlae_t_config& c) {
 }
 
 // ----------------------------------------------------------------------------- packing helpers
+// The packer records the device layout as a pack program (runtime.h): every packed float names the
+// flat-parameter entries it is gathered from.  Values are produced on the device (pack.hip).
 struct Packer {
   kdlae_t_handle* h;
-  Arena arena;
+  PackProgram prog;
   int err = KDLAE_OK;
 
-  const std::vector<float>* get(const std::string& k) {
-    auto it = h->staged.find(k);
-    if (it == h->staged.end()) {
-      if (err == KDLAE_OK) err = fail(KDLAE_EPARAM, "missing state_dict entry: " + k);
-      return nullptr;
-    }
-    return &it->second;
-  }
+  int32_t get(const std::string& k) { return h->ps.base(k, &err); }
 
-  // generic fragment-order pack: Wf(n, k) over [ntiles*16] x [kgroups*16]
+  // generic fragment-order pack: Wf(n, k) -> PEx over [ntiles*16] x [kgroups*16]
   template <class F>
   size_t pack(int ntiles, int kgroups, F Wf) {
-    std::vector<float> v((size_t)ntiles * kgroups * 256, 0.f);
-    for (int t = 0; t < ntiles; ++t)
-      for (int g = 0; g < kgroups; ++g)
-        for (int l = 0; l < 64; ++l)
-          for (int e = 0; e < 4; ++e) {
-            const int n = 16 * t + (l & 15), k = 16 * g + 4 * (l >> 4) + e;
-            v[(((size_t)t * kgroups + g) * 64 + l) * 4 + e] = Wf(n, k);
-          }
-    return arena.add(v);
+    return prog.add(pack_fragments(ntiles, kgroups, Wf));
   }
 
   // 1x1 conv [Cout][Cin] with optional LN(weight, bias) folded on the input side.
@@ -195,11 +177,10 @@ struct Packer {
   Gemm pointwise(const std::string& name, int Cout, int Cin, int Kpad, int nstore, RowMap row_map,
                  const std::string& ln_prefix, bool conv_bias, bool prefer_single_k) {
     Gemm g;
-    const std::vector<float>* W = get(name + ".weight");
-    const std::vector<float>* lnw = ln_prefix.empty() ? nullptr : get(ln_prefix + ".body.weight");
-    const std::vector<float>* lnb = nullptr;
-    if (!ln_prefix.empty() && !h->cfg.layernorm_biasfree) lnb = get(ln_prefix + ".body.bias");
-    const std::vector<float>* cb = conv_bias ? get(name + ".bias") : nullptr;
+    const int32_t W = get(name + ".weight");
+    const int32_t lnw = ln_prefix.empty() ? -1 : get(ln_prefix + ".body.weight");
+    const int32_t lnb = (!ln_prefix.empty() && !h->cfg.layernorm_biasfree) ? get(ln_prefix + ".body.bias") : -1;
+    const int32_t cb = conv_bias ? get(name + ".bias") : -1;
     if (err) return g;
     g.ntiles = (nstore + 15) / 16;
     g.kgroups = Kpad / 16;
@@ -208,24 +189,33 @@ struct Packer {
     g.ksize = 1;
     g.n_true = Cout;
     g.k_true = Cin;
-    g.w = pack(g.ntiles, g.kgroups, [&](int n, int k) -> float {
-      if (n >= nstore || k >= Cin) return 0.f;
+    g.w = pack(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
+      if (n >= nstore || k >= Cin) return PEx{};
       const int src = row_map(n);
-      if (src < 0) return 0.f;
-      const float s = lnw ? (*lnw)[k] : 1.f;
-      return (*W)[(size_t)src * Cin + k] * s;
+      if (src < 0) return PEx{};
+      return PEx{W + src * Cin + k, lnw >= 0 ? lnw + k : -1};
     });
-    if (cb || lnb) {
-      std::vector<float> bv((size_t)g.ntiles * 16, 0.f);
-      for (int n = 0; n < nstore; ++n) {
-        const int src = row_map(n);
-        if (src < 0) continue;
-        double acc = cb ? (*cb)[src] : 0.0;
-        if (lnb)
-          for (int k = 0; k < Cin; ++k) acc += (double)(*W)[(size_t)src * Cin + k] * (*lnb)[k];
-        bv[n] = (float)acc;
-      }
-      g.bias = arena.add(bv);
+    if (cb >= 0 || lnb >= 0) {
+      // bias' = conv bias + W . ln_bias (the WithBias LN shift pushed through the 1x1 conv)
+      std::vector<PEx> bv((size_t)g.ntiles * 16);
+      if (lnb < 0)
+        for (int n = 0; n < nstore; ++n) {
+          const int src = row_map(n);
+          if (src >= 0) bv[n].a = cb + src;
+        }
+      g.bias = prog.add(bv);
+      if (lnb >= 0)
+        for (int n = 0; n < nstore; ++n) {
+          const int src = row_map(n);
+          if (src < 0) continue;
+          PDot d;
+          d.dst = (int64_t)g.bias + n;
+          d.base = cb >= 0 ? cb + src : -1;
+          d.w = W + src * Cin;
+          d.v = lnb;
+          d.K = Cin;
+          prog.dots.push_back(d);
+        }
     }
     choose_variant(g, prefer_single_k);
     return g;
@@ -235,7 +225,7 @@ struct Packer {
   Gemm conv3(const std::string& name, int Cout, int Cin, int out_mode) {
     Gemm g;
     g.out_mode = out_mode;
-    const std::vector<float>* W = get(name + ".weight");
+    const int32_t W = get(name + ".weight");
     if (err) return g;
     g.ksize = 3;
     g.cg_per_tap = Cin / 16;
@@ -245,10 +235,10 @@ struct Packer {
     g.K = 9 * Cin;
     g.n_true = Cout;
     g.k_true = 9 * Cin;
-    g.w = pack(g.ntiles, g.kgroups, [&](int n, int k) -> float {
-      if (n >= Cout) return 0.f;
+    g.w = pack(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
+      if (n >= Cout) return PEx{};
       const int tap = k / Cin, c = k - tap * Cin;
-      return (*W)[((size_t)n * Cin + c) * 9 + tap];
+      return PEx{W + (n * Cin + c) * 9 + tap, -1};
     });
     choose_variant(g, false);
     return g;
@@ -258,11 +248,11 @@ struct Packer {
     SmallW s;
     s.Cout = Cout;
     s.Cin = Cin;
-    const std::vector<float>* W = get(name + ".weight");
-    const std::vector<float>* B = bias ? get(name + ".bias") : nullptr;
+    const int32_t W = get(name + ".weight");
+    const int32_t B = bias ? get(name + ".bias") : -1;
     if (err) return s;
-    s.w = arena.add(*W);
-    if (B) s.bias = arena.add(*B);
+    s.w = prog.copy(W, (size_t)Cout * Cin * 9);
+    if (B >= 0) s.bias = prog.copy(B, Cout);
     return s;
   }
 
@@ -276,28 +266,24 @@ struct Packer {
     b.hidS = ru16(b.hid);
     const int hid = b.hid, hidS = b.hidS;
     b.qkv = pointwise(p + ".attn.qkv", 3 * C, C, C, 3 * C, [](int n) { return n; }, p + ".norm1", c.bias, true);
-    const std::vector<float>* dw = get(p + ".attn.qkv_dwconv.weight");
-    const std::vector<float>* dwb = c.bias ? get(p + ".attn.qkv_dwconv.bias") : nullptr;
-    const std::vector<float>* pw = get(p + ".attn.project_out.weight");
-    const std::vector<float>* pb = c.bias ? get(p + ".attn.project_out.bias") : nullptr;
-    const std::vector<float>* tp = get(p + ".attn.temperature");
-    const std::vector<float>* fw = get(p + ".ffn.dwconv.weight");
-    const std::vector<float>* fb = c.bias ? get(p + ".ffn.dwconv.bias") : nullptr;
+    const int32_t dw = get(p + ".attn.qkv_dwconv.weight");
+    const int32_t dwb = c.bias ? get(p + ".attn.qkv_dwconv.bias") : -1;
+    const int32_t pw = get(p + ".attn.project_out.weight");
+    const int32_t pb = c.bias ? get(p + ".attn.project_out.bias") : -1;
+    const int32_t tp = get(p + ".attn.temperature");
+    const int32_t fw = get(p + ".ffn.dwconv.weight");
+    const int32_t fb = c.bias ? get(p + ".ffn.dwconv.bias") : -1;
     if (err) return b;
     {
-      std::vector<float> v((size_t)9 * 3 * C);
+      std::vector<PEx> v((size_t)9 * 3 * C);
       for (int ch = 0; ch < 3 * C; ++ch)
-        for (int t = 0; t < 9; ++t) v[(size_t)t * 3 * C + ch] = (*dw)[(size_t)ch * 9 + t];
-      b.dwqkv = arena.add(v);
-      if (dwb) b.dwqkv_b = arena.add(*dwb);
+        for (int t = 0; t < 9; ++t) v[(size_t)t * 3 * C + ch].a = dw + ch * 9 + t;
+      b.dwqkv = prog.add(v);
+      if (dwb >= 0) b.dwqkv_b = prog.copy(dwb, (size_t)3 * C);
     }
-    b.proj = arena.add(*pw);
-    if (pb) {
-      std::vector<float> v((size_t)C, 0.f);
-      std::copy(pb->begin(), pb->end(), v.begin());
-      b.proj_b = arena.add(v);
-    }
-    b.temp = arena.add(*tp);
+    b.proj = prog.copy(pw, (size_t)C * C);
+    if (pb >= 0) b.proj_b = prog.copy(pb, C);
+    b.temp = prog.copy(tp, heads);
     b.proj_gemm.ntiles = C / 16;
     b.proj_gemm.kgroups = C / 16;
     b.proj_gemm.N = C;
@@ -324,25 +310,25 @@ struct Packer {
     b.pin = pointwise(p + ".ffn.project_in", 2 * hid, C, C, 2 * hidS, rmap, p + ".norm2", c.bias, true);
     if (fz) {
       // per 32-channel chunk: [9 taps][32] weights, [32] bias at +288, zero pad to 512 (gdfn.hip)
-      std::vector<float> v((size_t)(hidS / 16) * 512, 0.f);
+      std::vector<PEx> v((size_t)(hidS / 16) * 512);
       for (int n = 0; n < 2 * hidS; ++n) {
         const int src = rmap(n);
         if (src < 0) continue;
-        float* blk = v.data() + (size_t)(n >> 5) * 512;
-        for (int t = 0; t < 9; ++t) blk[t * 32 + (n & 31)] = (*fw)[(size_t)src * 9 + t];
-        if (fb) blk[288 + (n & 31)] = (*fb)[src];
+        PEx* blk = v.data() + (size_t)(n >> 5) * 512;
+        for (int t = 0; t < 9; ++t) blk[t * 32 + (n & 31)].a = fw + src * 9 + t;
+        if (fb >= 0) blk[288 + (n & 31)].a = fb + src;
       }
-      b.dwffn = arena.add(v);
+      b.dwffn = prog.add(v);
     } else {
-      std::vector<float> v((size_t)9 * 2 * hidS, 0.f), vb((size_t)2 * hidS, 0.f);
+      std::vector<PEx> v((size_t)9 * 2 * hidS), vb((size_t)2 * hidS);
       for (int n = 0; n < 2 * hidS; ++n) {
         const int src = rmap(n);
         if (src < 0) continue;
-        for (int t = 0; t < 9; ++t) v[(size_t)t * 2 * hidS + n] = (*fw)[(size_t)src * 9 + t];
-        if (fb) vb[n] = (*fb)[src];
+        for (int t = 0; t < 9; ++t) v[(size_t)t * 2 * hidS + n].a = fw + src * 9 + t;
+        if (fb >= 0) vb[n].a = fb + src;
       }
-      b.dwffn = arena.add(v);
-      if (fb) b.dwffn_b = arena.add(vb);
+      b.dwffn = prog.add(v);
+      if (fb >= 0) b.dwffn_b = prog.add(vb);
     }
     b.pout = pointwise(p + ".ffn.project_out", C, hid, hidS, C, [](int n) { return n; }, "", c.bias, false);
     return b;
@@ -367,14 +353,16 @@ struct Plan {
   }
 };
 
-// Partial Gram slots per (image, head).  Row-sweep kernel (W % 16 == 0): strips x row segments,
-// sized for ~2048 workgroups per launch; generic kernel: 64-pixel steps grouped 16 per slot.
-static int nslots_for(int H, int W, int B, int heads) {
+// Partial Gram slots per (image, head).  The slot partition depends on the image size only, never on
+// the batch: image i of a batch then sums its Gram in exactly the order it does alone (bit-identical
+// batch invariance).  Row-sweep kernel (W % 16 == 0): 16-column strips x at most 8 row segments of
+// at least 32 rows (512^2: 64 rows, the 2-row halo costs 3%; 1024^2: 128 rows); generic kernel:
+// 64-pixel steps grouped 16 per slot.
+static int nslots_for(int H, int W, int /*B*/, int /*heads*/) {
   if (W % 16 == 0) {
     const int strips = W / 16;
-    long long nseg = (2048 + (long long)strips * B * heads - 1) / ((long long)strips * B * heads);
-    nseg = std::max<long long>(1, std::min<long long>(nseg, (H + 7) / 8));
-    return (int)(strips * nseg);
+    const int nseg = std::max(1, std::min(8, (H + 31) / 32));
+    return strips * nseg;
   }
   const int steps = (H * W + 63) / 64;
   int n = (steps + 15) / 16;
@@ -726,41 +714,38 @@ int kdlae_t_create(const kdlae_t_config* cfg, int device, kdlae_t_handle** out) 
 
 int kdlae_t_destroy(kdlae_t_handle* h) {
   if (!h) return KDLAE_OK;
-  if (h->dev) (void)hipFree(h->dev);
-  for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+  {
+    DeviceGuard g(h->device);
+    h->dw.release();
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+  }
   delete h;
   return KDLAE_OK;
 }
 
-int kdlae_t_num_params(const kdlae_t_handle* h) { return h ? (int)h->keys.size() : 0; }
+int kdlae_t_num_params(const kdlae_t_handle* h) { return h ? (int)h->ps.keys.size() : 0; }
 
 int kdlae_t_param_info(const kdlae_t_handle* h, int index, const char** name, int64_t* numel) {
-  if (!h || index < 0 || index >= (int)h->keys.size()) return fail(KDLAE_EPARAM, "param index out of range");
-  if (name) *name = h->keys[index].first.c_str();
-  if (numel) *numel = h->keys[index].second;
-  return KDLAE_OK;
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  return h->ps.info(index, name, numel);
 }
+
+int64_t kdlae_t_params_numel(const kdlae_t_handle* h) { return h ? h->ps.total : -1; }
 
 int kdlae_t_set_param(kdlae_t_handle* h, const char* name, const float* host_data, int64_t numel) {
   if (!h || !name || !host_data) return fail(KDLAE_ESTATE, "null argument");
-  auto it = h->key_index.find(name);
-  if (it == h->key_index.end()) return fail(KDLAE_EPARAM, std::string("unexpected key in state_dict: ") + name);
-  if (h->keys[it->second].second != numel)
-    return fail(KDLAE_EPARAM, std::string("size mismatch for ") + name + ": expected " +
-                                  std::to_string(h->keys[it->second].second) + " got " + std::to_string(numel));
-  h->staged[name].assign(host_data, host_data + numel);
-  h->committed = false;
-  return KDLAE_OK;
+  return h->ps.set(name, host_data, numel);
 }
 
-int kdlae_t_commit_params(kdlae_t_handle* h, void* stream) {
-  if (!h) return fail(KDLAE_ESTATE, "null handle");
-  for (auto& kv : h->keys)
-    if (!h->staged.count(kv.first)) return fail(KDLAE_EPARAM, "missing state_dict entry: " + kv.first);
-  HIPCHK(hipSetDevice(h->device));
+}  // extern "C"
+
+// Records the packed layout of this configuration (once per handle) and uploads the program.
+static int build_program(kdlae_t_handle* h) {
+  if (h->built) return KDLAE_OK;
   const kdlae_t_config& c = h->cfg;
   Packer pk{h};
-  h->zeros = pk.arena.add(std::vector<float>(64, 0.f));
+  pk.prog.nsrc = h->ps.total;
+  h->zeros = pk.prog.add(std::vector<PEx>(64));
   const int d = c.dim;
   const int* nb = c.num_blocks;
   const int* hd = c.heads;
@@ -794,17 +779,35 @@ int kdlae_t_commit_params(kdlae_t_handle* h, void* stream) {
     h->outputen = pk.small("outputen", c.out_channels, hc / 2, c.bias);
   }
   if (pk.err) return pk.err;
-  if (h->dev) {
-    HIPCHK(hipFree(h->dev));
-    h->dev = nullptr;
-  }
-  const size_t n = std::max<size_t>(pk.arena.h.size(), 64);
-  pk.arena.h.resize(n, 0.f);
-  HIPCHK(hipMalloc(&h->dev, n * sizeof(float)));
-  h->dev_floats = n;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  HIPCHK(hipMemcpyAsync(h->dev, pk.arena.h.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));
+  DeviceGuard g(h->device);
+  int rc = h->dw.upload_program(pk.prog);
+  if (rc) return rc;
+  h->built = true;
+  return KDLAE_OK;
+}
+
+extern "C" {
+
+int kdlae_t_commit_params(kdlae_t_handle* h, void* stream) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  int rc = h->ps.check_complete();
+  if (rc) return rc;
+  if ((rc = build_program(h))) return rc;
+  DeviceGuard g(h->device);
+  if ((rc = h->dw.run_host(h->ps.flat(), reinterpret_cast<hipStream_t>(stream)))) return rc;
+  h->committed = true;
+  return KDLAE_OK;
+}
+
+int kdlae_t_pack_device(kdlae_t_handle* h, const float* params, int64_t numel, void* stream) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  if (numel != h->ps.total)
+    return fail(KDLAE_EPARAM, "flat parameter vector has " + std::to_string(numel) + " floats, expected " +
+                                  std::to_string(h->ps.total));
+  int rc = build_program(h);
+  if (rc) return rc;
+  DeviceGuard g(h->device);
+  if ((rc = h->dw.run(params, reinterpret_cast<hipStream_t>(stream)))) return rc;
   h->committed = true;
   return KDLAE_OK;
 }
@@ -824,7 +827,7 @@ int64_t kdlae_t_workspace_bytes(const kdlae_t_handle* h, int B, int H, int W) {
 int kdlae_t_forward(kdlae_t_handle* h, const float* img, const float* rate, int B, int H, int W, float* hq,
                     float* sr, void* workspace, int64_t workspace_bytes, void* stream) {
   if (!h) return fail(KDLAE_ESTATE, "null handle");
-  if (!h->committed) return fail(KDLAE_ESTATE, "forward before kdlae_t_commit_params");
+  if (!h->committed) return fail(KDLAE_ESTATE, "forward before kdlae_t_commit_params / kdlae_t_pack_device");
   if (B <= 0 || H <= 0 || W <= 0 || H % 8 || W % 8)
     return fail(KDLAE_EINVAL_SHAPE, "KDLAE_teacher needs H % 8 == 0 and W % 8 == 0 (pixel_unshuffle x3, KDLAE_model.py:187)");
   if (!img || !hq) return fail(KDLAE_ESTATE, "img and hq are required");
@@ -833,7 +836,7 @@ int kdlae_t_forward(kdlae_t_handle* h, const float* img, const float* rate, int 
     return fail(KDLAE_ESTATE, "sr must be non-null iff static=='train'");
   Fwd f{h, reinterpret_cast<hipStream_t>(stream), reinterpret_cast<char*>(workspace), make_plan(h, B, H, W), B};
   if ((int64_t)f.pl.total > workspace_bytes) return fail(KDLAE_ESTATE, "workspace too small");
-  HIPCHK(hipSetDevice(h->device));
+  DeviceGuard g(h->device);
   return f.run(img, rate, H, W, hq, sr);
 }
 

@@ -750,8 +750,7 @@ int kdlae_tt_forward(kdlae_tt_handle* h, const float* theta, const float* img, c
   if (h->cfg.static_train && !sr) return fail(KDLAE_EINVAL_CONFIG, "static='train' needs the sr output");
   const int64_t need = kdlae_tt_workspace_bytes(h, B, H, W);
   if (need < 0 || (size_t)need > ws_bytes) return fail(KDLAE_ESTATE, "training workspace too small");
-  hipError_t e = hipSetDevice(h->device);
-  if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
+  kdlae::DeviceGuard dg(h->device);
   Ctx c;
   ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
   c.th = theta;
@@ -779,6 +778,7 @@ int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, 
     if (rc) return rc;
     if (d.peak > ws_bytes) return fail(KDLAE_ESTATE, "training workspace too small for the backward");
   }
+  kdlae::DeviceGuard dg(h->device);
   Ctx c;
   ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
   c.th = theta;

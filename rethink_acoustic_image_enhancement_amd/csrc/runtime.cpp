@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <mutex>
 #include <tuple>
 
 namespace kdlae {
@@ -122,30 +123,23 @@ int ParamStore::check_complete() const {
   return KDLAE_OK;
 }
 
-const std::vector<float>* ParamStore::get(const std::string& k, int* err) const {
-  auto it = staged.find(k);
-  if (it == staged.end()) {
+
+int32_t ParamStore::base(const std::string& k, int* err) const {
+  auto it = index.find(k);
+  if (it == index.end()) {
     if (err && *err == KDLAE_OK) *err = fail(KDLAE_EPARAM, "missing state_dict entry: " + k);
-    return nullptr;
+    return -1;
   }
-  return &it->second;
+  return (int32_t)offset[it->second];
 }
 
-int DeviceWeights::upload(Arena& a, hipStream_t s) {
-  release();
-  const size_t m = std::max<size_t>(a.h.size(), 64);
-  a.h.resize(m, 0.f);
-  HIPCHK(hipMalloc(&dev, m * sizeof(float)));
-  n = m;
-  HIPCHK(hipMemcpyAsync(dev, a.h.data(), m * sizeof(float), hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));
-  return KDLAE_OK;
-}
-
-void DeviceWeights::release() {
-  if (dev) (void)hipFree(dev);
-  dev = nullptr;
-  n = 0;
+std::vector<float> ParamStore::flat() const {
+  std::vector<float> v((size_t)total, 0.f);
+  for (size_t i = 0; i < keys.size(); ++i) {
+    auto it = staged.find(keys[i].first);
+    if (it != staged.end()) std::copy(it->second.begin(), it->second.end(), v.begin() + offset[i]);
+  }
+  return v;
 }
 
 int run_gemm(const GemmCall& c, hipStream_t s) {
@@ -197,14 +191,17 @@ int run_gemm(const GemmCall& c, hipStream_t s) {
 }
 
 int device_cu_count() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-      return 256;
-    return v;
-  }();
-  return n;
+  static std::mutex mu;
+  static std::map<int, int> per_device;  // a process may drive several GPUs (nn.DataParallel-style)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = per_device.find(dev);
+  if (it != per_device.end()) return it->second;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+  per_device[dev] = v;
+  return v;
 }
 
 // Tiles per block for a GEMM grid of ceil(T / tpb) x gy equal-work blocks.  One 8-wave block fills
@@ -213,11 +210,12 @@ int device_cu_count() {
 // blocks past a round (C192 project_in: 516 blocks = 3 rounds of 12 tiles for 24 tiles of work per
 // CU).  Resident blocks also restage their weight group once (about half a tile-time, from L2).
 int gemm_tiles_per_block(int total_tiles, int gy, bool resident, int wpe) {
-  thread_local std::map<std::tuple<int, int, bool, int>, int> memo;  // a forward repeats ~30 shapes
-  const auto key = std::make_tuple(total_tiles, gy, resident, wpe);
+  thread_local std::map<std::tuple<int, int, bool, int, int>, int> memo;  // a forward repeats ~30 shapes
+  const int cus = device_cu_count();
+  const auto key = std::make_tuple(total_tiles, gy, resident, wpe, cus);
   auto it = memo.find(key);
   if (it != memo.end()) return it->second;
-  const long long slots = (long long)device_cu_count() * (wpe == 4 ? 2 : 1);
+  const long long slots = (long long)cus * (wpe == 4 ? 2 : 1);
   const int target = resident ? 256 * wpe : 1024;  // previous heuristic: the tie-break
   const int gx0 = (int)std::min<long long>(total_tiles, std::max<long long>(1, ceil_div(target, gy)));
   int best = (int)ceil_div(total_tiles, gx0);

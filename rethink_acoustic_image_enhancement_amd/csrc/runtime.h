@@ -43,20 +43,47 @@ struct SmallW {
 
 void choose_variant(Gemm& g, bool prefer_single_k = false);
 
-struct Arena {
-  std::vector<float> h;
-  size_t add(const std::vector<float>& v) {
-    size_t off = (h.size() + 63) / 64 * 64;
-    h.resize(off + v.size());
-    std::copy(v.begin(), v.end(), h.begin() + off);
+// Packed weights are not computed on the host.  Each packed float is recorded as a gather from the
+// flat parameter vector (every state_dict entry in key order, fp32), and the device executes that
+// "pack program" (pack.hip) whenever the caller hands it the live parameters — so the packed copy
+// can never go stale, whatever wrote the parameters (load_state_dict, an optimizer, `.data` edits).
+struct PEx {                  // arena[i] = a < 0 ? 0 : src[a] * (b < 0 ? 1 : src[b])
+  int32_t a = -1, b = -1;
+};
+struct PDot {                 // arena[dst] = (base < 0 ? 0 : src[base]) + sum_k src[w + k] * src[v + k]
+  int64_t dst = 0;
+  int32_t base = -1, w = 0, v = 0, K = 0;
+};
+struct PDer {                 // derived source value src[nsrc + j], computed before the gathers
+  int32_t kind = 0;           // 0: src[a] / sqrt(src[b] + 1e-5)     (BatchNorm scale)
+  int32_t a = -1, b = -1, c = -1, d = -1;  // 1: (src[a] - src[b]) * src[c] + src[d]  (BatchNorm shift)
+};
+struct PackProgram {
+  std::vector<PEx> ex;        // one per arena float
+  std::vector<PDot> dots;
+  std::vector<PDer> der;
+  int64_t nsrc = 0;           // floats in the flat parameter vector
+  size_t add(const std::vector<PEx>& v) {
+    size_t off = (ex.size() + 63) / 64 * 64;
+    ex.resize(off + v.size());
+    std::copy(v.begin(), v.end(), ex.begin() + off);
     return off;
+  }
+  size_t copy(int32_t base, size_t n) {  // plain copy of n source floats
+    std::vector<PEx> v(n);
+    for (size_t i = 0; i < n; ++i) v[i].a = base + (int32_t)i;
+    return add(v);
+  }
+  int32_t derive(const PDer& d) {
+    der.push_back(d);
+    return (int32_t)(nsrc + (int64_t)der.size() - 1);
   }
 };
 
 // fragment-order pack: Wf(n, k) over [ntiles*16] x [kgroups*16]
 template <class F>
-std::vector<float> pack_fragments(int ntiles, int kgroups, F Wf) {
-  std::vector<float> v((size_t)ntiles * kgroups * 256, 0.f);
+std::vector<PEx> pack_fragments(int ntiles, int kgroups, F Wf) {
+  std::vector<PEx> v((size_t)ntiles * kgroups * 256);
   for (int t = 0; t < ntiles; ++t)
     for (int g = 0; g < kgroups; ++g)
       for (int l = 0; l < 64; ++l)
@@ -67,28 +94,56 @@ std::vector<float> pack_fragments(int ntiles, int kgroups, F Wf) {
   return v;
 }
 
-// expected state_dict keys + host copies staged through *_set_param (strict, like load_state_dict)
+// expected state_dict keys (flat offsets in key order) + host copies staged through *_set_param
 struct ParamStore {
   std::vector<std::pair<std::string, int64_t>> keys;
+  std::vector<int64_t> offset;
+  int64_t total = 0;
   std::unordered_map<std::string, int> index;
   std::unordered_map<std::string, std::vector<float>> staged;
   void add(const std::string& k, int64_t n) {
     index[k] = (int)keys.size();
     keys.emplace_back(k, n);
+    offset.push_back(total);
+    total += n;
   }
   int set(const char* name, const float* data, int64_t numel);
   int info(int i, const char** name, int64_t* numel) const;
   int check_complete() const;
-  const std::vector<float>* get(const std::string& k, int* err) const;
+  int32_t base(const std::string& k, int* err) const;  // flat offset of a key (-1 + err if unknown)
+  std::vector<float> flat() const;                       // staged entries in key order
 };
 
-// device weight arena owned by a handle
+// Device side of a handle's weights: the packed arena plus the pack program that fills it.
 struct DeviceWeights {
-  float* dev = nullptr;
+  float* dev = nullptr;       // packed arena
   size_t n = 0;
-  int upload(Arena& a, hipStream_t s);
+  PEx* ex = nullptr;
+  PDot* dots = nullptr;
+  PDer* der = nullptr;
+  float* ext = nullptr;       // derived values
+  float* src = nullptr;       // flat parameters staged from the host (set_param/commit path)
+  int64_t nsrc = 0;
+  int n_dots = 0, n_der = 0;
+  int device = -1;
+  int upload_program(const PackProgram& p);                 // allocates; synchronous, once per layout
+  int run(const float* params, hipStream_t s) const;        // enqueues the pack on `s`
+  int run_host(const std::vector<float>& params, hipStream_t s);  // host copy of the flat vector
   void release();
   const float* P(size_t off) const { return off == kNone ? nullptr : dev + off; }
+};
+
+// Restores the caller's current device when it goes out of scope.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
 };
 
 struct View {
@@ -113,7 +168,7 @@ struct GemmCall {
 };
 int run_gemm(const GemmCall& c, hipStream_t s);
 // Compute units of the current device (256 on MI355X) and the tail-aware GEMM grid split.
-int device_cu_count();
+int device_cu_count();  // of the current device
 int gemm_tiles_per_block(int total_tiles, int gy, bool resident, int wpe);
 
 }  // namespace kdlae

@@ -249,10 +249,136 @@ def train_goldens(KM, out):
         print(name, losses, norms, grad1.shape, f"{time.time() - t0:.1f}s")
 
 
+# ---------------------------------------------------------------- checkpoint layout
+CKPT_CASES = {
+    # name: (which model, ctor kwargs, input shape)
+    "ckpt_t_tiny": ("teacher", dict(dim=16, num_blocks=[1, 2, 1, 1], num_refinement_blocks=1, heads=[1, 2, 4, 8],
+                                    LayerNorm_type="BiasFree", bias=False, static="train", params="cat"), (1, 3, 32, 48)),
+    "ckpt_s_default": ("student", dict(inp_channels=1, out_channels=1, residual=True, hidden_channels=[16, 32, 64]),
+                       (1, 4, 32, 32)),
+    "ckpt_a_default": ("asdqe", dict(in_channels=3, dim=16), (2, 3, 48, 48)),
+}
+
+
+def _two_level(sd):
+    """Every float tensor snapped to its own {min, max}: the checkpoint keeps the reference's
+    layout (keys, shapes, dtypes, BN buffers) but compresses to ~1 bit per value under xz."""
+    out = {}
+    for k, v in sd.items():
+        if v.is_floating_point() and v.numel() > 1 and float(v.max()) > float(v.min()):
+            lo, hi = v.min(), v.max()
+            v = torch.where(v > (lo + hi) / 2, hi, lo).to(v.dtype)
+        out[k] = v.clone()
+    return out
+
+
+def ckpt_goldens(KM, AM, out):
+    """Checkpoints WRITTEN BY THE REFERENCE MODULES in the reference's on-disk layouts, plus the
+    reference's outputs for them:
+    * KDLAE-T / KDLAE-S: BasicSR save_network (Train/basicsr/models/base_model.py:213-244):
+      torch.save({'params': sd, 'params_ema': sd_ema}) of net.state_dict() moved to CPU;
+      consumers load ['params'] strictly (KDLAE_T.ipynb:1074-1075, KDLAE-S.ipynb:109-110).
+    * ASDQE: torch.save(model.state_dict()) (Train/ASDQE.py:210,215,219), raw, BN buffers
+      included; consumer load_state_dict(..., strict=False) (ASDQE/ASDQE_test.py:75-84).
+    Files are committed xz-compressed (tests decompress them to a temp dir)."""
+    import io
+    import lzma
+
+    for name, (kind, kw, shape) in CKPT_CASES.items():
+        ctor = {"teacher": KM.KDLAE_teacher, "student": KM.KDLAE_student, "asdqe": AM.DenoiseRatePredictor}[kind]
+        m = _load_hash(ctor(**kw))
+        sd = _two_level(m.state_dict())
+        m.load_state_dict(sd, strict=True)
+        ema = {k: (v * 0.75 if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+        outs = {}
+        for tag, weights in (("params", sd), ("params_ema", ema)):
+            if kind == "asdqe" and tag == "params_ema":
+                continue
+            m.load_state_dict(weights, strict=True)
+            m.eval()
+            with torch.no_grad():
+                if kind == "teacher":
+                    b, c, h, w = shape
+                    img = hash_images(f"img:{name}", shape)
+                    rate = np.full((b, 1, h, w), 0.6, np.float32)
+                    o = m({"img": torch.from_numpy(img), "denoise_rate": torch.from_numpy(rate)})
+                    outs.update({f"{tag}_hq": o["hq"].numpy(), f"{tag}_sr": o["sr"].numpy(), "img": img, "rate": rate})
+                elif kind == "student":
+                    x = hash_images(f"frames:{name}", shape)
+                    outs.update({f"{tag}_y": m(torch.from_numpy(x)).numpy(), "x": x})
+                else:
+                    gt = hash_images(f"gt:{name}", shape)
+                    lq = np.clip(gt + 0.1 * hash_normal(f"noise:{name}", shape), 0, 1).astype(np.float32)
+                    cap = {}
+                    hk = m.unet.register_forward_hook(lambda mod, i, o: cap.__setitem__("feat", o.detach().clone()))
+                    score = m(torch.from_numpy(lq), torch.from_numpy(gt)).numpy()
+                    hk.remove()
+                    outs.update({"score": score, "feat_sub": cap["feat"][:, :, ::4, ::4].numpy(), "lq": lq, "gt": gt})
+        buf = io.BytesIO()
+        if kind == "asdqe":
+            torch.save(m.state_dict(), buf)        # raw state_dict, as Train/ASDQE.py writes it
+        else:
+            save = {}
+            for tag, net_sd in (("params", sd), ("params_ema", ema)):
+                net = ctor(**kw)                      # net_g and net_g_ema are separate modules
+                net.load_state_dict(net_sd, strict=True)
+                state_dict = net.state_dict()         # base_model.py:237-242
+                for key, param in state_dict.items():
+                    if key.startswith("module."):
+                        key = key[7:]
+                    state_dict[key] = param.cpu()
+                save[tag] = state_dict
+            torch.save(save, buf)                   # base_model.py:244
+        raw = buf.getvalue()
+        with open(os.path.join(out, f"{name}.pth.xz"), "wb") as f:
+            f.write(lzma.compress(raw, preset=9 | lzma.PRESET_EXTREME))
+        np.savez_compressed(os.path.join(out, f"{name}.npz"), **outs,
+                            cfg=np.frombuffer(json.dumps(dict(kind=kind, kw=kw)).encode(), dtype=np.uint8))
+        print(name, f"pth {len(raw) / 1e6:.2f} MB -> xz {os.path.getsize(os.path.join(out, name + '.pth.xz')) / 1e3:.0f} KB",
+              {k: v.shape for k, v in outs.items()})
+
+
+def _restormer_arch():
+    import importlib.util
+    path = os.path.join(REF, "Train/basicsr/models/archs/restormer_arch.py")
+    spec = importlib.util.spec_from_file_location("ref_restormer_arch", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def key_lists(KM, AM, out):
+    """state_dict key -> [shape, dtype] lists of the reference modules at the released configs
+    (KDLAE_T.ipynb:1059-1071 / KDLAET.yml:65-78; KDLAE-S.ipynb:106 / KDLAES.yml:64-69; ASDQE
+    defaults), the BasicSR alias RestormerSuperResolutionParam2 and the plain Restormer whose
+    pretrained weights KDLAET.yml:82-83 loads with strict_load_g: false."""
+    RA = _restormer_arch()
+    t_kw = dict(inp_channels=3, out_channels=3, dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4,
+                heads=[1, 2, 4, 8], ffn_expansion_factor=2.66, bias=False, LayerNorm_type="BiasFree",
+                dual_pixel_task=False, static="train", params="cat")
+    mods = {
+        "KDLAE_teacher_released": (KM.KDLAE_teacher, t_kw),
+        "KDLAE_teacher_static_no": (KM.KDLAE_teacher, dict(t_kw, static="no")),
+        "KDLAE_teacher_ctor_defaults": (KM.KDLAE_teacher, {}),
+        "RestormerSuperResolutionParam2_KDLAET_yml": (RA.RestormerSuperResolutionParam2, t_kw),
+        "Restormer_BiasFree": (RA.Restormer, dict(LayerNorm_type="BiasFree")),
+        "KDLAE_student_released": (KM.KDLAE_student, dict(inp_channels=1, out_channels=1, residual=True,
+                                                          hidden_channels=[16, 32, 64])),
+        "DenoiseRatePredictor_default": (AM.DenoiseRatePredictor, {}),
+    }
+    res = {}
+    for name, (ctor, kw) in mods.items():
+        sd = ctor(**kw).state_dict()
+        res[name] = {"kwargs": kw, "keys": [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()]}
+        print(name, len(sd), "keys")
+    with open(os.path.join(out, "ref_state_dict_keys.json"), "w") as f:
+        json.dump(res, f, separators=(",", ":"))
+
+
 def main():
     KM, AM = _import_ref()
     out = HERE
-    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512", "train"]
+    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512", "train", "ckpt", "keys"]
     if "train" in which:
         train_goldens(KM, out)
     if "teacher" in which:
@@ -263,6 +389,10 @@ def main():
         asdqe_goldens(AM, out)
     if "t512" in which:
         teacher_512(KM, out)
+    if "ckpt" in which:
+        ckpt_goldens(KM, AM, out)
+    if "keys" in which:
+        key_lists(KM, AM, out)
 
 
 if __name__ == "__main__":

@@ -50,6 +50,10 @@ def test_param_enumeration_matches_module_state_dict(kw):
         name, numel = ctypes.c_char_p(), ctypes.c_int64()
         assert L.kdlae_t_param_info(h, i, ctypes.byref(name), ctypes.byref(numel)) == 0
         assert name.value.decode() == k and numel.value == v.numel()
+    # flat parameter vector of kdlae_t_pack_device: every key back to back in this order
+    assert L.kdlae_t_params_numel(h) == sum(v.numel() for v in sd.values())
+    assert L.kdlae_t_pack_device(h, None, L.kdlae_t_params_numel(h) - 1, None) == 4
+    assert "expected" in _lib.last_error()
     L.kdlae_t_destroy(h)
 
 

@@ -71,7 +71,7 @@ def test_score_only_path_batch_invariance_and_determinism():
         s2 = m(lq.to(DEV), gt.to(DEV)).cpu()
         s1 = m(lq[2:3].to(DEV), gt[2:3].to(DEV)).cpu()
     assert torch.equal(s, s2)
-    assert max_abs(s[2:3], s1) <= 1e-6
+    assert torch.equal(s[2:3], s1)  # GAP slots depend on the image size only (asdqe.cpp gap_slots)
     s_f, _ = _run(m, lq, gt)
     assert torch.equal(s, s_f)
 

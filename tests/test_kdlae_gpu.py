@@ -160,3 +160,55 @@ def test_error_behaviour():
     with pytest.raises(NotImplementedError):
         KDLAE_teacher(dim=16, dual_pixel_task=True).to(DEV)(
             {"img": torch.zeros(1, 3, 16, 16, device=DEV), "denoise_rate": torch.zeros(1, 1, 16, 16, device=DEV)})
+
+
+def test_data_writes_bypassing_autograd_are_seen():
+    """`.data` writes do not bump `_version`; BasicSR's model_ema (base_model.py:54-62)
+    updates net_g_ema that way.  The HIP path repacks from the live parameters on every forward."""
+    kw = dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1)
+    m = _model(kw)
+    img = torch.from_numpy(hash_images("dw", (1, 3, 16, 24)))
+    rate = torch.full((1, 1, 16, 24), 0.4)
+    a = _run(m, img, rate)
+    src = _model(kw)
+    with torch.no_grad():
+        for p in src.parameters():
+            p.data.mul_(0.9)
+        # model_ema(decay=0.5): net_g_ema.params.data.mul_(decay).add_(net_g.params.data, alpha=1 - decay)
+        for pe, ps in zip(m.parameters(), src.parameters()):
+            pe.data.mul_(0.5).add_(ps.data, alpha=0.5)
+        m.output2.weight.data[0, 0, 1, 1] += 0.25
+    b = _run(m, img, rate)
+    assert not torch.equal(a["hq"], b["hq"])
+    ref = teacher_forward({k: v.cpu() for k, v in m.state_dict().items()}, img, rate, TeacherCfg(**kw))
+    assert max_abs(b["hq"], ref["hq"]) <= TOL and max_abs(b["sr"], ref["sr"]) <= TOL
+
+
+def test_pack_device_rejects_wrong_size_and_host_commit_still_works():
+    import ctypes
+
+    from rethink_acoustic_image_enhancement_amd import _lib
+    kw = dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1)
+    m = _model(kw)
+    eng = m.engine(torch.device(DEV))
+    L = _lib.lib()
+    buf = torch.zeros(eng.numel + 1, device=DEV)
+    assert L.kdlae_t_pack_device(eng.handle, ctypes.c_void_p(buf.data_ptr()), eng.numel + 1, None) == 4
+    assert "expected" in _lib.last_error()
+    # the host-staged path (set_param + commit) packs the same arena as the device path
+    img = torch.from_numpy(hash_images("hc", (1, 3, 16, 16)))
+    rate = torch.full((1, 1, 16, 16), 0.5)
+    want = _run(m, img, rate)["hq"]
+    for name, t in m.state_dict().items():
+        host = t.detach().cpu().contiguous()
+        _lib.check(L.kdlae_t_set_param(eng.handle, name.encode(), ctypes.c_void_p(host.data_ptr()), host.numel()), name)
+    _lib.check(L.kdlae_t_commit_params(eng.handle, None), "commit")
+    out = torch.empty(1, 3, 16, 16, device=DEV)
+    sr = torch.empty(1, 3, 32, 32, device=DEV)
+    ws = eng.workspace(L.kdlae_t_workspace_bytes(eng.handle, 1, 16, 16), torch.device(DEV))
+    ic, rc = img.to(DEV).contiguous(), rate.to(DEV).contiguous()
+    _lib.check(L.kdlae_t_forward(eng.handle, ctypes.c_void_p(ic.data_ptr()), ctypes.c_void_p(rc.data_ptr()), 1, 16, 16,
+                                 ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(sr.data_ptr()),
+                                 ctypes.c_void_p(ws.data_ptr()), ws.numel(), None), "forward")
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), want)
