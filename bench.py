@@ -45,6 +45,34 @@ PROBE_CLASSES = {1: "conv_gemm (MFMA f32 1x1 / implicit-GEMM 3x3)", 2: "dwconv_g
                  3: "dwconv_gate (GDFN)"}
 
 
+def host_cores():
+    """Host cores the CPU baseline may use: os.cpu_count() (BASELINE.md's plan), bounded by this
+    process's CPU affinity and its cgroup CPU quota — on a shared GPU box os.cpu_count() reports the
+    whole machine while the job is given a share of it.  Returns (threads, description)."""
+    total = os.cpu_count() or 1
+    n, why = total, [f"os.cpu_count()={total}"]
+    try:
+        aff = len(os.sched_getaffinity(0))
+        why.append(f"affinity={aff}")
+        n = min(n, aff)
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+            why.append(f"cgroup quota={quota}")
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        why.append(f"OMP_NUM_THREADS={env}")
+        n = min(n, int(env))
+    return max(1, n), ", ".join(why)
+
+
 def make_inputs(first: int, n: int, H: int, W: int):
     imgs = np.stack([hash_images(f"img16:{first + i}", (3, H, W)) for i in range(n)])
     rates = (hash_uniform("rate16", first + n)[first:] + 1.0) * 0.5
@@ -151,7 +179,7 @@ def bench_secondary(args, world, rank, dev, distributed):
                                                                    if gather else ", no data-path collective)")},
            "roofline": roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        threads, tdesc = host_cores() if not args.cpu_threads else (args.cpu_threads, "--cpu-threads")
         torch.set_num_threads(threads)
         sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
         # bounded sample: whole samples of the workload until >= 10 s of CPU work (at most B)
@@ -170,6 +198,7 @@ def bench_secondary(args, world, rank, dev, distributed):
             n += 1
         got = out[:n].cpu()
         res["cpu_baseline"] = {"value": round(n / dt, 5), "unit": res["unit"], "cores": threads, "kind": "port",
+                               "cores_from": tdesc,
                                "sample": f"first {n} samples of the workload batch, torch-CPU oracle, {threads} "
                                          f"threads, {dt:.1f} s"}
         res["parity"] = {"vs": f"CPU oracle, samples 0..{n - 1}", "max_abs": float((got - ref).abs().max())}
@@ -249,7 +278,7 @@ def bench_train(args, world, rank, dev, distributed):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.kdlae_oracle import TeacherCfg
         from oracle.train_oracle import TrainStep
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        threads, tdesc = host_cores() if not args.cpu_threads else (args.cpu_threads, "--cpu-threads")
         torch.set_num_threads(threads)
         sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
         st = TrainStep(sd, TeacherCfg(**KW))
@@ -258,6 +287,7 @@ def bench_train(args, world, rank, dev, distributed):
                 {"hq": gt["hq"][:1].cpu(), "sr": gt["sr"][:1].cpu()})
         dt = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": round(1.0 / dt, 5), "unit": "images/s", "cores": threads, "kind": "port",
+                               "cores_from": tdesc,
                                "sample": f"1 image of the batch, one optimize_parameters step of the torch-CPU "
                                          f"training oracle, {threads} threads, {dt:.1f} s"}
         # parity of the trained weights' loss and gradients on image 0 (the oracle step above ran on the
@@ -294,7 +324,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the RCCL all-gather of outputs (default: gathered inside each step, §8e)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = the host cores this process may use, see host_cores)")
+    ap.add_argument("--no-bs1", action="store_true", help="t16: skip the single-image latency line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -379,6 +411,29 @@ def main():
                          "algorithmic_bytes_per_launch": by.value / n.value,
                          "algorithmic_flops_per_launch": fl.value / n.value})
 
+    bs1 = None
+    if not args.no_bs1 and B > 1:
+        # the metric names 1x512x512: single-image latency on the same module and GPU, each forward
+        # synchronised (HIP events on the forward's stream), after the throughput measurement
+        one = {"img": batch["img"][:1], "denoise_rate": batch["denoise_rate"][:1]}
+        with torch.no_grad():
+            for _ in range(3):
+                model(one)
+            torch.cuda.synchronize(dev)
+            times = []
+            for _ in range(10):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                model(one)
+                e1.record()
+                torch.cuda.synchronize(dev)
+                times.append(e0.elapsed_time(e1))
+        times.sort()
+        med = times[len(times) // 2]
+        bs1 = {"workload": f"KDLAE-T forward bs=1 1x3x{H}x{W} fp32 (same config), per GPU",
+               "latency_ms_median": round(med, 3), "latency_ms_min": round(times[0], 3),
+               "images_per_s": round(1e3 / med, 3), "runs": len(times)}
+
     imgs_total = world * B * args.steps
     res = {
         "metric": METRIC, "value": round(imgs_total / elapsed, 3), "unit": "images/s", "n_gpus": world,
@@ -391,6 +446,8 @@ def main():
                                                                 if gather else ", no data-path collective)")},
         "roofline": roof,
     }
+    if bs1 is not None:
+        res["bs1"] = bs1
     # algorithmic per-image figures of SURVEY.md §8d (KDLAE-T 512^2 static=train)
     if H == 512 and W == 512:
         ips = imgs_total / elapsed / world
@@ -430,7 +487,7 @@ def cpu_baseline(model, batch, out, threads):
     """Oracle (torch CPU restatement, test infrastructure) on image 0 of the workload."""
     from oracle.kdlae_oracle import TeacherCfg, psnr, teacher_forward
 
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads, tdesc = host_cores() if not threads else (threads, "--cpu-threads")
     torch.set_num_threads(threads)
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     img = batch["img"][:1].cpu()
@@ -444,8 +501,10 @@ def cpu_baseline(model, batch, out, threads):
               "sr_max_abs": float((sr - ref["sr"]).abs().max()),
               "hq_psnr_db": round(psnr(hq, ref["hq"]), 2), "sr_psnr_db": round(psnr(sr, ref["sr"]), 2)}
     base = {"value": round(1.0 / dt, 5), "unit": "images/s", "cores": threads, "kind": "port",
+            "cores_from": tdesc,
             "sample": f"1 image 1x3x{img.shape[-2]}x{img.shape[-1]} (image 0 of the bench batch), "
-                      f"torch-CPU oracle, {threads} threads, {dt:.1f} s"}
+                      f"torch-CPU oracle, {threads} threads, {dt:.1f} s (one timed run, no warm-up: "
+                      "the sample is bounded to ~30 s of CPU work)"}
     return base, parity
 
 

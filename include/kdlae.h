@@ -190,7 +190,16 @@ void kdlae_padded_size(int h, int w, int multiple, int* H, int* W);
 int kdlae_preprocess_u8(const uint8_t* images, int B, int h, int w, int channels, int bgr, int multiple,
                         const float* rate, float* img, float* rate_map, void* stream);
 
-/* out f32 [B, C, Hs, Ws] (model output, C <= 4) -> dst u8 [B, h*scale, w*scale, C]:
+/* KDLAE/KDLAE-S.ipynb load_consecutive_stack + padding cell: frames u8 [B, F, h, w, channels]
+ * (channels 1 = gray, 3 / 4 = BGR / BGRA as cv2.imread returns them) -> x f32 [B, F, H, W] =
+ * cv2 COLOR_BGR2GRAY (8-bit fixed point) / 255, reflect-padded on the bottom/right to
+ * kdlae_padded_size(h, w, multiple) (the notebook uses multiple 32).  Frames of one call share h, w
+ * (the notebook cv2.resizes odd-sized frames first; that resize stays on the host). */
+int kdlae_frames_preprocess_u8(const uint8_t* frames, int B, int F, int h, int w, int channels, int multiple,
+                               float* x, void* stream);
+
+/* out f32 [B, C, Hs, Ws] (model output, C <= 64: image channels, or the F frames of KDLAE-S) ->
+ * dst u8 [B, h*scale, w*scale, C]:
  * clamp(0, 1), crop, rint(x * 255) (skimage img_as_ubyte), and 0 where the input pixel
  * lq u8 [B, h, w, lq_channels] (nullable) is black in every colour channel; scale 2 maps each
  * output pixel to its nearest input pixel (the notebook's np.repeat x2 mask for sr). */

@@ -5,6 +5,12 @@ Restates, on numpy/torch CPU tensors, the inference cell of KDLAE/KDLAE_T.ipynb 
 ``alpha = ones * denoise_rate``; ``clamp`` / crop / ``img_as_ubyte`` / the black-pixel mask and its
 ``np.repeat`` x2 for sr) and ASDQE_test.py's ToTensor + ``calculate_statistics`` (:107-120).
 
+KDLAE/KDLAE-S.ipynb's ``load_consecutive_stack`` (cv2.imread -> COLOR_BGR2GRAY -> /255 -> stack) and its
+padding / output cell (pad to a multiple of 32; clamp, crop, permute to [h, w, F], img_as_ubyte) are
+restated too.  cv2 is not importable here either: ``bgr2gray_u8`` restates OpenCV's published 8-bit
+fixed-point rule (yuv_shift 14, B2Y 1868 / G2Y 9617 / R2Y 4899), so it is "parity unpinned" by the
+reference as well — except on gray-as-RGB frames (the MDD samples), where it is the identity.
+
 ``img_as_ubyte`` is scikit-image (not importable in this image; the reference pins no version):
 restated from its published float->uint8 conversion, ``rint(x * 255)`` in float32 then clip.
 That rounding rule is therefore "parity unpinned" by the reference; everything else follows the
@@ -68,3 +74,26 @@ def calculate_statistics(values) -> dict:
     v = np.asarray(values)
     return {"mean": np.mean(v), "std": np.std(v), "min": np.min(v), "25%": np.percentile(v, 25),
             "50%": np.percentile(v, 50), "75%": np.percentile(v, 75), "max": np.max(v)}
+
+
+def bgr2gray_u8(img_u8: np.ndarray) -> np.ndarray:
+    """cv2.cvtColor(img, COLOR_BGR2GRAY) for 8-bit BGR / BGRA (alpha ignored)."""
+    b, g, r = (img_u8[..., i].astype(np.uint32) for i in range(3))
+    return ((1868 * b + 9617 * g + 4899 * r + 8192) >> 14).astype(np.uint8)
+
+
+def load_consecutive_stack(frames_u8) -> torch.Tensor:
+    """KDLAE-S.ipynb load_consecutive_stack for already-read equally sized frames (cv2.imread
+    IMREAD_UNCHANGED arrays, in sequence order): gray, /255, stacked -> [1, F, h, w]."""
+    out = []
+    for img in frames_u8:
+        if img.ndim == 3:
+            img = bgr2gray_u8(img) if img.shape[2] >= 3 else img[:, :, 0]
+        out.append(img.astype(np.float32) / 255.0)
+    return torch.from_numpy(np.stack(out, axis=0)).unsqueeze(0)
+
+
+def student_postprocess(restored: torch.Tensor, h: int, w: int) -> np.ndarray:
+    """KDLAE-S.ipynb output cell: clamp, crop, permute(0, 2, 3, 1), img_as_ubyte(restored[0]) -> [h, w, F]."""
+    r = torch.clamp(restored, 0, 1)[:, :, :h, :w]
+    return img_as_ubyte(r.permute(0, 2, 3, 1).numpy()[0])

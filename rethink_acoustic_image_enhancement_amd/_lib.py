@@ -30,7 +30,7 @@ EXPORTS = (
     "kdlae_s_workspace_bytes", "kdlae_s_forward",
     "asdqe_create", "asdqe_destroy", "asdqe_num_params", "asdqe_param_info", "asdqe_set_param",
     "asdqe_commit_params", "asdqe_params_numel", "asdqe_pack_device", "asdqe_workspace_bytes", "asdqe_forward",
-    "kdlae_padded_size", "kdlae_preprocess_u8", "kdlae_postprocess_u8",
+    "kdlae_padded_size", "kdlae_preprocess_u8", "kdlae_frames_preprocess_u8", "kdlae_postprocess_u8",
     "kdlae_tt_create", "kdlae_tt_destroy", "kdlae_tt_num_params", "kdlae_tt_param_info", "kdlae_tt_num_floats",
     "kdlae_tt_workspace_bytes", "kdlae_tt_forward", "kdlae_tt_backward",
     "kdlae_train_l1sr_scratch_floats", "kdlae_train_l1sr", "kdlae_train_adamw_scratch_floats",
@@ -120,6 +120,8 @@ def lib() -> ctypes.CDLL:
     L.kdlae_padded_size.restype = None
     L.kdlae_preprocess_u8.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                       c_void_p, c_void_p]
+    L.kdlae_frames_preprocess_u8.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                             c_void_p]
     L.kdlae_postprocess_u8.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_void_p]
     L.kdlae_tt_create.argtypes = [ctypes.POINTER(TConfig), c_int, ctypes.POINTER(c_void_p)]

@@ -120,6 +120,7 @@ hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s);
 // Pre/post-processing around the forward (pipeline.hip)
 struct PreParams {
   const uint8_t* in; int B, h, w, cin, cout, bgr;  // u8 [B][h][w][cin]
+  int gray;                                          // 1: cv2 COLOR_BGR2GRAY of a BGR(A) pixel, cout = 1
   int H, W;                                          // padded size (reflect, bottom/right)
   float* img;                                        // f32 [B][cout][H][W]
   const float* rate; float* rate_map;                // per-image rate [B] -> [B][1][H][W] (optional)

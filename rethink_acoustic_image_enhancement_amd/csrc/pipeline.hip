@@ -3,6 +3,9 @@
 // preprocess (KDLAE/KDLAE_T.ipynb, load_image_as_tensor + the padding cell; ASDQE ToTensor):
 //   u8 HWC (1, 3 or 4 channels; cv2 BGR optional) -> f32 NCHW / 255, alpha dropped, reflect-padded on
 //   the bottom/right to (H, W), plus the constant denoise_rate map [B,1,H,W].
+// frames (KDLAE/KDLAE-S.ipynb load_consecutive_stack + its padding cell): F frames of u8 HWC (gray,
+//   or BGR/BGRA as cv2.imread returns them) -> cv2 COLOR_BGR2GRAY -> f32 [B,F,H,W] / 255, reflect-
+//   padded to a multiple of 32; the output cell is the same postprocess with C = F frames.
 // postprocess (the clamp / crop / img_as_ubyte / zero-mask cell):
 //   clamp(x, 0, 1) -> crop to (h*s, w*s) -> rint(x * 255) as u8 HWC; pixels whose input pixel
 //   (nearest, for the x2 SR output) is black in every channel are set to 0.
@@ -19,6 +22,12 @@ namespace {
 // torch.nn.functional.pad(mode='reflect') index map for a pad that is shorter than the input
 __device__ __forceinline__ int reflect_idx(int i, int n) { return i < n ? i : 2 * (n - 1) - i; }
 
+// cv2.cvtColor(COLOR_BGR2GRAY) on 8-bit data: fixed point, Y = (1868 B + 9617 G + 4899 R + 2^13) >> 14
+// (OpenCV's yuv_shift = 14 and its B2Y / G2Y / R2Y coefficients; alpha ignored)
+__device__ __forceinline__ uint8_t bgr2gray_u8(const uint8_t* px) {
+  return (uint8_t)((1868u * px[0] + 9617u * px[1] + 4899u * px[2] + 8192u) >> 14);
+}
+
 __global__ __launch_bounds__(256) void preprocess_u8_kernel(PreParams p) {
   const long long total = (long long)p.B * p.H * p.W;
   const long long HW = (long long)p.H * p.W;
@@ -28,6 +37,10 @@ __global__ __launch_bounds__(256) void preprocess_u8_kernel(PreParams p) {
     const int y = rem / p.W, x = rem - (rem / p.W) * p.W;
     const int sy = reflect_idx(y, p.h), sx = reflect_idx(x, p.w);
     const uint8_t* px = p.in + (((long long)b * p.h + sy) * p.w + sx) * p.cin;
+    if (p.gray) {
+      p.img[(long long)b * HW + rem] = (float)(p.cin >= 3 ? bgr2gray_u8(px) : px[0]) / 255.0f;
+      continue;
+    }
     for (int c = 0; c < p.cout; ++c) {
       const int sc = (p.bgr && p.cin >= 3 && c < 3) ? 2 - c : c;
       p.img[((long long)b * p.cout + c) * HW + rem] = (float)px[sc] / 255.0f;
@@ -69,14 +82,14 @@ long long grid_for(long long total) {
 
 hipError_t launch_preprocess_u8(const PreParams& p, hipStream_t s) {
   if (p.h > p.H || p.w > p.W || p.H - p.h >= p.h || p.W - p.w >= p.w || p.cout < 1 || p.cout > p.cin ||
-      p.cin > 4)
+      p.cin > 4 || (p.gray && p.cout != 1))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(preprocess_u8_kernel, dim3((unsigned)grid_for((long long)p.B * p.H * p.W)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
 hipError_t launch_postprocess_u8(const PostParams& p, hipStream_t s) {
-  if (p.h * p.scale > p.Hs || p.w * p.scale > p.Ws || p.C < 1 || p.C > 4 || (p.scale != 1 && p.scale != 2))
+  if (p.h * p.scale > p.Hs || p.w * p.scale > p.Ws || p.C < 1 || p.C > 64 || (p.scale != 1 && p.scale != 2))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(postprocess_u8_kernel, dim3((unsigned)grid_for((long long)p.B * p.h * p.scale * p.w * p.scale)),
                      dim3(256), 0, s, p);
@@ -96,7 +109,21 @@ int kdlae_preprocess_u8(const uint8_t* images, int B, int h, int w, int channels
   int H, W;
   kdlae_padded_size(h, w, multiple, &H, &W);
   if (H - h >= h || W - w >= w) return fail(KDLAE_EINVAL_SHAPE, "image smaller than its reflect padding");
-  PreParams p{images, B, h, w, channels, channels == 4 ? 3 : channels, bgr, H, W, img, rate, rate_map};
+  PreParams p{images, B, h, w, channels, channels == 4 ? 3 : channels, bgr, 0, H, W, img, rate, rate_map};
+  HIPCHK(launch_preprocess_u8(p, reinterpret_cast<hipStream_t>(stream)));
+  return KDLAE_OK;
+}
+
+int kdlae_frames_preprocess_u8(const uint8_t* frames, int B, int F, int h, int w, int channels, int multiple,
+                               float* x, void* stream) {
+  using namespace kdlae;
+  if (!frames || !x || B <= 0 || F <= 0 || h <= 0 || w <= 0 || multiple <= 0) return fail(KDLAE_ESTATE, "bad argument");
+  if (channels != 1 && channels != 3 && channels != 4) return fail(KDLAE_EINVAL_SHAPE, "channels must be 1, 3 or 4");
+  int H, W;
+  kdlae_padded_size(h, w, multiple, &H, &W);
+  if (H - h >= h || W - w >= w) return fail(KDLAE_EINVAL_SHAPE, "frame smaller than its reflect padding");
+  // the F frames of a sample are independent images: [B*F][h][w][channels] -> [B*F][1][H][W] = [B][F][H][W]
+  PreParams p{frames, B * F, h, w, channels, 1, 0, 1, H, W, x, nullptr, nullptr};
   HIPCHK(launch_preprocess_u8(p, reinterpret_cast<hipStream_t>(stream)));
   return KDLAE_OK;
 }

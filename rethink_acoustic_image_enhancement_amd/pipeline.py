@@ -5,6 +5,9 @@
   multiple of 8, constant ``denoise_rate`` map, forward, then clamp / crop / ``img_as_ubyte`` and the
   zero-mask of input-black pixels (x2 nearest for ``sr``).  Pre and post are HIP kernels
   (``kdlae_preprocess_u8`` / ``kdlae_postprocess_u8``); images never round-trip through the host.
+* ``frames_preprocess_u8`` / ``enhance_frames_u8`` — KDLAE/KDLAE-S.ipynb's cell: F frames (gray or
+  cv2 BGR/BGRA u8) -> COLOR_BGR2GRAY -> /255 -> [B,F,H,W] reflect-padded to a multiple of 32 ->
+  KDLAE_student -> clamp / crop / permute to [h,w,F] / ``img_as_ubyte``, pre and post on the GPU.
 * ``asdqe_scores`` / ``score_statistics`` / ``write_statistics_csv`` — ASDQE/ASDQE_test.py's
   ``infer`` + ``calculate_statistics`` + ``visualize_comparison`` CSV (:87-133).
 """
@@ -75,22 +78,52 @@ def enhance_u8(model, images: torch.Tensor, denoise_rate, bgr: bool = False, mul
     return hq, sr
 
 
+def frames_preprocess_u8(frames: torch.Tensor, multiple: int = 32) -> torch.Tensor:
+    """u8 frames (cuda) [B,F,h,w] (gray) or [B,F,h,w,C] (cv2 BGR / BGRA) -> f32 [B,F,H,W]."""
+    if frames.device.type != "cuda" or frames.dtype != torch.uint8 or frames.dim() not in (4, 5):
+        raise RuntimeError("frames_preprocess_u8 expects a cuda uint8 tensor [B,F,h,w] or [B,F,h,w,C]")
+    frames = frames.contiguous()
+    B, F, h, w = frames.shape[:4]
+    C = frames.shape[4] if frames.dim() == 5 else 1
+    H, W = padded_size(h, w, multiple)
+    x = torch.empty((B, F, H, W), device=frames.device, dtype=torch.float32)
+    rc = _lib.lib().kdlae_frames_preprocess_u8(ctypes.c_void_p(frames.data_ptr()), B, F, h, w, C, multiple,
+                                               ctypes.c_void_p(x.data_ptr()), _stream(frames.device))
+    _lib.check(rc, "kdlae_frames_preprocess_u8")
+    return x
+
+
+def enhance_frames_u8(model, frames: torch.Tensor, multiple: int = 32) -> torch.Tensor:
+    """KDLAE-S.ipynb inference for u8 frame stacks [B,F,h,w(,C)] -> u8 [B,h,w,F] (restored frames)."""
+    h, w = frames.shape[2], frames.shape[3]
+    x = frames_preprocess_u8(frames, multiple)
+    with torch.no_grad():
+        y = model(x)
+    return postprocess_u8(y, h, w, 1, None)
+
+
 def to_tensor_u8(images: torch.Tensor) -> torch.Tensor:
     """torchvision ToTensor for u8 [B,h,w,C] RGB on the GPU: f32 [B,C,h,w] / 255 (no padding)."""
     img, _ = preprocess_u8(images, None, multiple=1)
     return img
 
 
-def asdqe_scores(model, lq_u8: torch.Tensor, gt_u8: torch.Tensor) -> np.ndarray:
-    """ASDQE_test.py ``infer`` (:87-104) for one batch of equally sized RGB pairs -> scores [B]."""
+def asdqe_scores(model, lq_u8: torch.Tensor, gt_u8: torch.Tensor, chunk: int = 64) -> np.ndarray:
+    """ASDQE_test.py ``infer`` (:87-104) for equally sized RGB pairs u8 [N,h,w,3] -> float32 scores [N].
+    The script scores one pair per forward; every pair is independent (GAP slots depend on the image
+    size only), so scoring ``chunk`` pairs per forward gives the same values."""
+    out = []
     with torch.no_grad():
-        s = model(to_tensor_u8(lq_u8), to_tensor_u8(gt_u8))
-    return s.float().cpu().numpy().reshape(-1)
+        for c0 in range(0, lq_u8.shape[0], chunk):
+            s = model(to_tensor_u8(lq_u8[c0:c0 + chunk]), to_tensor_u8(gt_u8[c0:c0 + chunk]))
+            out.append(s.float().cpu().numpy().reshape(-1))
+    return np.concatenate(out)
 
 
 def score_statistics(values) -> dict:
-    """ASDQE_test.py ``calculate_statistics`` (:107-120)."""
-    v = np.asarray(values, dtype=np.float64)
+    """ASDQE_test.py ``calculate_statistics`` (:107-120), on the float32 predictions as the script
+    has them (np.mean / np.std of a float32 array accumulate in float32, pairwise)."""
+    v = np.asarray(values)
     return {"mean": float(np.mean(v)), "std": float(np.std(v)), "min": float(np.min(v)),
             "25%": float(np.percentile(v, 25)), "50%": float(np.percentile(v, 50)),
             "75%": float(np.percentile(v, 75)), "max": float(np.max(v))}
@@ -101,7 +134,7 @@ def write_statistics_csv(stats_by_method: dict, path: str) -> None:
     methods = list(stats_by_method)
     keys = list(next(iter(stats_by_method.values())))
     with open(path, "w", newline="") as f:
-        wr = csv.writer(f)
+        wr = csv.writer(f, lineterminator="\n")  # pandas DataFrame.to_csv line endings
         wr.writerow([""] + methods)
         for k in keys:
             wr.writerow([k] + [f"{stats_by_method[m][k]:.6f}" for m in methods])

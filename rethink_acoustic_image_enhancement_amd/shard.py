@@ -20,16 +20,28 @@ def shard_range(n_items: int, rank: int, world: int) -> tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
+def _batch_size(batch: dict) -> int:
+    if batch.get("img") is not None:
+        return batch["img"].shape[0]
+    for v in batch.values():
+        if v is not None:
+            return v.shape[0]
+    raise ValueError("empty batch")
+
+
 def shard_batch(batch: dict, rank: int, world: int) -> dict:
-    """Slice every tensor of a KDLAE-T input dict ({'img', 'denoise_rate'}) to this rank's images."""
-    n = next(iter(batch.values())).shape[0]
-    s, e = shard_range(n, rank, world)
-    return {k: v[s:e] for k, v in batch.items()}
+    """Slice every tensor of a KDLAE-T input dict ({'img', 'denoise_rate'}) to this rank's images;
+    None entries (``denoise_rate`` when params != 'cat') pass through."""
+    s, e = shard_range(_batch_size(batch), rank, world)
+    return {k: (v[s:e] if v is not None else None) for k, v in batch.items()}
 
 
 def gather_outputs(local: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather equal-sized per-rank shards into the full batch in rank order."""
     world = dist.get_world_size(group)
+    if local.is_cuda and dist.get_backend(group) != "nccl":
+        # gloo moves host memory: stage a device shard through the host (multi-process tests on one GPU)
+        return gather_outputs(local.cpu(), group).to(local.device)
     out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, local.contiguous(), group=group)
@@ -44,10 +56,42 @@ def sharded_forward(model, batch: dict, group=None, gather: bool = True) -> dict
     The global batch must divide evenly across ranks when ``gather`` is set (equal shard sizes).
     """
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    n = next(iter(batch.values())).shape[0]
+    n = _batch_size(batch)
     if gather and n % world:
         raise ValueError(f"global batch {n} must be divisible by world size {world} to gather")
     out = model(shard_batch(batch, rank, world))
     if not gather:
         return out
     return {k: (gather_outputs(v, group) if v is not None else None) for k, v in out.items()}
+
+
+def gather_varlen(local: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather shards whose leading sizes differ by rank (a contiguous split of N items that
+    does not divide evenly): pad to the largest shard, gather, trim, concatenate in rank order."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    m = max(sizes)
+    padded = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    padded[:local.shape[0]] = local
+    full = gather_outputs(padded, group)
+    return torch.cat([full[r * m:r * m + sizes[r]] for r in range(world)])
+
+
+def sharded_scores(model, lq: torch.Tensor, gt: torch.Tensor, group=None, gather: bool = True,
+                   chunk: int = 64) -> torch.Tensor:
+    """ASDQE batch scoring (ASDQE/ASDQE_test.py:87-104 ``infer``) split across ranks: rank r scores
+    its contiguous share of the N (lq, gt) pairs in chunks of ``chunk`` images, then (``gather``)
+    the [N, 1] scores are all-gathered in rank order, so every rank holds the full score list."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    s, e = shard_range(lq.shape[0], rank, world)
+    dev = next(model.parameters()).device
+    parts = []
+    with torch.no_grad():
+        for c0 in range(s, e, chunk):
+            c1 = min(e, c0 + chunk)
+            parts.append(model(lq[c0:c1].to(dev), gt[c0:c1].to(dev)).reshape(-1, 1))
+    local = torch.cat(parts) if parts else torch.zeros((0, 1), device=dev)
+    return gather_varlen(local, group) if gather else local

@@ -18,6 +18,7 @@ There is no CPU fallback: every entry point raises on CPU tensors or a missing l
 from __future__ import annotations
 
 import ctypes
+import math
 import random
 
 import torch
@@ -148,6 +149,9 @@ class TeacherTrainFn(torch.autograd.Function):
     def forward(ctx, engine, img, rate, *params):
         theta = engine.flatten(params)
         hq, sr = engine.forward(theta, img, rate)
+        # an output the loss ignores arrives as None (not zeros), so the branch that produced only it
+        # gets None gradients and torch.optim skips those parameters, as with the reference module
+        ctx.set_materialize_grads(False)
         ctx.engine = engine
         ctx.generation = engine.generation
         ctx.theta = theta
@@ -162,11 +166,16 @@ class TeacherTrainFn(torch.autograd.Function):
         if eng.generation != ctx.generation:
             raise RuntimeError("KDLAE_teacher: a second training forward ran before this graph's backward; "
                                "the HIP engine keeps one set of saved activations per model and device")
+        if dhq is None and dsr is None:
+            return (None, None, None, *[None] * len(ctx.shapes))
         grad = torch.empty(eng.numel, dtype=torch.float32, device=ctx.theta.device)
-        eng.backward(ctx.theta, dhq, dsr, grad)
+        eng.backward(ctx.theta, dhq, dsr, grad)  # a None output gradient is read as zero
+        # sr = enhance(cen(hq)) (KDLAE_model.py:324-329): with no sr gradient that branch is untouched
+        skip = ("cen.", "upen.", "enhance.", "outputen.") if dsr is None else None
         grads = []
         for (k, n, off), shape, used in zip(eng.keys, ctx.shapes, eng.used):
-            grads.append(grad[off:off + n].view(shape) if used else None)
+            live = used and not (skip and k.startswith(skip))
+            grads.append(grad[off:off + n].view(shape) if live else None)
         return (None, None, None, *grads)
 
 
@@ -282,8 +291,42 @@ def sync_gradients(grad: torch.Tensor, group=None) -> float:
     ws = dist.get_world_size(group)
     if ws == 1:
         return 1.0
-    dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+    if grad.is_cuda and dist.get_backend(group) != "nccl":
+        host = grad.cpu()  # gloo reduces host memory (multi-process tests sharing one GPU)
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        grad.copy_(host)
+    else:
+        dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
     return 1.0 / ws
+
+
+def _position_from_periods(iteration: int, cumulative_period) -> int:
+    """get_position_from_periods (Train/basicsr/models/lr_scheduler.py:115-133)."""
+    for i, period in enumerate(cumulative_period):
+        if iteration <= period:
+            return i
+    return None
+
+
+class CosineAnnealingRestartCyclicLR:
+    """The LR schedule of KDLAET.yml (train.scheduler, :95-99), lr_scheduler.py:186-233 restated
+    over the trainer's single parameter group: ``lr(last_epoch)`` is what the reference's
+    ``get_lr`` returns after ``last_epoch`` scheduler steps."""
+
+    def __init__(self, base_lr: float, periods, restart_weights=(1,), eta_mins=(0,)):
+        if len(periods) != len(restart_weights):
+            raise ValueError("periods and restart_weights should have the same length.")
+        self.base_lr = float(base_lr)
+        self.periods, self.restart_weights, self.eta_mins = list(periods), list(restart_weights), list(eta_mins)
+        self.cumulative_period = [sum(self.periods[:i + 1]) for i in range(len(self.periods))]
+
+    def lr(self, last_epoch: int) -> float:
+        idx = _position_from_periods(last_epoch, self.cumulative_period)
+        w = self.restart_weights[idx]
+        nearest_restart = 0 if idx == 0 else self.cumulative_period[idx - 1]
+        eta_min = self.eta_mins[idx]
+        return eta_min + w * 0.5 * (self.base_lr - eta_min) * (
+            1 + math.cos(math.pi * ((last_epoch - nearest_restart) / self.periods[idx])))
 
 
 class KDLAETrainer:
@@ -293,7 +336,7 @@ class KDLAETrainer:
     weight_decay 5e-5, betas (0.2, 0.999); use_grad_clip -> clip_grad_norm_(0.01); L1LossSr."""
 
     def __init__(self, model, lr=1e-5, weight_decay=0.5e-4, betas=(0.2, 0.999), eps=1e-8, use_grad_clip=True,
-                 max_norm=0.01, loss_weight=1.0, group=None, mixing_augs=None, ema_decay=0.0):
+                 max_norm=0.01, loss_weight=1.0, group=None, mixing_augs=None, ema_decay=0.0, scheduler=None):
         params = list(model.parameters())
         if not params or params[0].device.type != "cuda":
             raise RuntimeError("KDLAETrainer: move the model to a ROCm device first (no CPU fallback)")
@@ -310,6 +353,10 @@ class KDLAETrainer:
         self.exp_avg = torch.zeros_like(self.grad)
         self.exp_avg_sq = torch.zeros_like(self.grad)
         self.lr, self.weight_decay, self.betas, self.eps = lr, weight_decay, tuple(betas), eps
+        self.init_lr = lr
+        # train.scheduler (e.g. CosineAnnealingRestartCyclicLR for KDLAET.yml); driven by the caller
+        # through update_learning_rate(current_iter) like BaseModel's, else the lr stays fixed
+        self.scheduler = scheduler
         self.max_norm = max_norm if use_grad_clip else 0.0
         self.loss_weight = loss_weight
         self.group = group
@@ -330,6 +377,16 @@ class KDLAETrainer:
         # train.ema_decay (ImageCleanModel.__init__: net_g_ema starts as a copy of net_g, model_ema(0))
         self.ema_decay = float(ema_decay)
         self.theta_ema = self.theta.clone() if self.ema_decay > 0 else None
+
+    def update_learning_rate(self, current_iter: int, warmup_iter: int = -1) -> float:
+        """BaseModel.update_learning_rate (Train/basicsr/models/base_model.py:183-205): the scheduler
+        has stepped current_iter - 1 times by iteration current_iter (train.py calls this before
+        optimize_parameters); linear warm-up below warmup_iter.  Returns the lr now in force."""
+        if self.scheduler is not None:
+            self.lr = self.scheduler.lr(max(current_iter - 1, 0))
+        if current_iter < warmup_iter:
+            self.lr = self.init_lr / warmup_iter * current_iter
+        return self.lr
 
     def feed_train_data(self, lq: dict, gt: dict):
         """ImageCleanModel.feed_train_data (:161-186): the optional mixup of (gt, lq)."""
@@ -375,8 +432,6 @@ class KDLAETrainer:
             float(self.weight_decay), self.step_count, self._ranges if self._nranges else None, self._nranges,
             _vp(self._opt_scratch), _stream(self.theta.device))
         _lib.check(rc, "kdlae_train_clip_adamw")
-        for eng in getattr(self.model, "_engines", {}).values():
-            eng.signature = None  # inference handles re-pack the updated weights on next use
         if self.theta_ema is not None:  # model_ema(decay) after the step (:221-222)
             rc = _lib.lib().kdlae_train_ema(_vp(self.theta_ema), _vp(self.theta), self.engine.numel,
                                             self.ema_decay, _stream(self.theta.device))

@@ -375,10 +375,109 @@ def key_lists(KM, AM, out):
         json.dump(res, f, separators=(",", ":"))
 
 
+def lr_goldens(out):
+    """KDLAET.yml's LR curve from the reference scheduler itself (Train/basicsr/models/lr_scheduler.py,
+    imported by file path): lr in force at iteration i, where BasicSR steps the scheduler once per
+    iteration from i = 2 on (base_model.py:183-193)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_lr_scheduler",
+                                                  os.path.join(REF, "Train/basicsr/models/lr_scheduler.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    cfg = dict(periods=[90000, 8000], restart_weights=[1, 1], eta_mins=[0.0003, 0.000001])
+    opt = torch.optim.AdamW([torch.nn.Parameter(torch.zeros(1))], lr=1e-5)
+    sch = mod.CosineAnnealingRestartCyclicLR(opt, **cfg)
+    marks = sorted(set([1, 2, 3, 100, 45000, 89999, 90000, 90001, 90002, 94000, 97999, 98000, 98001]
+                       + list(range(1, 98001, 997))))
+    res = {}
+    for it in range(1, 98002):
+        if it > 1:
+            sch.step()
+        if it in marks:
+            res[str(it)] = opt.param_groups[0]["lr"]
+    with open(os.path.join(out, "lr_kdlaet.json"), "w") as f:
+        json.dump({"scheduler": cfg, "base_lr": 1e-5, "lr_at_iter": res}, f)
+    print("lr", len(res), "points")
+
+
+def frames_goldens(KM, out):
+    """KDLAE-S.ipynb's default sample ('Sample for US': Sample/CAMUS/origin, inp_frames 7, KDLAE_student
+    hidden [16,32,64] residual): the first 7 frames in sorted order (the notebook draws a random start),
+    cropped to 70x60 to keep the fixture small.  The PNGs are lossless BGRA-equivalent RGBA, so the
+    decoded bytes are what cv2.imread(IMREAD_UNCHANGED) returns (channels reordered to BGRA).  Saved:
+    the u8 frames, and the reference module's output on load_consecutive_stack -> pad-to-32 input."""
+    import glob as _glob
+
+    from PIL import Image
+
+    from oracle.pipeline_oracle import load_consecutive_stack, notebook_pad
+    files = sorted(_glob.glob(os.path.join(REF, "Sample/CAMUS/origin/*.png")))[:7]
+    frames = []
+    for f in files:
+        a = np.asarray(Image.open(f))                    # RGBA
+        a = a[..., [2, 1, 0, 3]] if a.shape[2] == 4 else a[..., ::-1]  # cv2 order: BGRA / BGR
+        frames.append(np.ascontiguousarray(a[240:310, 260:320]))
+    frames = np.stack(frames)                            # [7, 70, 60, 4]
+    kw = dict(inp_channels=1, out_channels=1, residual=True, hidden_channels=[16, 32, 64])
+    m = _load_hash(KM.KDLAE_student(**kw))
+    x = notebook_pad(load_consecutive_stack(list(frames)), 32)
+    with torch.no_grad():
+        y = m(x)
+    np.savez_compressed(os.path.join(out, "frames_camus7.npz"), frames=frames, restored=y.numpy(),
+                        files=np.frombuffer(json.dumps([os.path.basename(f) for f in files]).encode(), np.uint8),
+                        cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8))
+    print("frames", frames.shape, tuple(x.shape), tuple(y.shape))
+
+
+def asdqe_scoring_goldens(AM, out):
+    """ASDQE/ASDQE_test.py __main__ on the reference's own MDD samples: methods origin / Teacher /
+    Student@0.05 (:145-149), pairs from sorted folder listings (:42-50), PIL RGB + ToTensor (:59-65),
+    bs=1 infer (:87-104), calculate_statistics (:107-120) and visualize_comparison's CSV (:123-133,
+    written here by pandas exactly as the script does).  Each 658x438 JPEG is cropped to 64x64 so the
+    fixture stays small; hash weights (the released ASDQE.pth is not available offline)."""
+    import io as _io
+
+    import pandas as pd
+    from PIL import Image
+
+    base = os.path.join(REF, "Sample/MDD/origin")
+    methods = {"origin": base, "Teacher": os.path.join(REF, "Sample/MDD/denoise/KDLAE-T"),
+               "Student@0.05": os.path.join(REF, "Sample/MDD/denoise/KDLAE-S_prob@0.05")}
+    m = _load_hash(AM.DenoiseRatePredictor())
+    crop = (slice(200, 264), slice(180, 244))
+    load = lambda p: np.asarray(Image.open(p).convert("RGB"))[crop]  # noqa: E731
+    lq_files = sorted(os.listdir(base))
+    lq = np.stack([load(os.path.join(base, f)) for f in lq_files])
+    arrays, preds, stats = {"lq": lq}, {}, []
+    for name, d in methods.items():
+        gt = np.stack([load(os.path.join(d, f)) for f in sorted(os.listdir(d))])
+        arrays["gt_" + name] = gt
+        p = []
+        with torch.no_grad():
+            for i in range(len(lq_files)):
+                t = lambda a: torch.from_numpy(a[i].astype(np.float32) / 255.0).permute(2, 0, 1)[None]  # noqa: E731
+                p.extend(m(t(lq), t(gt)).cpu().numpy().flatten())
+        p = np.array(p)
+        preds[name] = p
+        stats.append({"mean": np.mean(p), "std": np.std(p), "min": np.min(p), "25%": np.percentile(p, 25),
+                      "50%": np.percentile(p, 50), "75%": np.percentile(p, 75), "max": np.max(p)})
+    df = pd.DataFrame(stats)
+    df.index = list(methods)
+    buf = _io.StringIO()
+    df.T.to_csv(buf, float_format="%.6f", index=True)
+    np.savez_compressed(os.path.join(out, "asdqe_scoring_mdd.npz"), **arrays,
+                        **{"pred_" + k: v for k, v in preds.items()},
+                        csv=np.frombuffer(buf.getvalue().encode(), np.uint8),
+                        methods=np.frombuffer(json.dumps(list(methods)).encode(), np.uint8),
+                        cfg=np.frombuffer(json.dumps(dict(in_channels=3, dim=16)).encode(), np.uint8))
+    print("asdqe scoring", {k: v.round(5).tolist()[:3] for k, v in preds.items()})
+    print(buf.getvalue())
+
+
 def main():
     KM, AM = _import_ref()
     out = HERE
-    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512", "train", "ckpt", "keys"]
+    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512", "train", "ckpt", "keys", "lr", "frames", "scoring"]
     if "train" in which:
         train_goldens(KM, out)
     if "teacher" in which:
@@ -393,6 +492,12 @@ def main():
         ckpt_goldens(KM, AM, out)
     if "keys" in which:
         key_lists(KM, AM, out)
+    if "lr" in which:
+        lr_goldens(out)
+    if "frames" in which:
+        frames_goldens(KM, out)
+    if "scoring" in which:
+        asdqe_scoring_goldens(AM, out)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,106 @@
+"""Multi-process readiness on one GPU: the real HIP modules in two
+fresh processes (one per rank, as torchrun launches them), rendezvous over gloo on 127.0.0.1.
+
+* Inference: ``sharded_forward(KDLAE_teacher, gather=True)`` on a bs=4 batch split 2 + 2 equals the
+  single-process bs=4 run bit for bit (every image's reductions are batch-independent).
+* Training: ``KDLAETrainer.optimize_parameters`` with the DDP-style flat-gradient all-reduce
+  (``sync_gradients``, base_model.py:76-82) on 2 + 2 images: both ranks end with identical
+  parameters, and the averaged gradient matches the single-process bs=4 gradient.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+KW = dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, LayerNorm_type="BiasFree")
+
+
+def _inputs():
+    from rethink_acoustic_image_enhancement_amd.hashweights import hash_images
+    img = torch.from_numpy(hash_images("mp_img", (4, 3, 32, 48)))
+    rate = torch.from_numpy(hash_images("mp_rate", (4, 1, 32, 48)))
+    gt = {"hq": torch.from_numpy(hash_images("mp_gt", (4, 3, 32, 48))),
+          "sr": torch.from_numpy(hash_images("mp_gtsr", (4, 3, 64, 96)))}
+    return img, rate, gt
+
+
+def _model():
+    from rethink_acoustic_image_enhancement_amd.hashweights import load_hash_weights
+    from rethink_acoustic_image_enhancement_amd.KDLAE_model import KDLAE_teacher
+    m = KDLAE_teacher(**KW)
+    load_hash_weights(m)
+    return m.to("cuda:0")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from rethink_acoustic_image_enhancement_amd.shard import shard_range, sharded_forward
+    from rethink_acoustic_image_enhancement_amd.train import KDLAETrainer
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        img, rate, gt = _inputs()
+        m = _model().eval()
+        with torch.no_grad():
+            out = sharded_forward(m, {"img": img.cuda(), "denoise_rate": rate.cuda()}, gather=True)
+        res = {"hq": out["hq"].cpu(), "sr": out["sr"].cpu()}
+        tm = _model().train()
+        tr = KDLAETrainer(tm, lr=1e-3)
+        s, e = shard_range(4, rank, world)
+        lq = {"img": img[s:e].cuda(), "denoise_rate": rate[s:e].cuda()}
+        tr.forward_backward(lq, {k: v[s:e].cuda() for k, v in gt.items()})
+        from rethink_acoustic_image_enhancement_amd.train import sync_gradients
+        scale = sync_gradients(tr.grad)
+        res["grad_mean"] = (tr.grad * scale).cpu()
+        tr.step(scale)
+        res["theta"] = tr.theta.detach().cpu()
+        q.put((rank, res))
+        dist.destroy_process_group()
+    except Exception as ex:  # surface the failure in the parent instead of hanging on the queue
+        q.put((rank, repr(ex)))
+
+
+def test_two_processes_share_the_gpu():
+    img, rate, gt = _inputs()
+    from rethink_acoustic_image_enhancement_amd.train import KDLAETrainer
+    m = _model().eval()
+    with torch.no_grad():
+        ref = m({"img": img.cuda(), "denoise_rate": rate.cuda()})
+    ref = {k: v.cpu() for k, v in ref.items()}
+    tm = _model().train()
+    tr = KDLAETrainer(tm, lr=1e-3)
+    tr.forward_backward({"img": img.cuda(), "denoise_rate": rate.cuda()}, {k: v.cuda() for k, v in gt.items()})
+    g_ref = tr.grad.detach().cpu()
+    torch.cuda.synchronize()
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert isinstance(res[r], dict), res[r]
+        assert torch.equal(res[r]["hq"], ref["hq"]) and torch.equal(res[r]["sr"], ref["sr"])
+    assert torch.equal(res[0]["theta"], res[1]["theta"])
+    err = float((res[0]["grad_mean"] - g_ref).abs().max() / g_ref.abs().max())
+    print(f"2-rank mean gradient vs single-process bs=4: {err:.3e} of max |g|")
+    assert err <= 1e-4
+    assert np.isfinite(res[0]["theta"].numpy()).all()

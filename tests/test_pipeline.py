@@ -76,3 +76,48 @@ def test_checkpoint_raw_state_dicts(tmp_path):
     torch.save({"something": 3}, tmp_path / "bad.pth")
     with pytest.raises(RuntimeError):
         read_state_dict(str(tmp_path / "bad.pth"))
+
+
+def test_frames_oracle_pinned_by_camus_fixture():
+    """KDLAE-S.ipynb cell on the reference's own CAMUS frames (tests/golden/frames_camus7.npz): the
+    oracle's load_consecutive_stack + pad-to-32 + student forward reproduces the reference module's
+    output; COLOR_BGR2GRAY is the identity on these gray-as-BGRA frames (and on any R = G = B)."""
+    from oracle.kdlae_oracle import StudentCfg, student_forward, student_param_shapes
+    from oracle.pipeline_oracle import bgr2gray_u8, load_consecutive_stack, notebook_pad
+    from tests.util import hash_sd_for, load_fixture
+
+    d, kw = load_fixture("frames_camus7")
+    frames = d["frames"]
+    x = load_consecutive_stack(list(frames))
+    assert torch.equal(x[0], torch.from_numpy(frames[..., 0].astype(np.float32) / 255.0))
+    v = np.arange(256, dtype=np.uint8)
+    assert np.array_equal(bgr2gray_u8(np.stack([v, v, v], -1)), v)
+    xp = notebook_pad(x, 32)
+    assert tuple(xp.shape) == (1, 7, 96, 64)
+    cfg = StudentCfg(**kw)
+    with torch.no_grad():
+        y = student_forward(hash_sd_for(student_param_shapes(cfg)), xp, cfg)
+    assert float((y - torch.from_numpy(d["restored"])).abs().max()) <= 1e-5
+
+
+def test_asdqe_statistics_and_csv_match_the_script(tmp_path):
+    """ASDQE_test.py calculate_statistics + visualize_comparison's CSV (pandas, float_format %.6f),
+    from the fixture the script's own code path wrote (tests/golden/asdqe_scoring_mdd.npz)."""
+    import json
+
+    from oracle.asdqe_oracle import AsdqeCfg, asdqe_forward, asdqe_param_shapes
+    from rethink_acoustic_image_enhancement_amd.pipeline import score_statistics, write_statistics_csv
+    from tests.util import hash_sd_for, load_fixture
+
+    d, kw = load_fixture("asdqe_scoring_mdd")
+    methods = json.loads(bytes(d["methods"]).decode())
+    stats = {m: score_statistics(d["pred_" + m]) for m in methods}
+    write_statistics_csv(stats, str(tmp_path / "stats.csv"))
+    assert (tmp_path / "stats.csv").read_text() == bytes(d["csv"]).decode()
+    # the oracle reproduces the script's predictions from the same u8 pairs (ToTensor = /255)
+    cfg = AsdqeCfg(**kw)
+    sd = hash_sd_for(asdqe_param_shapes(cfg))
+    t = lambda a: torch.from_numpy(a.astype(np.float32) / 255.0).permute(0, 3, 1, 2)  # noqa: E731
+    with torch.no_grad():
+        p = asdqe_forward(sd, t(d["lq"]), t(d["gt_Teacher"]), cfg).numpy().reshape(-1)
+    assert np.abs(p - d["pred_Teacher"]).max() <= 1e-6

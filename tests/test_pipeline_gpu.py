@@ -69,3 +69,82 @@ def test_enhance_u8_end_to_end():
         exp = postprocess(r, 58, 42, u8, s)
         d = np.abs(got[0].cpu().numpy().astype(np.int32) - exp.astype(np.int32))
         assert d.max() <= 1 and (d == 0).mean() > 0.99
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+def test_frames_preprocess_matches_notebook(c):
+    """KDLAE-S.ipynb load_consecutive_stack (cv2 BGR2GRAY, /255) + reflect pad to 32, bit-exact."""
+    from oracle.pipeline_oracle import load_consecutive_stack, notebook_pad
+    from rethink_acoustic_image_enhancement_amd.pipeline import frames_preprocess_u8
+
+    B, F, h, w = 2, 5, 45, 70
+    rng = np.random.default_rng(c)
+    fr = rng.integers(0, 256, (B, F, h, w, c), dtype=np.uint8)
+    t = torch.from_numpy(fr if c > 1 else fr[..., 0]).to(DEV)
+    x = frames_preprocess_u8(t, 32).cpu()
+    for b in range(B):
+        ref = notebook_pad(load_consecutive_stack([f if c > 1 else f[..., 0] for f in fr[b]]), 32)
+        assert torch.equal(x[b:b + 1], ref)
+
+
+def test_enhance_frames_camus_end_to_end():
+    """The KDLAE-S notebook cell on the reference's CAMUS frames: HIP pre -> HIP KDLAE_student -> HIP
+    post vs the reference module's output run through the notebook's output cell (u8 [h, w, F]).
+    u8 values may differ by one level where fp32 results straddle a rounding boundary."""
+    from oracle.pipeline_oracle import student_postprocess
+    from rethink_acoustic_image_enhancement_amd.KDLAE_model import KDLAE_student
+    from rethink_acoustic_image_enhancement_amd.hashweights import load_hash_weights
+    from rethink_acoustic_image_enhancement_amd.pipeline import enhance_frames_u8
+    from tests.util import load_fixture
+
+    d, kw = load_fixture("frames_camus7")
+    m = KDLAE_student(**kw)
+    load_hash_weights(m)
+    m = m.to(DEV).eval()
+    out = enhance_frames_u8(m, torch.from_numpy(d["frames"][None]).to(DEV)).cpu().numpy()[0]
+    exp = student_postprocess(torch.from_numpy(d["restored"]), 70, 60)
+    assert out.shape == exp.shape == (70, 60, 7)
+    diff = np.abs(out.astype(np.int32) - exp.astype(np.int32))
+    assert diff.max() <= 1 and (diff == 0).mean() > 0.99
+
+
+def test_postprocess_frames_bit_exact():
+    from oracle.pipeline_oracle import student_postprocess
+    rng = np.random.default_rng(5)
+    y = torch.from_numpy(rng.uniform(-0.3, 1.3, (2, 7, 64, 96)).astype(np.float32))
+    got = postprocess_u8(y.to(DEV), 50, 81, 1, None).cpu().numpy()
+    for b in range(2):
+        assert np.array_equal(got[b], student_postprocess(y[b:b + 1], 50, 81))
+
+
+def test_asdqe_scoring_pipeline_vs_script():
+    """ASDQE_test.py end to end on the GPU (asdqe_scores -> score_statistics -> CSV) on the reference's
+    MDD sample crops for the script's three methods, vs the values the script's code path produced."""
+    import csv
+    import io
+    import json
+
+    from rethink_acoustic_image_enhancement_amd.ASDQE_model import DenoiseRatePredictor
+    from rethink_acoustic_image_enhancement_amd.hashweights import load_hash_weights
+    from rethink_acoustic_image_enhancement_amd.pipeline import asdqe_scores, score_statistics, write_statistics_csv
+    from tests.util import load_fixture
+
+    d, kw = load_fixture("asdqe_scoring_mdd")
+    methods = json.loads(bytes(d["methods"]).decode())
+    m = DenoiseRatePredictor(**kw)
+    load_hash_weights(m)
+    m = m.to(DEV).eval()
+    lq = torch.from_numpy(d["lq"]).to(DEV)
+    stats = {}
+    for name in methods:
+        s = asdqe_scores(m, lq, torch.from_numpy(d["gt_" + name]).to(DEV), chunk=4)
+        assert s.dtype == np.float32 and np.abs(s - d["pred_" + name]).max() <= 1e-3
+        stats[name] = score_statistics(s)
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        write_statistics_csv(stats, td + "/stats.csv")
+        got = list(csv.reader(open(td + "/stats.csv")))
+    want = list(csv.reader(io.StringIO(bytes(d["csv"]).decode())))
+    assert got[0] == want[0] and [r[0] for r in got] == [r[0] for r in want]
+    for a, b in zip(got[1:], want[1:]):
+        assert all(abs(float(x) - float(y)) <= 2e-6 for x, y in zip(a[1:], b[1:])), (a, b)

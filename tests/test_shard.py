@@ -68,3 +68,48 @@ def test_sharded_forward_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert all(res[r] for r in range(world)), res
+
+
+class _ScoreStandIn(torch.nn.Module):
+    """Per-pair deterministic score with the DenoiseRatePredictor contract ([B,1])."""
+
+    def __init__(self):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.tensor(0.5))
+
+    def forward(self, lq, gt):
+        return torch.tanh(self.w * (lq - gt).abs().mean(dim=(1, 2, 3))).unsqueeze(1)
+
+
+def _score_worker(rank, world, port, q):
+    from rethink_acoustic_image_enhancement_amd.shard import shard_batch, sharded_scores
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(1)
+    n = 11  # does not divide by the world size: uneven shards, gathered in rank order
+    lq, gt = torch.rand(n, 3, 8, 8, generator=g), torch.rand(n, 3, 8, 8, generator=g)
+    m = _ScoreStandIn()
+    full = sharded_scores(m, lq, gt, chunk=2)
+    ok = full.shape == (n, 1) and torch.equal(full, m(lq, gt).detach())
+    s, e = shard_range(n, rank, world)
+    ok = ok and torch.equal(sharded_scores(m, lq, gt, gather=False, chunk=3), m(lq[s:e], gt[s:e]).detach())
+    # params != 'cat': denoise_rate is None and passes through the shard
+    sb = shard_batch({"img": lq, "denoise_rate": None}, rank, world)
+    ok = ok and sb["denoise_rate"] is None and torch.equal(sb["img"], lq[s:e])
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_asdqe_scores_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_score_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r] for r in range(world)), res

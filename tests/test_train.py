@@ -178,3 +178,25 @@ def test_sync_gradients_single_process_is_identity():
     g = torch.ones(4)
     assert sync_gradients(g) == 1.0
     assert torch.equal(g, torch.ones(4))
+
+
+def test_lr_schedule_matches_reference_scheduler():
+    """KDLAET.yml train.scheduler: CosineAnnealingRestartCyclicLR values produced by the reference's
+    own scheduler (tests/golden/lr_kdlaet.json, make_golden.py lr_goldens) at the lr BasicSR has in
+    force at each iteration (scheduler stepped from iteration 2 on, base_model.py:183-193)."""
+    import json
+    import types
+
+    from rethink_acoustic_image_enhancement_amd.train import CosineAnnealingRestartCyclicLR, KDLAETrainer
+    from tests.util import GOLDEN
+
+    with open(os.path.join(GOLDEN, "lr_kdlaet.json")) as f:
+        g = json.load(f)
+    sch = CosineAnnealingRestartCyclicLR(g["base_lr"], **g["scheduler"])
+    fake = types.SimpleNamespace(scheduler=sch, init_lr=g["base_lr"], lr=g["base_lr"])
+    for it, want in g["lr_at_iter"].items():
+        got = KDLAETrainer.update_learning_rate(fake, int(it))
+        assert abs(got - want) <= 1e-12 + 1e-9 * abs(want), (it, got, want)
+    # linear warm-up (base_model.py:194-205) when warmup_iter > current_iter
+    fake2 = types.SimpleNamespace(scheduler=None, init_lr=1e-4, lr=1e-4)
+    assert abs(KDLAETrainer.update_learning_rate(fake2, 5, warmup_iter=10) - 5e-5) < 1e-15
