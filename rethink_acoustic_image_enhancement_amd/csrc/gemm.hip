@@ -20,6 +20,9 @@
 // fma chain (no xf32 on gfx950), so numerics equal an f32 dot product with a permuted k order.
 #include "kernels.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace kdlae {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -364,6 +367,157 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Resident 1x1 schedule, r02 ("straight-line"): the same work decomposition as the RES branch of
+// conv_gemm_kernel, restructured so the compiler can count every vector-memory op.
+//  * The n-chunk loop is unrolled (NCH = ceil(group_tiles / NT) is a template parameter) and every
+//    global access is a raw BUFFER load/store through a per-image descriptor: rows past the image
+//    and channels past N fall outside the descriptor's range, so out-of-range loads return 0 and
+//    out-of-range stores are dropped by the hardware.  No exec-masked branches remain, so hipcc's
+//    waitcnt pass sees one straight-line tile body and waits for exactly the loads it needs
+//    (r01's kernel drained every store with vmcnt(0) inside the n-chunk loop: the PMC profile showed
+//    waves parked on waitcnt for 32% of their cycles and the matrix pipe 58% busy).
+//  * The next tile's A rows are always prefetched (the last tile re-reads its own rows) so the
+//    count of outstanding ops is the same on every path; the residual of a chunk is loaded before
+//    that chunk's MFMAs and consumed after them.
+//  * ReLU is max(v, floor) with floor = 0 or -inf: no branch.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, 0);
+}
+constexpr unsigned kOOB = 0x80000000u;  // a byte offset past every descriptor's range
+
+template <int NT, int KG, int NCH, int WPE, bool HASR, bool PF>
+__global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int HW = p.F * p.H * p.W;
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
+  if (t_begin >= t_end) return;
+  const int g0 = blockIdx.y * p.group_tiles;
+  const int gtiles = min(p.group_tiles, p.ntiles - g0);
+  constexpr int TP = NT * NCH;  // tiles staged per group (zero weights past gtiles)
+  // weights are per image when w_img_stride != 0 (the MDTA-folded projection M = W_proj blockdiag(A))
+  auto stage = [&](int wkey) {
+    const f32x4* wbase =
+        reinterpret_cast<const f32x4*>(p.Wp + (long long)wkey * p.w_img_stride + (long long)g0 * p.kgroups * 256);
+    const int n4 = gtiles * KG * 64;
+    for (int idx = tid; idx < TP * KG * 64; idx += kGemmThreads)
+      wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int idx = tid; idx < TP * 4; idx += kGemmThreads) {
+      const int n = g0 * 16 + 4 * idx;
+      wlds[TP * KG * 64 + idx] = (p.bias && idx < gtiles * 4 && n < p.N)
+                                      ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  int staged = p.w_img_stride ? t_begin / p.tiles_per_img : 0;
+  stage(staged);
+  __syncthreads();
+  const float relu_floor = p.relu ? 0.f : -__builtin_huge_valf();
+  const unsigned a_bytes = (unsigned)HW * (unsigned)p.lda * 4u;
+  const unsigned o_bytes = (unsigned)HW * (unsigned)p.ldo * 4u;
+  const unsigned r_bytes = (unsigned)HW * (unsigned)p.ldr * 4u;
+  // per-lane channel byte offset of staged tile t (kOOB past N / past the group)
+  auto ch_off = [&](int t) -> unsigned {
+    const int nq = (g0 + t) * 16 + 4 * lq;
+    return (t < gtiles && nq < p.N) ? (unsigned)nq * 4u : kOOB;
+  };
+  auto rows_of = [&](int tile, int& b, int& row0) {
+    b = tile / p.tiles_per_img;
+    row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
+  };
+  auto load_rows = [&](int tile, f32x4 (&dst)[kGemmRT][KG]) {
+    int b, row0;
+    rows_of(tile, b, row0);
+    const __amdgpu_buffer_rsrc_t ra = buf_rsrc(p.A + (long long)b * HW * p.lda, a_bytes);
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r) {
+      const unsigned pix = (unsigned)(row0 + r * 16 + li);
+      const unsigned base = pix < (unsigned)HW ? pix * (unsigned)p.lda * 4u + 16u * lq : kOOB;
+#pragma unroll
+      for (int g = 0; g < KG; ++g) dst[r][g] = buf_load4(ra, base + 64u * g);
+    }
+  };
+  f32x4 a[kGemmRT][KG];
+  [[maybe_unused]] f32x4 an[kGemmRT][KG];
+  if constexpr (PF) load_rows(t_begin, an);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    int b, row0;
+    rows_of(tile, b, row0);
+    if (p.w_img_stride && b != staged) {  // block-uniform: the tile range crossed into the next image
+      __syncthreads();
+      stage(b);
+      __syncthreads();
+      staged = b;
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r)
+#pragma unroll
+        for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
+      load_rows(min(tile + 1, t_end - 1), an);  // unconditional: same op count on every path
+    } else {
+      load_rows(tile, a);
+    }
+    if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
+    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t rr;
+    if constexpr (HASR) rr = buf_rsrc(p.R + (long long)b * HW * p.ldr, r_bytes);
+    unsigned pix_o[kGemmRT], pix_r[kGemmRT];
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r) {
+      const unsigned pix = (unsigned)(row0 + r * 16 + li);
+      pix_o[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldo * 4u : kOOB;
+      pix_r[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldr * 4u : kOOB;
+    }
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      [[maybe_unused]] f32x4 res[NT][kGemmRT];
+      if constexpr (HASR) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < kGemmRT; ++r) {
+            const unsigned c = ch_off(ch * NT + t);
+            res[t][r] = buf_load4(rr, ((pix_r[r] | c) & kOOB) ? kOOB : pix_r[r] + c);
+          }
+      }
+      f32x4 acc[NT][kGemmRT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_chunk<NT, KG>(wlds + (size_t)ch * NT * KG * 64, KG, lane, a, acc);
+      const f32x4* bl = wlds + TP * KG * 64 + ch * NT * 4;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f32x4 bias = bl[4 * t + lq];
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) {
+          f32x4 v = acc[t][r] + bias;
+          if constexpr (HASR) v += res[t][r];
+          v = f32x4{fmaxf(v.x, relu_floor), fmaxf(v.y, relu_floor), fmaxf(v.z, relu_floor), fmaxf(v.w, relu_floor)};
+          // pix | ch: both are byte offsets; an out-of-range half sets bit 31 -> dropped
+          const unsigned c = ch_off(ch * NT + t);
+          const unsigned off = ((pix_o[r] | c) & kOOB) ? kOOB : pix_o[r] + c;
+          buf_store4(ro, off, v);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
+    }
+  }
+}
+
 // (NT, KG, CONV3, OUT, PF, WPE, RES).  Resident variants need KG == kgroups exactly.
 #define KDLAE_GEMM_VARIANTS(X) \
   X(9, 3, false, 0, true, 2, true) X(8, 3, false, 0, true, 2, true) X(3, 3, false, 0, true, 2, true) \
@@ -412,9 +566,58 @@ static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, si
   return hipGetLastError();
 }
 
+// (NT, KG, NCH, PF) of the straight-line resident kernel; launched for both HASR values
+#define KDLAE_GEMM_RES2_VARIANTS(X) \
+  X(9, 3, 1, true) X(9, 3, 2, true) X(8, 3, 1, true) X(8, 3, 2, true) X(3, 3, 1, true) X(3, 3, 2, true) \
+  X(6, 3, 1, true) X(6, 3, 2, true) X(9, 6, 1, true) X(9, 6, 2, true) X(8, 6, 1, true) X(8, 6, 2, true) \
+  X(6, 6, 1, true) X(6, 6, 2, true) X(3, 6, 1, true) X(3, 6, 2, true) X(3, 8, 1, true) X(3, 8, 2, true) \
+  X(6, 8, 1, true) X(6, 8, 2, true) X(6, 12, 1, false) X(6, 12, 2, false) X(8, 12, 1, false) \
+  X(8, 12, 2, false) X(3, 12, 1, false) X(3, 12, 2, false) X(6, 16, 1, false) X(3, 16, 1, false)
+
+template <int NT, int KG, int NCH, bool PF>
+static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
+  static size_t attr_lds[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (lds > attr_lds[dev]) {
+    for (const void* f : {reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, 2, true, PF>),
+                          reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, 2, false, PF>)}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    attr_lds[dev] = lds;
+  }
+  if (p.R)
+    hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, true, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+  else
+    hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, false, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+  return hipGetLastError();
+}
+
+static bool use_res2() {
+  static const bool off = getenv("KDLAE_GEMM_RES1") != nullptr;  // A/B hook: the r01 resident kernel
+  return !off;
+}
+
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s) {
   const bool c3 = p.ksize == 3;
   const bool res = p.group_tiles > 0;
+  if (res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && use_res2()) {
+    const long long HW = (long long)p.F * p.H * p.W;
+    const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;
+    const int nch = (p.group_tiles + NT - 1) / NT;
+    const int grid_y = (p.ntiles + p.group_tiles - 1) / p.group_tiles;
+    const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64;
+    // residual variants keep NT x 2 residual float4 live across the chunk's MFMAs: only where that
+    // fits the 256-VGPR budget without spills (hipcc -Rpass-analysis), else the r01 kernel
+    const bool res_ok = !p.R || (NT * nch <= 12 && KG <= 8 && p.ldr % 4 == 0);
+    if (mx < (1LL << 31) && lds <= 160 * 1024 && p.lda % 4 == 0 && p.ldo % 4 == 0 && res_ok) {
+#define X(a, b, c, f) \
+      if (NT == a && KG == b && nch == c) return launch_res2<a, b, c, f>(p, grid_x, grid_y, lds, s);
+      KDLAE_GEMM_RES2_VARIANTS(X)
+#undef X
+    }
+  }
   if (p.out_mode == 0 && (p.N % 16)) return hipErrorInvalidValue;  // plain stores are whole 16-channel tiles
   int grid_y;
   size_t lds;

@@ -6,7 +6,7 @@ VALUBusy formula), GRBM_GUI_ACTIVE (GPU-busy cycles; rocprofv3 reports the sum o
 SQ_WAVE_CYCLES / SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY (wave-state split).
 
   MfmaUtil  = MFMA_BUSY / (GUI_ACTIVE/8 * 1024 SIMDs)          (rocprofv3 derived 'MfmaUtil')
-  VALUBusy  = 4 * ACTIVE_INST_VALU / 256 CUs / (GUI_ACTIVE/8)    (derived 'VALUBusy' with quad-cycles)
+  VALUBusy  = ACTIVE_INST_VALU / 256 CUs / (GUI_ACTIVE/8)        (rocprofv3 derived 'VALUBusy')
   clock     = GUI_ACTIVE/8 / kernel duration                      (MI355X_MICROARCH.md, DVFS give-back)
 
 usage: python tools/pmc_busy.py <counter_collection.csv> <out.json> [label]
@@ -61,7 +61,7 @@ def main():
             if "SQ_VALU_MFMA_BUSY_CYCLES" in a:
                 row["mfma_util"] = round(a["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui * 1024), 4)
             if "SQ_ACTIVE_INST_VALU" in a:
-                row["valu_busy"] = round(4 * a["SQ_ACTIVE_INST_VALU"] / 256 / gui, 4)
+                row["valu_busy"] = round(a["SQ_ACTIVE_INST_VALU"] / 256 / gui, 4)
             if a.get("seconds"):
                 row["clock_ghz"] = round(gui / a["seconds"] / 1e9, 3)
                 row["seconds"] = round(a["seconds"], 6)
