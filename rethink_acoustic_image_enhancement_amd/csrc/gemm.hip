@@ -518,6 +518,194 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Chunked schedule, r02 (deep 1x1 layers with K > the LDS budget, every implicit 3x3 / 3x3x3 conv):
+// the block walks its pixel tiles x k-chunks as one sequence of steps.  Per step:
+//   s_waitcnt vmcnt(0) + barrier   (this step's weights and A rows were issued one step earlier);
+//   issue the NEXT step's weight chunk by buffer-load-to-LDS (double-buffered slots; out-of-range
+//   records come back as zeros) and its A rows into registers (buffer loads, zero outside the image
+//   or past K, so the 3x3 zero padding needs no branch);
+//   16 x NT x KG MFMAs on this step's operands; at a tile's last k-chunk the epilogue.
+// r01's version staged each weight chunk through VGPRs behind two __syncthreads and loaded A only
+// after them, so every k-chunk exposed two memory latencies with both waves of a SIMD parked.
+template <int NT, int KG, bool CONV3, int OUT, bool HASR>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
+  constexpr int SLOT = NT * KG * 64;                  // f32x4 per weight slot
+  constexpr int PIECES = NT * KG;                     // 1 KiB records per chunk
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lq = lane >> 4;
+  const int HW = p.F * p.H * p.W;
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
+  if (t_begin >= t_end) return;
+  const int nc = blockIdx.y;
+  const int KC = p.kchunks;
+  f32x4* bias_l = wlds + 2 * SLOT;
+  for (int idx = tid; idx < NT * 4; idx += kGemmThreads) {
+    const int n = nc * NT * 16 + 4 * idx;
+    bias_l[idx] = (p.bias && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const unsigned w_bytes = (unsigned)p.ntiles * (unsigned)p.kgroups * 1024u;
+  const unsigned a_bytes = (unsigned)HW * (unsigned)p.lda * 4u;
+  // weights of step (tile, kc) -> slot; record (t, g) of the chunk = packed record (nc*NT + t, kc*KG + g)
+  auto issue_w = [&](int tile, int kc, int slot) {
+    const int b = tile / p.tiles_per_img;
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.Wp + (p.w_img_stride ? (long long)b * p.w_img_stride : 0LL)),
+                                          0, (int)w_bytes, 0x00020000);
+    f32x4* dst = wlds + slot * SLOT;
+#pragma unroll
+    for (int j = 0; j < (PIECES + 7) / 8; ++j) {
+      const int k = wave + 8 * j;
+      if (k >= PIECES) break;
+      const int t = k / KG, g = k - (k / KG) * KG;
+      const int gt = nc * NT + t, gg = kc * KG + g;
+      const unsigned off = (gt < p.ntiles && gg < p.kgroups) ? (unsigned)(gt * p.kgroups + gg) * 1024u + 16u * lane : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + 64 * k), 16, (int)off,
+                                               0, 0, 0);
+    }
+  };
+  auto load_a2 = [&](int tile, int kc, f32x4 (&dst)[kGemmRT][KG]) {
+    const int b = tile / p.tiles_per_img;
+    const int row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(p.A + (long long)b * HW * p.lda), 0, (int)a_bytes, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r) {
+      const int prow = row0 + r * 16 + li;
+      const bool pv = prow < HW;
+      if constexpr (!CONV3) {
+        const unsigned base = (unsigned)(prow * p.lda + 4 * lq) * 4u;
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+          const int gg = kc * KG + g;
+          dst[r][g] = buf_load4(ra, (pv && gg < p.kgroups) ? base + 64u * gg : kOOB);
+        }
+      } else {
+        const int fhw = p.H * p.W;
+        const int pt = prow / fhw;
+        const int rem = prow - pt * fhw;
+        const int py = rem / p.W;
+        const int px = rem - py * p.W;
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+          const int gg = kc * KG + g;
+          const int tap = gg / p.cg_per_tap;
+          const int cgi = gg - tap * p.cg_per_tap;
+          const int t9 = p.kt == 3 ? tap - (tap / 9) * 9 : tap;
+          const int tt = p.kt == 3 ? pt + tap / 9 - 1 : pt;
+          const int ty = t9 / 3;
+          const int yy = py + (ty - 1) * p.dil;
+          const int xx = px + (t9 - 3 * ty - 1) * p.dil;
+          const bool ok = pv && gg < p.kgroups && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W &&
+                          (unsigned)tt < (unsigned)p.F;
+          dst[r][g] = buf_load4(ra, ok ? (unsigned)(((tt * p.H + yy) * p.W + xx) * p.lda + cgi * 16 + 4 * lq) * 4u : kOOB);
+        }
+      }
+    }
+  };
+  // LN row statistics (mean, rstd) of the chunk's rows, precomputed by ln_stats (K is chunked)
+  // (p.stats is null when the whole LN row fits one k-chunk: then the row is normalised in registers)
+  auto load_stats = [&](int b, int row0, float2 (&st)[kGemmRT]) {
+    if (!p.stats) return;
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r) {
+      const int prow = min(row0 + r * 16 + li, HW - 1);
+      st[r] = *reinterpret_cast<const float2*>(p.stats + 2 * ((long long)b * HW + prow));
+    }
+  };
+  auto ln_apply = [&](int b, int row0, const float2 (&st)[kGemmRT], f32x4 (&x)[kGemmRT][KG]) {
+    if (!p.stats) {
+      apply_ln<KG>(p, b, row0, li, HW, x);
+      return;
+    }
+    const float wb = (p.ln == 2) ? 1.f : 0.f;
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r)
+#pragma unroll
+      for (int g = 0; g < KG; ++g) x[r][g] = (x[r][g] - st[r].x * wb) * st[r].y;
+  };
+  f32x4 a[kGemmRT][KG], an[kGemmRT][KG];
+  f32x4 acc[NT][kGemmRT];
+  issue_w(t_begin, 0, 0);
+  load_a2(t_begin, 0, an);
+  int slot = 0;
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int b = tile / p.tiles_per_img;
+    const int row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // one step: wait + barrier, operands of step (ntile, nkc) in flight, MFMAs of this step
+    auto begin_step = [&]() {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r)
+#pragma unroll
+        for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
+    };
+    float2 st[kGemmRT];
+    for (int kc = 0; kc + 1 < KC; ++kc) {
+      begin_step();
+      if (p.ln) load_stats(b, row0, st);
+      issue_w(tile, kc + 1, slot ^ 1);
+      load_a2(tile, kc + 1, an);
+      if (p.ln) ln_apply(b, row0, st, a);
+      mfma_chunk<NT, KG>(wlds + slot * SLOT, KG, lane, a, acc);
+      slot ^= 1;
+    }
+    // last k-chunk: residual loads, then the next tile's first operands (clamped, so the count of
+    // memory ops is the same on every path), MFMAs, epilogue
+    begin_step();
+    if (p.ln) load_stats(b, row0, st);
+    [[maybe_unused]] f32x4 res[NT][kGemmRT];
+    if constexpr (HASR && OUT == 0) {
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(p.R + (long long)b * HW * p.ldr), 0, (int)((unsigned)HW * (unsigned)p.ldr * 4u), 0x00020000);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int nq = (nc * NT + t) * 16 + 4 * lq;
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) {
+          const int pl = row0 + r * 16 + li;
+          res[t][r] = buf_load4(rr, (pl < HW && nq < p.N) ? (unsigned)(pl * p.ldr + nq) * 4u : kOOB);
+        }
+      }
+    }
+    const int ntile = min(tile + 1, t_end - 1);
+    issue_w(ntile, 0, slot ^ 1);
+    load_a2(ntile, 0, an);
+    if (p.ln) ln_apply(b, row0, st, a);
+    mfma_chunk<NT, KG>(wlds + slot * SLOT, KG, lane, a, acc);
+    slot ^= 1;
+    if constexpr (OUT == 0) {
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          p.out + (long long)b * HW * p.ldo, 0, (int)((unsigned)HW * (unsigned)p.ldo * 4u), 0x00020000);
+      const float relu_floor = p.relu ? 0.f : -__builtin_huge_valf();
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int nq = (nc * NT + t) * 16 + 4 * lq;
+        const f32x4 bias = bias_l[4 * t + lq];
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) {
+          const int pl = row0 + r * 16 + li;
+          f32x4 v = acc[t][r] + bias;
+          if constexpr (HASR) v += res[t][r];
+          v = f32x4{fmaxf(v.x, relu_floor), fmaxf(v.y, relu_floor), fmaxf(v.z, relu_floor), fmaxf(v.w, relu_floor)};
+          buf_store4(ro, (pl < HW && nq < p.N) ? (unsigned)(pl * p.ldo + nq) * 4u : kOOB, v);
+        }
+      }
+    } else {
+      epilogue<NT, OUT, HASR>(p, b, row0, nc * NT, NT, li, lq, HW, acc, bias_l);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped last prefetch lands before exit
+}
+
 // (NT, KG, CONV3, OUT, PF, WPE, RES).  Resident variants need KG == kgroups exactly.
 #define KDLAE_GEMM_VARIANTS(X) \
   X(9, 3, false, 0, true, 2, true) X(8, 3, false, 0, true, 2, true) X(3, 3, false, 0, true, 2, true) \
@@ -594,6 +782,55 @@ static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_
   return hipGetLastError();
 }
 
+// (NT, KG, CONV3, OUT) of the r02 chunked kernel: two weight slots of NT x KG KiB must fit the LDS
+// (only shapes whose A double buffer + accumulators fit 256 VGPRs without spills: NT x KG <= ~64)
+#define KDLAE_GEMM_CHUNK2_VARIANTS(X) \
+  X(3, 3, false, 0) X(6, 6, false, 0) X(8, 8, false, 0) X(12, 4, false, 0) X(1, 3, false, 0) X(3, 4, false, 0) \
+  X(3, 3, true, 1) X(3, 6, true, 1) X(6, 6, true, 1) X(2, 6, true, 1) X(8, 6, true, 1) \
+  X(3, 3, true, 2) X(3, 6, true, 2) X(6, 6, true, 2) X(2, 6, true, 2) X(8, 6, true, 2) \
+  X(1, 9, true, 0) X(2, 9, true, 0) X(4, 9, true, 0) X(8, 6, true, 0) X(4, 6, true, 0) X(2, 6, true, 0) \
+  X(4, 4, false, 2) X(8, 4, false, 2) X(4, 2, false, 2) X(3, 3, false, 2)
+
+bool gemm_chunk2_enabled() {
+  static const bool off = getenv("KDLAE_GEMM_CHUNK1") != nullptr;  // A/B hook: the r01 chunked kernel
+  return !off;
+}
+
+bool gemm_has_variant2(int NT, int KG, bool conv3, int out_mode) {
+#define X(a, b, c, o) \
+  if (NT == a && KG == b && conv3 == c && out_mode == o) return true;
+  KDLAE_GEMM_CHUNK2_VARIANTS(X)
+#undef X
+  return false;
+}
+
+template <int NT, int KG, bool C3, int OUT>
+static hipError_t launch_chunk2(const GemmParams& p, int grid_x, int grid_y, hipStream_t s) {
+  const size_t lds = (size_t)2 * NT * KG * 1024 + (size_t)NT * 64;
+  static size_t attr_lds[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  constexpr bool R0 = (OUT == 0 && !C3 && NT * KG <= 36);  // residual variants without spills
+  if (lds > attr_lds[dev]) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_chunk_kernel<NT, KG, C3, OUT, false>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if (R0) {
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_chunk_kernel<NT, KG, C3, OUT, R0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    attr_lds[dev] = lds;
+  }
+  if (R0 && p.R)
+    hipLaunchKernelGGL((gemm_chunk_kernel<NT, KG, C3, OUT, R0>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+  else if (OUT == 0 && p.R)
+    return hipErrorInvalidValue;  // (no residual variant: the host picks another NT x KG)
+  else
+    hipLaunchKernelGGL((gemm_chunk_kernel<NT, KG, C3, OUT, false>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+  return hipGetLastError();
+}
+
 static bool use_res2() {
   static const bool off = getenv("KDLAE_GEMM_RES1") != nullptr;  // A/B hook: the r01 resident kernel
   return !off;
@@ -602,6 +839,7 @@ static bool use_res2() {
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s) {
   const bool c3 = p.ksize == 3;
   const bool res = p.group_tiles > 0;
+  if (p.ln && !p.stats && (p.kchunks > 1 || p.kgroups > KG)) return hipErrorInvalidValue;  // LN needs whole rows
   if (res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && use_res2()) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;
@@ -632,6 +870,18 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
     lds = (size_t)NT * KG * 1024 + (size_t)NT * 64;
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (!res && gemm_chunk2_enabled() && gemm_has_variant2(NT, KG, c3, p.out_mode) && p.lda % 4 == 0) {
+    const long long HW = (long long)p.F * p.H * p.W;
+    const long long osz = p.out_mode == 2 ? 4 * HW : (p.out_mode == 1 ? HW / 4 : HW);
+    const bool fits = HW * p.lda * 4 < (1LL << 31) && osz * p.ldo * 4 < (1LL << 31) &&
+                      (!p.R || osz * p.ldr * 4 < (1LL << 31)) && (long long)p.ntiles * p.kgroups * 1024 < (1LL << 31);
+    if (fits) {
+#define X(a, b, c, o) \
+      if (NT == a && KG == b && c3 == c && p.out_mode == o) return launch_chunk2<a, b, c, o>(p, grid_x, grid_y, s);
+      KDLAE_GEMM_CHUNK2_VARIANTS(X)
+#undef X
+    }
+  }
 #define X(a, b, c, o, f, w, r)                                                                 \
   if (NT == a && KG == b && c3 == c && p.out_mode == o && wpe == w && res == r)                \
     return launch_variant<a, b, c, o, f, w, r>(p, grid_x, grid_y, lds, s);

@@ -31,6 +31,7 @@ struct BlockW {
   size_t dwqkv = kNone, dwqkv_b = kNone, proj = kNone, proj_b = kNone, temp = kNone;
   size_t dwffn = kNone, dwffn_b = kNone;
   bool fused_gdfn = false;  // project_in output chunk-interleaved; dwconv+gate+project_out in one kernel
+  bool fused_ffn = false;   // the whole FFN (LN + project_in + dwconv + gate + project_out) in one kernel
 };
 
 }  // namespace kdlae
@@ -291,6 +292,7 @@ struct Packer {
     b.proj_gemm.n_true = C;
     b.proj_gemm.k_true = C;
     b.proj_gemm.bias = b.proj_b;
+    b.proj_gemm.has_res = true;
     choose_variant(b.proj_gemm, true);
     // FFN: project_in rows [x1 (hid) | x2 (hid)].  Unfused: stored [x1 padded to hidS | x2 padded
     // to hidS] for the gate kernel.  Fused (gdfn.hip): chunk-interleaved, 16 channels of x1 then the
@@ -331,6 +333,10 @@ struct Packer {
       if (fb >= 0) b.dwffn_b = prog.add(vb);
     }
     b.pout = pointwise(p + ".ffn.project_out", C, hid, hidS, C, [](int n) { return n; }, "", c.bias, false);
+    b.pout.has_res = true;  // x += project_out(...) (unfused path)
+    choose_variant(b.pout, false);
+    // opt-in (KDLAE_FFN_FUSION=1): measured 1.8x slower than project_in GEMM + gdfn_out in r02 v1
+    b.fused_ffn = fz && ffn_fused_supported(C, hidS) && getenv("KDLAE_FFN_FUSION") != nullptr;
     return b;
   }
 
@@ -493,8 +499,11 @@ struct Fwd {
     return probe_end(1, probeC, bytes, 2.0 * P * g.n_true * g.k_true);
   }
 
-  int block(const BlockW& b, View x, int Hh, int Ww) {
+  // One TransformerBlock in place on x, except that with the fully fused FFN (ffn.hip) the block's
+  // output lands in `alt` (*swapped = true): the FFN reads x's 3x3 halo, so it cannot write x.
+  int block(const BlockW& b, View x, View alt, bool* swapped, int Hh, int Ww) {
     const int HW = Hh * Ww;
+    *swapped = false;
     const int ln = h->cfg.layernorm_biasfree ? 1 : 2;
     const long long P = (long long)B * HW;
     int rc;
@@ -530,6 +539,31 @@ struct Fwd {
               0, b.C);
     if (rc) return rc;
     // --- feed-forward
+    if (b.fused_ffn && alt.p) {
+      FfnParams fp{};
+      fp.x = x.p;
+      fp.ldx = x.ld;
+      fp.y = alt.p;
+      fp.ldy = alt.ld;
+      fp.Win = h->P(b.pin.w);
+      fp.bin = h->P(b.pin.bias);
+      fp.dw = h->P(b.dwffn);
+      fp.Wout = h->P(b.pout.w);
+      fp.bout = h->P(b.pout.bias);
+      fp.C = b.C;
+      fp.hidS = b.hidS;
+      fp.ln = ln;
+      fp.Bn = B;
+      fp.H = Hh;
+      fp.W = Ww;
+      if ((rc = probe_begin(3, b.C))) return rc;
+      tag = "ffn C" + std::to_string(b.C) + " hid" + std::to_string(b.hid) + " HW" + std::to_string(HW);
+      HIPCHK(launch_ffn_fused(fp, s));
+      *swapped = true;
+      // algorithmic: read x (+ its residual use) and write y; every FFN FLOP (SURVEY 8d model)
+      return probe_end(3, b.C, 4.0 * P * 3.0 * b.C,
+                       2.0 * P * (2.0 * b.hid * b.C + 18.0 * b.hid + (double)b.hid * b.C));
+    }
     View fpre{buf(pl.fpre), 2 * b.hidS};
     rc = gemm(b.pin, h->P(b.pin.w), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
     if (rc) return rc;
@@ -574,11 +608,22 @@ struct Fwd {
     return gemm(b.pout, h->P(b.pout.w), 0, View{buf(pl.fg), b.hidS}, Hh, Ww, x, 0, x.p, x.ld, 0, 0, b.C);
   }
 
+  // Blocks of a stage ping-pong between x and a dense scratch view (the unfused FFN's pre-gate
+  // buffer, free when the FFN is fused) whenever the fused FFN runs; an odd number of swaps ends
+  // with one strided copy back into x.
   int stage(const std::vector<BlockW>& st, View x, int Hh, int Ww) {
+    View cur = x;
+    View alt{nullptr, 0};
     for (const BlockW& b : st) {
-      int rc = block(b, x, Hh, Ww);
+      View other = alt;
+      if (b.fused_ffn) other = (cur.p == x.p) ? View{buf(pl.fpre), b.C} : x;
+      bool swapped = false;
+      int rc = block(b, cur, other, &swapped, Hh, Ww);
       if (rc) return rc;
+      if (swapped) cur = other;
     }
+    if (cur.p != x.p && !st.empty())
+      HIPCHK(launch_copy_view(cur.p, cur.ld, x.p, x.ld, st[0].C, (long long)B * Hh * Ww, s));
     return KDLAE_OK;
   }
 

@@ -31,7 +31,7 @@ static int forced_wpe() {
 
 void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
   static const int nts[] = {1, 2, 3, 4, 6, 8, 9, 12};
-  static const int kgs[] = {2, 3, 4, 6, 8, 9, 12, 16};
+  static const int kgs[] = {2, 3, 4, 6, 8, 9, 12, 16};  // (12 x 8 and wider only on the r01 chunked kernel)
   g.group_tiles = 0;
   g.WPE = 2;
   if (g.ksize == 1) {
@@ -72,9 +72,12 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
     }
   }
   double best = 1e30;
+  const bool v2 = gemm_chunk2_enabled();
   for (int nt : nts)
     for (int kg : kgs) {
-      if (!gemm_has_variant(nt, kg, g.ksize == 3, 2, false, g.out_mode)) continue;
+      if (v2 ? !gemm_has_variant2(nt, kg, g.ksize == 3, g.out_mode) || (g.has_res && nt * kg > 36)
+             : !gemm_has_variant(nt, kg, g.ksize == 3, 2, false, g.out_mode))
+        continue;
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
       // every k-chunk restages weights behind two barriers; every n-chunk re-reads A.

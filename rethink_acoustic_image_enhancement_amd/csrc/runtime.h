@@ -35,6 +35,7 @@ struct Gemm {
   int out_mode = 0;  // store map the variant must support (0 plain, 1 unshuffle, 2 shuffle)
   int NT = 0, KG = 0, group_tiles = 0, WPE = 2;
   int n_true = 0, k_true = 0;  // un-padded sizes (FLOP accounting)
+  bool has_res = false;         // launched with a residual epilogue (variant choice)
 };
 struct SmallW {
   size_t w = kNone, bias = kNone;
