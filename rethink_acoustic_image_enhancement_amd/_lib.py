@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkdlae.so")
+# KDLAE_LIB overrides the library (kernel A/B builds under tools/); default: the in-tree build
+LIB_PATH = os.environ.get("KDLAE_LIB") or os.path.join(_HERE, "libkdlae.so")
 
 c_int, c_int64, c_double, c_void_p, c_char_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_double,
                                                 ctypes.c_void_p, ctypes.c_char_p)

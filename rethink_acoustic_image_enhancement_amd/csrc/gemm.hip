@@ -398,7 +398,7 @@ template <int NT, int KG, int NCH, int WPE, bool HASR, bool PF>
 __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lq = lane >> 4;
   const int HW = p.F * p.H * p.W;
   const int t_begin = blockIdx.x * p.tiles_per_block;
@@ -423,16 +423,18 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
   int staged = p.w_img_stride ? t_begin / p.tiles_per_img : 0;
   stage(staged);
   __syncthreads();
-  const float relu_floor = p.relu ? 0.f : -__builtin_huge_valf();
   const unsigned a_bytes = (unsigned)HW * (unsigned)p.lda * 4u;
   const unsigned o_bytes = (unsigned)HW * (unsigned)p.ldo * 4u;
   const unsigned r_bytes = (unsigned)HW * (unsigned)p.ldr * 4u;
-  // per-lane channel byte offset of staged tile t (kOOB past N / past the group)
-  auto ch_off = [&](int t) -> unsigned {
-    const int nq = (g0 + t) * 16 + 4 * lq;
-    return (t < gtiles && nq < p.N) ? (unsigned)nq * 4u : kOOB;
-  };
-  auto rows_of = [&](int tile, int& b, int& row0) {
+  // Output / residual addresses: voffset = the lane's pixel row + the group's first channel + its
+  // channel quad (computed once per tile; the buffer size for rows past the image), plus t * 64 for
+  // staged tile t, a constant hipcc folds into the instruction's offset field.  Padding tiles of a
+  // partial group select the buffer size (a block-uniform v_cndmask), so the range check drops them.
+  // soffset stays 0: with an SGPR soffset hipcc stops padding the store-data hazard of the x4
+  // stores it emits (the data VGPRs were rewritten right after issue: wrong outputs on the GPU).
+  auto tile_voff = [&](int t, unsigned v, unsigned bytes) -> int {
+    return (int)(((t < gtiles) ? v : bytes) + 64u * (unsigned)t);
+  };  auto rows_of = [&](int tile, int& b, int& row0) {
     b = tile / p.tiles_per_img;
     row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
   };
@@ -473,12 +475,12 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
     [[maybe_unused]] __amdgpu_buffer_rsrc_t rr;
     if constexpr (HASR) rr = buf_rsrc(p.R + (long long)b * HW * p.ldr, r_bytes);
-    unsigned pix_o[kGemmRT], pix_r[kGemmRT];
+    unsigned vo[kGemmRT], vr[kGemmRT];
 #pragma unroll
     for (int r = 0; r < kGemmRT; ++r) {
       const unsigned pix = (unsigned)(row0 + r * 16 + li);
-      pix_o[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldo * 4u : kOOB;
-      pix_r[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldr * 4u : kOOB;
+      vo[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldo * 4u + 16u * lq + 64u * g0 : o_bytes;
+      vr[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldr * 4u + 16u * lq + 64u * g0 : r_bytes;
     }
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
@@ -487,10 +489,9 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int r = 0; r < kGemmRT; ++r) {
-            const unsigned c = ch_off(ch * NT + t);
-            res[t][r] = buf_load4(rr, ((pix_r[r] | c) & kOOB) ? kOOB : pix_r[r] + c);
-          }
+          for (int r = 0; r < kGemmRT; ++r)
+            res[t][r] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, tile_voff(ch * NT + t, vr[r], r_bytes), 0, 0));
       }
       f32x4 acc[NT][kGemmRT];
 #pragma unroll
@@ -498,6 +499,8 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
       mfma_chunk<NT, KG>(wlds + (size_t)ch * NT * KG * 64, KG, lane, a, acc);
+      // bias after the K sum, as every other GEMM schedule does: a pixel's result must not depend
+      // on which schedule (batch size) produced it
       const f32x4* bl = wlds + TP * KG * 64 + ch * NT * 4;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -506,11 +509,8 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
         for (int r = 0; r < kGemmRT; ++r) {
           f32x4 v = acc[t][r] + bias;
           if constexpr (HASR) v += res[t][r];
-          v = f32x4{fmaxf(v.x, relu_floor), fmaxf(v.y, relu_floor), fmaxf(v.z, relu_floor), fmaxf(v.w, relu_floor)};
-          // pix | ch: both are byte offsets; an out-of-range half sets bit 31 -> dropped
-          const unsigned c = ch_off(ch * NT + t);
-          const unsigned off = ((pix_o[r] | c) & kOOB) ? kOOB : pix_o[r] + c;
-          buf_store4(ro, off, v);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro, tile_voff(ch * NT + t, vo[r], o_bytes),
+                                                 0, 0);
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
@@ -840,7 +840,7 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
   const bool c3 = p.ksize == 3;
   const bool res = p.group_tiles > 0;
   if (p.ln && !p.stats && (p.kchunks > 1 || p.kgroups > KG)) return hipErrorInvalidValue;  // LN needs whole rows
-  if (res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && use_res2()) {
+  if (res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && !p.relu && use_res2()) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;
     const int nch = (p.group_tiles + NT - 1) / NT;
@@ -848,7 +848,7 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
     const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64;
     // residual variants keep NT x 2 residual float4 live across the chunk's MFMAs: only where that
     // fits the 256-VGPR budget without spills (hipcc -Rpass-analysis), else the r01 kernel
-    const bool res_ok = !p.R || (NT * nch <= 12 && KG <= 8 && p.ldr % 4 == 0);
+    const bool res_ok = !p.R || (NT * nch <= 12 && NT * nch * KG <= 72 && KG <= 8 && p.ldr % 4 == 0);  // no VGPR spills
     if (mx < (1LL << 31) && lds <= 160 * 1024 && p.lda % 4 == 0 && p.ldo % 4 == 0 && res_ok) {
 #define X(a, b, c, f) \
       if (NT == a && KG == b && nch == c) return launch_res2<a, b, c, f>(p, grid_x, grid_y, lds, s);
