@@ -29,7 +29,10 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include <algorithm>
+
 #include "kernels.h"
+#include "runtime.h"
 
 namespace kdlae {
 
@@ -75,6 +78,9 @@ __device__ __forceinline__ float gelu_erf_g(float x) {
   const float e = 1.0f - poly * __expf(-z * z);     // erf(|x| / sqrt 2)
   return 0.5f * x * (1.0f + copysignf(e, x));
 }
+
+typedef unsigned u32x4g __attribute__((ext_vector_type(4)));
+constexpr unsigned kOOB2 = 0x80000000u;  // a byte offset past every descriptor's range
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -301,15 +307,264 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// r02 schedule ("gdfn2"): no LDS halo, no per-chunk barrier.  A persistent grid of one 4-wave
+// block per CU; after one barrier that stages every chunk's project_out W fragments and dw block
+// in LDS (C = 96: 96 + 20 KiB), each WAVE runs on its own: it owns strips of 16 columns x R rows and,
+// per hidden chunk g, walks the strip's R + 2 input rows top to bottom:
+//   * the three column-shifted 16-pixel rows of x1 and x2 (6 buffer loads, 16 B per lane; rows and
+//     columns outside the image fall outside the descriptor and load zeros = the conv's padding)
+//     are prefetched two input rows ahead, straight into VGPRs (the shifted loads hit the L1/L2
+//     lines of the centre load, so HBM sees each 128 B pixel line about once);
+//   * input row k adds its 3 x 3 taps into the running depthwise sums of output rows k-2..k;
+//   * output row r is complete after input row r+2, gated at r+3 and multiplied (24 MFMAs for
+//     C = 96) at r+4, so the stencil VALU of one row, the gate of the row before and the MFMAs of
+//     the row before that are independent instruction streams the scheduler interleaves.  The
+//     last two rows' gate/MFMA are carried into the next chunk's first two input rows.
+// One wave per SIMD with up to 512 VGPRs: the accumulators of the strip (R x C/16 float4), the
+// three prefetched rows and the chunk's dw weights stay in registers.  r01's kernel spent about a
+// third of its wave cycles parked on the per-chunk barrier / DMA waits (profiles/r02_pmc_*).
+template <int CTRL>
+__device__ __forceinline__ f32x4 dpp4(const f32x4& old, const f32x4& v) {
+  f32x4 r;
+  r.x = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old.x), __builtin_bit_cast(int, v.x), CTRL, 0xf, 0xf, false));
+  r.y = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old.y), __builtin_bit_cast(int, v.y), CTRL, 0xf, 0xf, false));
+  r.z = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old.z), __builtin_bit_cast(int, v.z), CTRL, 0xf, 0xf, false));
+  r.w = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old.w), __builtin_bit_cast(int, v.w), CTRL, 0xf, 0xf, false));
+  return r;
+}
+
+template <int NT, int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gdfn2_kernel(GdfnParams p, int nunits) {
+  constexpr int K = R + 2;  // input rows per strip and chunk
+  static_assert(K % 3 == 0, "the 3 prefetch slots must line up at chunk boundaries");
+  extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+  const int kch = p.hidS >> 4;
+  f32x4* wl = lds;                          // [kch][NT][64] project_out fragments, chunk-major
+  f32x4* dl = lds + kch * NT * 64;          // [kch][80]     dw taps [9][8] + bias [8]
+  {
+    const f32x4* Wf = reinterpret_cast<const f32x4*>(p.Wp);  // [NT][kch][64]
+    const f32x4* Dw = reinterpret_cast<const f32x4*>(p.dw);  // [kch][128]
+    for (int i = threadIdx.x; i < kch * NT * 64; i += 256) {
+      const int g = i / (NT * 64), rem = i - g * (NT * 64);
+      wl[i] = Wf[((size_t)(rem >> 6) * kch + g) * 64 + (rem & 63)];
+    }
+    for (int i = threadIdx.x; i < kch * 80; i += 256) {
+      const int g = i / 80;
+      dl[i] = Dw[(size_t)g * 128 + (i - g * 80)];
+    }
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, lq = lane >> 4;
+  const int sx_n = (p.W + 15) >> 4, sy_n = (p.H + R - 1) / R;
+  // XCD-aware split: XCD k (blocks k, k+8, ...) takes a contiguous range of strips, so the strips
+  // whose halos overlap run at the same time under one L2
+  const int per_xcd = (nunits + 7) >> 3;
+  const int u_begin = (int)(blockIdx.x & 7) * per_xcd;
+  const int u_end = min(u_begin + per_xcd, nunits);
+  const int wstride = (int)(gridDim.x >> 3) * 4;
+  const unsigned row_bytes = (unsigned)p.W * (unsigned)p.ld * 4u;
+  const unsigned img_bytes = (unsigned)p.H * row_bytes;
+  constexpr unsigned kFar = 0x40000000u;  // row or column offset outside the image (img_bytes <= 2^30)
+
+  for (int u = u_begin + (int)(blockIdx.x >> 3) * 4 + wave; u < u_end; u += wstride) {
+    const int sc = u % sx_n, t2 = u / sx_n;
+    const int sr = t2 % sy_n, b = t2 / sy_n;
+    const int x0 = sc * 16, y0 = sr * R;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(p.x + (long long)b * p.H * p.W * p.ld), 0, (int)img_bytes, 0x00020000);
+    // centre column (lane li <-> column x0+li) and the two edge columns (lane 0 <-> x0-1,
+    // lane 15 <-> x0+16; the other lanes' edge offsets fall outside the descriptor)
+    const int xc = x0 + li, xe = li == 0 ? x0 - 1 : (li == 15 ? x0 + 16 : -1);
+    const unsigned ccoff = ((unsigned)xc < (unsigned)p.W ? (unsigned)xc * (unsigned)p.ld * 4u : kFar) + 16u * lq;
+    const unsigned ecoff = ((unsigned)xe < (unsigned)p.W ? (unsigned)xe * (unsigned)p.ld * 4u : kFar) + 16u * lq;
+    // input row k (0..K-1 <-> image row y0-1+k) of chunk g: x1 (h=0) and x2 (h=1), centre and edge
+    auto load_row = [&](int g, int k, f32x4 (&dst)[2][2]) {
+      const int yy = y0 - 1 + k;
+      const unsigned so = ((unsigned)yy < (unsigned)p.H ? (unsigned)yy * row_bytes : kFar) + 128u * (unsigned)g;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        dst[h][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(ccoff + so + 64u * h), 0, 0));
+        dst[h][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(ecoff + so + 64u * h), 0, 0));
+      }
+    };
+    f32x4 acc[R][NT];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 xs[3][2][2];
+    load_row(0, 0, xs[0]);
+    load_row(0, 1, xs[1]);
+    // carried from the previous chunk: the depthwise sums of row R-1 (not yet gated) and the gated
+    // row R-2 (not yet multiplied); zeros before chunk 0, so the carried MFMAs add nothing
+    f32x4 dpend[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 gpend = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto gate4 = [](const f32x4& a, const f32x4& v) {
+      return f32x4{gelu_erf_g(a.x) * v.x, gelu_erf_g(a.y) * v.y, gelu_erf_g(a.z) * v.z, gelu_erf_g(a.w) * v.w};
+    };
+    auto mfma_row = [&](const f32x4 (&wf)[NT], const f32x4& gb, f32x4 (&ac)[NT]) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ac[t] = mfma4(wf[t][e], gb[e], ac[t]);
+    };
+    for (int g = 0; g < kch; ++g) {
+      const f32x4* dwl = dl + g * 80;
+      f32x4 wdw[9][2], bdw[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bdw[h] = dwl[72 + 4 * h + lq];
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) wdw[tap][h] = dwl[tap * 8 + 4 * h + lq];
+      }
+      f32x4 wf[NT], wfp[NT];
+      const int gp = g > 0 ? g - 1 : 0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        wf[t] = wl[(g * NT + t) * 64 + lane];
+        wfp[t] = wl[(gp * NT + t) * 64 + lane];
+      }
+      f32x4 d[R][2];      // depthwise sums per output row (only a window of 3 is live)
+      f32x4 gb[R];        // gated rows
+      f32x4 gq;           // gated carried row R-1
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        // prefetch input row k+2 (of this chunk, or row 0/1 of the next; the last chunk re-reads)
+        if (k + 2 < K) load_row(g, k + 2, xs[(k + 2) % 3]);
+        else load_row(g + 1 < kch ? g + 1 : g, k + 2 - K, xs[(k + 2) % 3]);
+        // column neighbours by DPP within each 16-lane row (= one channel quad): row_shr:1 gives
+        // lane i the value of lane i-1, lane 0 keeps the edge load (column x0-1); row_shl:1 alike
+        f32x4 v[2][3];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          v[h][1] = xs[k % 3][h][0];
+          v[h][0] = dpp4<0x111>(xs[k % 3][h][1], v[h][1]);
+          v[h][2] = dpp4<0x101>(xs[k % 3][h][1], v[h][1]);
+        }
+        // stencil: input row k -> output rows k - i (tap row i)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int r = k - i;
+          if (r < 0 || r >= R) continue;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f32x4 s = (i == 0) ? bdw[h] : d[r][h];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const f32x4 w = wdw[3 * i + c][h];
+              s.x = fmaf(v[h][c].x, w.x, s.x);
+              s.y = fmaf(v[h][c].y, w.y, s.y);
+              s.z = fmaf(v[h][c].z, w.z, s.z);
+              s.w = fmaf(v[h][c].w, w.w, s.w);
+            }
+            d[r][h] = s;
+          }
+        }
+        // the previous chunk's last rows
+        if (k == 0) {
+          gq = gate4(dpend[0], dpend[1]);
+          mfma_row(wfp, gpend, acc[R - 2]);
+        }
+        if (k == 1) mfma_row(wfp, gq, acc[R - 1]);
+        // this chunk: gate row k-3, multiply row k-4
+        if (k - 3 >= 0 && k - 3 < R) gb[k - 3] = gate4(d[k - 3][0], d[k - 3][1]);
+        if (k - 4 >= 0 && k - 4 < R) mfma_row(wf, gb[k - 4], acc[k - 4]);
+      }
+      dpend[0] = d[R - 1][0];
+      dpend[1] = d[R - 1][1];
+      gpend = gb[R - 2];
+    }
+    {  // drain the last chunk's carried rows
+      const int gl = kch - 1;
+      f32x4 wf[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) wf[t] = wl[(gl * NT + t) * 64 + lane];
+      const f32x4 gq = gate4(dpend[0], dpend[1]);
+      mfma_row(wf, gpend, acc[R - 2]);
+      mfma_row(wf, gq, acc[R - 1]);
+    }
+    // epilogue: every residual (and the bias) loaded before the first store (vmcnt retires in order)
+    const int xo = x0 + li;
+    const unsigned o_bytes = (unsigned)p.H * (unsigned)p.W * (unsigned)p.ldo * 4u;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        p.out + (long long)b * p.H * p.W * p.ldo, 0, (int)o_bytes, 0x00020000);
+    f32x4 bias[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      bias[t] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + 16 * t + 4 * lq) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (p.R) {
+      const unsigned r_bytes = (unsigned)p.H * (unsigned)p.W * (unsigned)p.ldr * 4u;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(p.R + (long long)b * p.H * p.W * p.ldr), 0, (int)r_bytes, 0x00020000);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int yo = y0 + r;
+        const unsigned off = (yo < p.H && xo < p.W) ? ((unsigned)(yo * p.W + xo) * (unsigned)p.ldr + 4u * lq) * 4u : kOOB2;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[r][t] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(off + 64u * t), 0, 0));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int yo = y0 + r;
+      const unsigned off = (yo < p.H && xo < p.W) ? ((unsigned)(yo * p.W + xo) * (unsigned)p.ldo + 4u * lq) * 4u : kOOB2;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4g, acc[r][t] + bias[t]), ro, (int)(off + 64u * t), 0, 0);
+    }
+  }
+}
+
 bool gdfn_supported(int C, int hidS) {
   return (C == 48 || C == 96) && hidS % 16 == 0 && hidS <= 256;
 }
 
 size_t gdfn_lds_bytes(int C) { return (size_t)(kNStage * kStageSlot + kNW * 64 * (C / 16)) * sizeof(f32x4); }
 
+template <int NT, int R>
+static hipError_t launch_gdfn2(const GdfnParams& p, hipStream_t s) {
+  static size_t attr[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  const int kch = p.hidS / 16;
+  const size_t lds = (size_t)kch * (NT * 64 + 80) * sizeof(f32x4);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > attr[dev]) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gdfn2_kernel<NT, R>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr[dev] = lds;
+  }
+  const long long units = (long long)p.Bn * ((p.H + R - 1) / R) * ((p.W + 15) / 16);
+  if (units >= (1LL << 31)) return hipErrorInvalidValue;
+  const int grid = std::max(8, device_cu_count() / 8 * 8);  // persistent: one block per CU
+  hipLaunchKernelGGL((gdfn2_kernel<NT, R>), dim3((unsigned)grid), dim3(256), lds, s, p, (int)units);
+  return hipGetLastError();
+}
+
+// gdfn2 needs each image's x (and out / residual) under 2^30 bytes (offset sentinels) and W/dw in LDS
+static bool gdfn2_ok(const GdfnParams& p, int C) {
+  const long long hw = (long long)p.H * p.W;
+  static const bool on = getenv("KDLAE_GDFN2") != nullptr;  // opt-in until it beats r01's kernel
+  return on && hw * p.ld * 4 <= (1LL << 30) && hw * p.ldo * 4 < (1LL << 31) &&
+         (!p.R || hw * p.ldr * 4 < (1LL << 31)) && (size_t)(p.hidS / 16) * ((C / 16) * 64 + 80) * 16 <= 160 * 1024;
+}
+
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
   if (!gdfn_supported(C, p.hidS) || p.ld != 2 * p.hidS || p.ldo % 4 || (p.R && p.ldr % 4) || !p.zeros)
     return hipErrorInvalidValue;
+  if (gdfn2_ok(p, C)) {
+    static const int rows = getenv("KDLAE_GDFN2_ROWS") ? atoi(getenv("KDLAE_GDFN2_ROWS")) : 7;
+    if (C == 96) return launch_gdfn2<6, 4>(p, s);  // R = 7 spills at NT = 6
+    return rows == 4 ? launch_gdfn2<3, 4>(p, s) : rows == 10 ? launch_gdfn2<3, 10>(p, s) : launch_gdfn2<3, 7>(p, s);
+  }
   const long long tiles = (long long)p.Bn * ((p.H + kTile - 1) / kTile) * ((p.W + kTile - 1) / kTile);
   const long long grid = (tiles + 7) / 8 * 8;
   const size_t lds = gdfn_lds_bytes(C);

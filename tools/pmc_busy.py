@@ -8,6 +8,11 @@ SQ_WAVE_CYCLES / SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY (wave-state
   MfmaUtil  = MFMA_BUSY / (GUI_ACTIVE/8 * 1024 SIMDs)          (rocprofv3 derived 'MfmaUtil')
   VALUBusy  = ACTIVE_INST_VALU / 256 CUs / (GUI_ACTIVE/8)        (rocprofv3 derived 'VALUBusy')
   clock     = GUI_ACTIVE/8 / kernel duration                      (MI355X_MICROARCH.md, DVFS give-back)
+  LDS pass (optional): lds_idx_active_per_cu_cycle = SQ_LDS_IDX_ACTIVE / 256 / (GUI_ACTIVE/8),
+  lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, wait_inst_lds_frac = SQ_WAIT_INST_LDS /
+  SQ_WAVE_CYCLES (issue stalls on the LDS queue), lds_insts = SQ_INSTS_LDS
+  memory pass (optional): ta_busy_per_cu = TA_TA_BUSY_sum / 256 / (GUI_ACTIVE/8), l2_hit_rate = TCC_HIT / (HIT + MISS),
+  sq_inst_level_vmem_frac = SQ_INST_LEVEL_VMEM / SQ_WAVE_CYCLES (average VMEM instructions in flight per wave)
 
 usage: python tools/pmc_busy.py <counter_collection.csv> <out.json> [label]
 """
@@ -17,8 +22,11 @@ import json
 import sys
 
 CLASSES = [("conv_gemm_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
+           ("gemm_res_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
+           ("gemm_chunk_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
            ("dwconv_gram", "dwconv_gram (MDTA pass 1: dwconv + MFMA Gram)"),
            ("gdfn_out_kernel", "gdfn_out (fused GDFN tail: dwconv + gate + MFMA project_out)"),
+           ("gdfn2_kernel", "gdfn_out (fused GDFN tail: dwconv + gate + MFMA project_out)"),
            ("dwconv_gate_kernel", "dwconv_gate (unfused GDFN gate, C >= 192)"),
            ("conv_small", "conv_small (stem / head convs)"),
            ("mfma_loop", "mfma_peak micro (bare MFMA loop)")]
@@ -65,9 +73,17 @@ def main():
             if a.get("seconds"):
                 row["clock_ghz"] = round(gui / a["seconds"] / 1e9, 3)
                 row["seconds"] = round(a["seconds"], 6)
+            if "SQ_LDS_IDX_ACTIVE" in a:
+                row["lds_idx_active_per_cu_cycle"] = round(a["SQ_LDS_IDX_ACTIVE"] / 256 / gui, 4)
+                if a["SQ_LDS_IDX_ACTIVE"]:
+                    row["lds_bank_conflict_frac"] = round(a.get("SQ_LDS_BANK_CONFLICT", 0.0) / a["SQ_LDS_IDX_ACTIVE"], 4)
+            if "TA_TA_BUSY_sum" in a:
+                row["ta_busy_per_cu"] = round(a["TA_TA_BUSY_sum"] / 256 / gui, 4)
+            if "TCC_HIT_sum" in a and (a["TCC_HIT_sum"] + a.get("TCC_MISS_sum", 0.0)) > 0:
+                row["l2_hit_rate"] = round(a["TCC_HIT_sum"] / (a["TCC_HIT_sum"] + a.get("TCC_MISS_sum", 0.0)), 4)
         wc = a.get("SQ_WAVE_CYCLES", 0.0)
         if wc:
-            for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_INST_LEVEL_VMEM"):
                 if k in a:
                     row[k.lower() + "_frac_of_wave_cycles"] = round(a[k] / wc, 4)
         row["raw"] = {k: v for k, v in a.items() if k not in ("dispatches",)}
@@ -75,7 +91,11 @@ def main():
     json.dump(res, open(out, "w"), indent=1)
     for lab, row in res["classes"].items():
         print(f"{lab:60s} n={row['dispatches']:5d} mfma={row.get('mfma_util')} valu={row.get('valu_busy')} "
-              f"clk={row.get('clock_ghz')}")
+              f"clk={row.get('clock_ghz')} lds={row.get('lds_idx_active_per_cu_cycle')} "
+              f"bankc={row.get('lds_bank_conflict_frac')} waitlds={row.get('sq_wait_inst_lds_frac_of_wave_cycles')} "
+              f"ta={row.get('ta_busy_per_cu')} l2hit={row.get('l2_hit_rate')} "
+              f"wait={row.get('sq_wait_any_frac_of_wave_cycles')} winst={row.get('sq_wait_inst_any_frac_of_wave_cycles')} "
+              f"vmemlvl={row.get('sq_inst_level_vmem_frac_of_wave_cycles')}")
 
 
 if __name__ == "__main__":
