@@ -40,29 +40,28 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int kTile = 16;                          // output tile edge (pixels)
-constexpr int kHalo = kTile + 2;                   // 18
-constexpr int kHaloPx = kHalo * kHalo;             // 324
-constexpr int kStageItems = kHaloPx * 8;           // float4 items per chunk (x1 4 quads + x2 4 quads)
-constexpr int kStageF4 = 2624;                     // >= kStageItems; the last DMA round is wave 0's 64 lanes
+constexpr int kTile = 16;                          // output tile width (pixels); height TH is a parameter
+constexpr int kHalo = kTile + 2;                   // 18 halo columns
 constexpr int kDwF4 = 128;                         // per-chunk dw block: [9][8] weights, [8] bias, pad
-constexpr int kNStage = 3;                         // stage ring (halo + dw block), read by gate(c) in iteration c-1
-constexpr int kNW = 4;                             // W ring, read by the MFMAs of chunk c in iteration c
-constexpr int kStageSlot = kStageF4 + kDwF4;       // 2752 float4
 
-// The halo stage is kStagePieces lane-linear 1 KiB DMA wave-instructions (piece k -> items
-// 64k..64k+63), dealt round-robin: wave w issues pieces w, w + WAVES, ...
-constexpr int kStagePieces = (kStageItems + 63) / 64;  // 41
-static_assert(kStagePieces * 64 == kStageF4, "stage layout");
-template <int WAVES> constexpr int stage_pieces(int w) { return (kStagePieces - w + WAVES - 1) / WAVES; }
-
-// DMA wave-instructions wave w issues per chunk: its stage pieces, W records t with
-// (t+1)%WAVES == w, the 2 dw-block pieces on the last wave
-template <int NT, int WAVES> constexpr int dma_per_chunk(int w) {
-  int n = stage_pieces<WAVES>(w) + (w == WAVES - 1 ? 2 : 0);
-  for (int t = 0; t < NT; ++t) n += ((t + 1) % WAVES == w) ? 1 : 0;
-  return n;
-}
+// Stage slot geometry of a 16 x TH tile: the (TH+2) x 18 halo, one 128 B line (x1|x2 of the chunk,
+// 8 float4 items) per pixel, staged as lane-linear 1 KiB DMA wave-instructions (piece k -> items
+// 64k..64k+63) dealt round-robin over the waves, then the chunk's dw block.
+template <int TH> struct GdTile {
+  static constexpr int kHaloPx = (TH + 2) * kHalo;                 // 324 at TH = 16
+  static constexpr int kStageItems = kHaloPx * 8;
+  static constexpr int kStagePieces = (kStageItems + 63) / 64;     // 41 at TH = 16, 23 at TH = 8
+  static constexpr int kStageF4 = kStagePieces * 64;
+  static constexpr int kStageSlot = kStageF4 + kDwF4;
+  template <int WAVES> static constexpr int stage_pieces(int w) { return (kStagePieces - w + WAVES - 1) / WAVES; }
+  // DMA wave-instructions wave w issues per chunk: its stage pieces, W records t with
+  // (t+1)%WAVES == w, the 2 dw-block pieces on the last wave
+  template <int NT, int WAVES> static constexpr int dma_per_chunk(int w) {
+    int n = stage_pieces<WAVES>(w) + (w == WAVES - 1 ? 2 : 0);
+    for (int t = 0; t < NT; ++t) n += ((t + 1) % WAVES == w) ? 1 : 0;
+    return n;
+  }
+};
 
 // Exact-erf GELU, 0.5 x (1 + erf(x / sqrt 2)), with erf from Abramowitz & Stegun 7.1.26
 // (|error| <= 1.5e-7): branch-free, so the gate VALU stays in one basic block with the MFMAs it is
@@ -102,9 +101,15 @@ __device__ __forceinline__ void dma16(const void* src, f32x4* lds_wave_base) {
 
 }  // namespace
 
-template <int NT, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
-  constexpr int RPW = kTile / WAVES;                           // tile rows per wave
+template <int NT, int WAVES, int TH, int NSTG>
+__global__ __launch_bounds__(64 * WAVES) void gdfn_out_kernel(GdfnParams p) {
+  using T = GdTile<TH>;
+  constexpr int kStageItems = T::kStageItems, kStagePieces = T::kStagePieces;
+  constexpr int kStageF4 = T::kStageF4, kStageSlot = T::kStageSlot;
+  constexpr int kNStage = NSTG;                                // stage ring (halo + dw block)
+  constexpr int kNW = NSTG + 1;  // W ring: chunk c is multiplied in iteration c, chunk c+NSTG issued then
+  constexpr int RPW = TH / WAVES;                              // tile rows per wave
+  static_assert(RPW * WAVES == TH && NSTG >= 2, "tile rows per wave / ring depth");
   constexpr int kRounds = (kStagePieces + WAVES - 1) / WAVES;  // stage pieces per wave (max)
   extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
   f32x4* wring = lds + kNStage * kStageSlot;        // [kNW][NT][64]
@@ -115,7 +120,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
 
   // XCD-aware tile order: logical tiles [k*per, (k+1)*per) run on XCD k, so tiles that share halo
   // rows/columns share an L2.  The grid is padded to a multiple of 8.
-  const int tx_n = (p.W + kTile - 1) / kTile, ty_n = (p.H + kTile - 1) / kTile;
+  const int tx_n = (p.W + kTile - 1) / kTile, ty_n = (p.H + TH - 1) / TH;
   const int ntiles = p.Bn * tx_n * ty_n;
   const int per = (int)(gridDim.x >> 3);
   int bid = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
@@ -124,7 +129,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
   bid /= tx_n;
   const int ty = bid % ty_n;
   const int b = bid / ty_n;
-  const int x0 = tx * kTile, y0 = ty * kTile;
+  const int x0 = tx * kTile, y0 = ty * TH;
   const long long HW = (long long)p.H * p.W;
   const float* X = p.x + (long long)b * HW * p.ld;
 
@@ -165,29 +170,27 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
   auto wait_chunks = [&](auto nchunks) {
     constexpr int K = decltype(nchunks)::value;
     switch (wave) {
-      case 0: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(0 % WAVES)>(); break;
-      case 1: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(1 % WAVES)>(); break;
-      case 2: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(2 % WAVES)>(); break;
-      case 3: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(3 % WAVES)>(); break;
-      case 4: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(4 % WAVES)>(); break;
-      case 5: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(5 % WAVES)>(); break;
-      case 6: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(6 % WAVES)>(); break;
-      case 7: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(7 % WAVES)>(); break;
-      case 8: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(8 % WAVES)>(); break;
-      case 9: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(9 % WAVES)>(); break;
-      case 10: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(10 % WAVES)>(); break;
-      case 11: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(11 % WAVES)>(); break;
-      case 12: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(12 % WAVES)>(); break;
-      case 13: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(13 % WAVES)>(); break;
-      case 14: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(14 % WAVES)>(); break;
-      default: wait_vmcnt<K * dma_per_chunk<NT, WAVES>(15 % WAVES)>(); break;
+      case 0: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(0 % WAVES)>(); break;
+      case 1: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(1 % WAVES)>(); break;
+      case 2: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(2 % WAVES)>(); break;
+      case 3: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(3 % WAVES)>(); break;
+      case 4: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(4 % WAVES)>(); break;
+      case 5: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(5 % WAVES)>(); break;
+      case 6: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(6 % WAVES)>(); break;
+      case 7: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(7 % WAVES)>(); break;
+      case 8: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(8 % WAVES)>(); break;
+      case 9: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(9 % WAVES)>(); break;
+      case 10: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(10 % WAVES)>(); break;
+      case 11: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(11 % WAVES)>(); break;
+      case 12: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(12 % WAVES)>(); break;
+      case 13: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(13 % WAVES)>(); break;
+      case 14: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(14 % WAVES)>(); break;
+      default: wait_vmcnt<K * T::template dma_per_chunk<NT, WAVES>(15 % WAVES)>(); break;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // no LDS read may move above the barrier
   };
-  auto wait_keep_one = [&]() { wait_chunks(std::integral_constant<int, 1>{}); };
-  auto wait_keep_two = [&]() { wait_chunks(std::integral_constant<int, 2>{}); };
   auto wait_all = [&]() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -255,22 +258,21 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
     }
   };
 
-  // prologue: chunks 0, 1, 2 in flight; gate(0) once chunk 0 has landed
+  // prologue: chunks 0 .. NSTG-1 in flight; gate(0) once chunk 0 has landed
   f32x4 gb[RPW];
-  issue(0);
-  if (kch > 1) issue(1);
-  if (kch > 2) issue(2);
-  if (kch > 2) wait_keep_two();
-  else if (kch > 1) wait_keep_one();
+#pragma unroll
+  for (int c = 0; c < NSTG; ++c)
+    if (c < kch) issue(c);
+  if (kch >= NSTG) wait_chunks(std::integral_constant<int, NSTG - 1>{});
   else wait_all();
   gate(0, gb);
   for (int g = 0; g + 1 < kch; ++g) {
-    // issued so far: chunks 0..g+2.  gate(g+1) needs chunk g+1; chunk g+2 may stay in flight.
-    if (g + 2 < kch) wait_keep_one();
+    // issued so far: chunks 0..g+NSTG-1.  gate(g+1) needs chunk g+1; younger chunks may stay in flight.
+    if (g + NSTG - 1 < kch) wait_chunks(std::integral_constant<int, NSTG - 2>{});
     else wait_all();
-    // past this barrier every wave is done with gate(g) (stage slot g%3) and mfma(g-1) (W slot
-    // (g-1)%4 == (g+3)%4): chunk g+3 can reuse both
-    if (g + 3 < kch) issue(g + 3);
+    // past this barrier every wave is done with gate(g) (stage slot g%NSTG) and mfma(g-1) (W slot
+    // (g-1)%kNW = (g+NSTG)%kNW): chunk g+NSTG can reuse both
+    if (g + NSTG < kch) issue(g + NSTG);
     f32x4 gbn[RPW];
     gate(g + 1, gbn);
     mfma_chunk(g, gb);
@@ -325,21 +327,32 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gdfn_out_kernel(GdfnParams p) {
 // One wave per SIMD with up to 512 VGPRs: the accumulators of the strip (R x C/16 float4), the
 // three prefetched rows and the chunk's dw weights stay in registers.  r01's kernel spent about a
 // third of its wave cycles parked on the per-chunk barrier / DMA waits (profiles/r02_pmc_*).
+// DPP lane shift of one float.  The empty asm keeps each component a separate scalar: hipcc
+// (ROCm 7.2, -O3) otherwise merges the four update_dpp calls of a float4 into ONE v_mov_b32_dpp of
+// the x component and copies it into y, z and w (wrong results; seen in the ISA of gdfn2 and of a
+// 10-line reproducer, tools/micro/dpp_probe.hip documents the lane mapping).
+template <int CTRL>
+__device__ __forceinline__ float dpp1(float old, float v) {
+  int o = __builtin_bit_cast(int, old), x = __builtin_bit_cast(int, v);
+  asm("" : "+v"(x));
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(o, x, CTRL, 0xf, 0xf, false));
+}
 template <int CTRL>
 __device__ __forceinline__ f32x4 dpp4(const f32x4& old, const f32x4& v) {
-  f32x4 r;
-  r.x = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old.x), __builtin_bit_cast(int, v.x), CTRL, 0xf, 0xf, false));
-  r.y = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old.y), __builtin_bit_cast(int, v.y), CTRL, 0xf, 0xf, false));
-  r.z = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old.z), __builtin_bit_cast(int, v.z), CTRL, 0xf, 0xf, false));
-  r.w = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old.w), __builtin_bit_cast(int, v.w), CTRL, 0xf, 0xf, false));
-  return r;
+  return f32x4{dpp1<CTRL>(old.x, v.x), dpp1<CTRL>(old.y, v.y), dpp1<CTRL>(old.z, v.z), dpp1<CTRL>(old.w, v.w)};
 }
 
-template <int NT, int R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+template <int NT, int R, int WPS>
+__global__ __launch_bounds__(256 * WPS) __attribute__((amdgpu_waves_per_eu(WPS, WPS)))
 void gdfn2_kernel(GdfnParams p, int nunits) {
-  constexpr int K = R + 2;  // input rows per strip and chunk
-  static_assert(K % 3 == 0, "the 3 prefetch slots must line up at chunk boundaries");
+  constexpr int K = R + 2;             // input rows per strip and chunk
+  constexpr int PD = WPS == 1 ? 2 : 1;  // rows prefetched ahead (the second wave of a SIMD hides more)
+  constexpr int NS = PD + 1;           // row slots
+  static_assert(K % NS == 0, "the prefetch slots must line up at chunk boundaries");
+  // one wave per SIMD (512 VGPRs): the chunk's dw taps stay in registers; two waves per SIMD
+  // (256 VGPRs): they are re-read from LDS where they are used.  W fragments: always from LDS.
+  constexpr bool kWRegs = WPS == 1;
+  constexpr int WAVES = 4 * WPS;
   extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
   const int kch = p.hidS >> 4;
   f32x4* wl = lds;                          // [kch][NT][64] project_out fragments, chunk-major
@@ -347,11 +360,11 @@ void gdfn2_kernel(GdfnParams p, int nunits) {
   {
     const f32x4* Wf = reinterpret_cast<const f32x4*>(p.Wp);  // [NT][kch][64]
     const f32x4* Dw = reinterpret_cast<const f32x4*>(p.dw);  // [kch][128]
-    for (int i = threadIdx.x; i < kch * NT * 64; i += 256) {
+    for (int i = threadIdx.x; i < kch * NT * 64; i += 64 * WAVES) {
       const int g = i / (NT * 64), rem = i - g * (NT * 64);
       wl[i] = Wf[((size_t)(rem >> 6) * kch + g) * 64 + (rem & 63)];
     }
-    for (int i = threadIdx.x; i < kch * 80; i += 256) {
+    for (int i = threadIdx.x; i < kch * 80; i += 64 * WAVES) {
       const int g = i / 80;
       dl[i] = Dw[(size_t)g * 128 + (i - g * 80)];
     }
@@ -367,12 +380,12 @@ void gdfn2_kernel(GdfnParams p, int nunits) {
   const int per_xcd = (nunits + 7) >> 3;
   const int u_begin = (int)(blockIdx.x & 7) * per_xcd;
   const int u_end = min(u_begin + per_xcd, nunits);
-  const int wstride = (int)(gridDim.x >> 3) * 4;
+  const int wstride = (int)(gridDim.x >> 3) * WAVES;
   const unsigned row_bytes = (unsigned)p.W * (unsigned)p.ld * 4u;
   const unsigned img_bytes = (unsigned)p.H * row_bytes;
   constexpr unsigned kFar = 0x40000000u;  // row or column offset outside the image (img_bytes <= 2^30)
 
-  for (int u = u_begin + (int)(blockIdx.x >> 3) * 4 + wave; u < u_end; u += wstride) {
+  for (int u = u_begin + (int)(blockIdx.x >> 3) * WAVES + wave; u < u_end; u += wstride) {
     const int sc = u % sx_n, t2 = u / sx_n;
     const int sr = t2 % sy_n, b = t2 / sy_n;
     const int x0 = sc * 16, y0 = sr * R;
@@ -398,9 +411,9 @@ void gdfn2_kernel(GdfnParams p, int nunits) {
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 xs[3][2][2];
-    load_row(0, 0, xs[0]);
-    load_row(0, 1, xs[1]);
+    f32x4 xs[NS][2][2];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) load_row(0, k, xs[k]);
     // carried from the previous chunk: the depthwise sums of row R-1 (not yet gated) and the gated
     // row R-2 (not yet multiplied); zeros before chunk 0, so the carried MFMAs add nothing
     f32x4 dpend[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -416,36 +429,47 @@ void gdfn2_kernel(GdfnParams p, int nunits) {
     };
     for (int g = 0; g < kch; ++g) {
       const f32x4* dwl = dl + g * 80;
-      f32x4 wdw[9][2], bdw[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bdw[h] = dwl[72 + 4 * h + lq];
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) wdw[tap][h] = dwl[tap * 8 + 4 * h + lq];
-      }
-      f32x4 wf[NT], wfp[NT];
       const int gp = g > 0 ? g - 1 : 0;
+      [[maybe_unused]] f32x4 wdw[9][2];
+      if constexpr (kWRegs) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        wf[t] = wl[(g * NT + t) * 64 + lane];
-        wfp[t] = wl[(gp * NT + t) * 64 + lane];
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) wdw[tap][h] = dwl[tap * 8 + 4 * h + lq];
       }
+      // tap (row i, column c) of x_h, from registers or (opaque pointer: no hoisting) from LDS
+      auto tapw = [&](const f32x4* dwk, int i, int c, int h) -> f32x4 {
+        if constexpr (kWRegs) return wdw[3 * i + c][h];
+        else return dwk[(3 * i + c) * 8 + 4 * h + lq];
+      };
+      auto mfma_lds = [&](auto prev, const f32x4& gbv, f32x4 (&ac)[NT]) {
+        constexpr bool kPrev = decltype(prev)::value;
+        const f32x4* wk = wl + (kPrev ? gp : g) * NT * 64 + lane;
+        asm("" : "+v"(wk));  // W fragments are read where used (not hoisted into 24 live VGPRs)
+        f32x4 w[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) w[t] = wk[64 * t];
+        mfma_row(w, gbv, ac);
+      };
       f32x4 d[R][2];      // depthwise sums per output row (only a window of 3 is live)
       f32x4 gb[R];        // gated rows
       f32x4 gq;           // gated carried row R-1
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        // prefetch input row k+2 (of this chunk, or row 0/1 of the next; the last chunk re-reads)
-        if (k + 2 < K) load_row(g, k + 2, xs[(k + 2) % 3]);
-        else load_row(g + 1 < kch ? g + 1 : g, k + 2 - K, xs[(k + 2) % 3]);
+        // prefetch input row k+PD (of this chunk, or the first rows of the next; the last chunk re-reads)
+        if (k + PD < K) load_row(g, k + PD, xs[(k + PD) % NS]);
+        else load_row(g + 1 < kch ? g + 1 : g, k + PD - K, xs[(k + PD) % NS]);
+        const f32x4* dwk = dwl;
+        if constexpr (!kWRegs) asm("" : "+v"(dwk));
+        const f32x4 bdw[2] = {dwk[72 + lq], dwk[76 + lq]};
         // column neighbours by DPP within each 16-lane row (= one channel quad): row_shr:1 gives
         // lane i the value of lane i-1, lane 0 keeps the edge load (column x0-1); row_shl:1 alike
         f32x4 v[2][3];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          v[h][1] = xs[k % 3][h][0];
-          v[h][0] = dpp4<0x111>(xs[k % 3][h][1], v[h][1]);
-          v[h][2] = dpp4<0x101>(xs[k % 3][h][1], v[h][1]);
+          v[h][1] = xs[k % NS][h][0];
+          v[h][0] = dpp4<0x111>(xs[k % NS][h][1], v[h][1]);
+          v[h][2] = dpp4<0x101>(xs[k % NS][h][1], v[h][1]);
         }
         // stencil: input row k -> output rows k - i (tap row i)
 #pragma unroll
@@ -457,7 +481,7 @@ void gdfn2_kernel(GdfnParams p, int nunits) {
             f32x4 s = (i == 0) ? bdw[h] : d[r][h];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-              const f32x4 w = wdw[3 * i + c][h];
+              const f32x4 w = tapw(dwk, i, c, h);
               s.x = fmaf(v[h][c].x, w.x, s.x);
               s.y = fmaf(v[h][c].y, w.y, s.y);
               s.z = fmaf(v[h][c].z, w.z, s.z);
@@ -469,12 +493,12 @@ void gdfn2_kernel(GdfnParams p, int nunits) {
         // the previous chunk's last rows
         if (k == 0) {
           gq = gate4(dpend[0], dpend[1]);
-          mfma_row(wfp, gpend, acc[R - 2]);
+          mfma_lds(std::true_type{}, gpend, acc[R - 2]);
         }
-        if (k == 1) mfma_row(wfp, gq, acc[R - 1]);
+        if (k == 1) mfma_lds(std::true_type{}, gq, acc[R - 1]);
         // this chunk: gate row k-3, multiply row k-4
         if (k - 3 >= 0 && k - 3 < R) gb[k - 3] = gate4(d[k - 3][0], d[k - 3][1]);
-        if (k - 4 >= 0 && k - 4 < R) mfma_row(wf, gb[k - 4], acc[k - 4]);
+        if (k - 4 >= 0 && k - 4 < R) mfma_lds(std::false_type{}, gb[k - 4], acc[k - 4]);
       }
       dpend[0] = d[R - 1][0];
       dpend[1] = d[R - 1][1];
@@ -526,9 +550,26 @@ bool gdfn_supported(int C, int hidS) {
   return (C == 48 || C == 96) && hidS % 16 == 0 && hidS <= 256;
 }
 
-size_t gdfn_lds_bytes(int C) { return (size_t)(kNStage * kStageSlot + kNW * 64 * (C / 16)) * sizeof(f32x4); }
+template <int NT, int WAVES, int TH, int NSTG>
+static hipError_t launch_gdfn1(const GdfnParams& p, hipStream_t s) {
+  const size_t lds = (size_t)(NSTG * GdTile<TH>::kStageSlot + (NSTG + 1) * 64 * NT) * sizeof(f32x4);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  static size_t attr[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (lds > 64 * 1024 && lds > attr[dev]) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gdfn_out_kernel<NT, WAVES, TH, NSTG>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr[dev] = lds;
+  }
+  const long long tiles = (long long)p.Bn * ((p.H + TH - 1) / TH) * ((p.W + kTile - 1) / kTile);
+  const long long grid = (tiles + 7) / 8 * 8;
+  hipLaunchKernelGGL((gdfn_out_kernel<NT, WAVES, TH, NSTG>), dim3((unsigned)grid), dim3(64 * WAVES), lds, s, p);
+  return hipGetLastError();
+}
 
-template <int NT, int R>
+template <int NT, int R, int WPS>
 static hipError_t launch_gdfn2(const GdfnParams& p, hipStream_t s) {
   static size_t attr[64] = {};
   int dev = 0;
@@ -537,7 +578,7 @@ static hipError_t launch_gdfn2(const GdfnParams& p, hipStream_t s) {
   const size_t lds = (size_t)kch * (NT * 64 + 80) * sizeof(f32x4);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > attr[dev]) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gdfn2_kernel<NT, R>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gdfn2_kernel<NT, R, WPS>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr[dev] = lds;
@@ -545,7 +586,7 @@ static hipError_t launch_gdfn2(const GdfnParams& p, hipStream_t s) {
   const long long units = (long long)p.Bn * ((p.H + R - 1) / R) * ((p.W + 15) / 16);
   if (units >= (1LL << 31)) return hipErrorInvalidValue;
   const int grid = std::max(8, device_cu_count() / 8 * 8);  // persistent: one block per CU
-  hipLaunchKernelGGL((gdfn2_kernel<NT, R>), dim3((unsigned)grid), dim3(256), lds, s, p, (int)units);
+  hipLaunchKernelGGL((gdfn2_kernel<NT, R, WPS>), dim3((unsigned)grid), dim3(256 * WPS), lds, s, p, (int)units);
   return hipGetLastError();
 }
 
@@ -561,25 +602,25 @@ hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
   if (!gdfn_supported(C, p.hidS) || p.ld != 2 * p.hidS || p.ldo % 4 || (p.R && p.ldr % 4) || !p.zeros)
     return hipErrorInvalidValue;
   if (gdfn2_ok(p, C)) {
-    static const int rows = getenv("KDLAE_GDFN2_ROWS") ? atoi(getenv("KDLAE_GDFN2_ROWS")) : 7;
-    if (C == 96) return launch_gdfn2<6, 4>(p, s);  // R = 7 spills at NT = 6
-    return rows == 4 ? launch_gdfn2<3, 4>(p, s) : rows == 10 ? launch_gdfn2<3, 10>(p, s) : launch_gdfn2<3, 7>(p, s);
+    static const int rows = getenv("KDLAE_GDFN2_ROWS") ? atoi(getenv("KDLAE_GDFN2_ROWS")) : 10;
+    if (C == 96) return launch_gdfn2<6, 4, 1>(p, s);  // R = 7 spills at NT = 6
+    return rows == 4 ? launch_gdfn2<3, 4, 1>(p, s) : rows == 7 ? launch_gdfn2<3, 7, 1>(p, s) : launch_gdfn2<3, 10, 1>(p, s);
   }
-  const long long tiles = (long long)p.Bn * ((p.H + kTile - 1) / kTile) * ((p.W + kTile - 1) / kTile);
-  const long long grid = (tiles + 7) / 8 * 8;
-  const size_t lds = gdfn_lds_bytes(C);
-  static const int waves = getenv("KDLAE_GDFN_WAVES") ? atoi(getenv("KDLAE_GDFN_WAVES")) : 8;
-  const int w = (waves == 4 || waves == 16) ? waves : 8;
-  switch ((C / 16) * 100 + w) {
-    case 304: hipLaunchKernelGGL((gdfn_out_kernel<3, 4>), dim3((unsigned)grid), dim3(256), lds, s, p); break;
-    case 308: hipLaunchKernelGGL((gdfn_out_kernel<3, 8>), dim3((unsigned)grid), dim3(512), lds, s, p); break;
-    case 316: hipLaunchKernelGGL((gdfn_out_kernel<3, 16>), dim3((unsigned)grid), dim3(1024), lds, s, p); break;
-    case 604: hipLaunchKernelGGL((gdfn_out_kernel<6, 4>), dim3((unsigned)grid), dim3(256), lds, s, p); break;
-    case 608: hipLaunchKernelGGL((gdfn_out_kernel<6, 8>), dim3((unsigned)grid), dim3(512), lds, s, p); break;
-    case 616: hipLaunchKernelGGL((gdfn_out_kernel<6, 16>), dim3((unsigned)grid), dim3(1024), lds, s, p); break;
-    default: return hipErrorInvalidValue;
+  // r01 schedule.  KDLAE_GDFN_TILE picks the tile height / stage ring / waves:
+  //   0: 16 rows, 3 stage slots, 8 waves (one block per CU, 156 KB of LDS; r01's configuration);
+  //   1 (default): 8 rows, 2 slots, 4 waves (69 KB: two independent blocks per CU);
+  //   2: 4 rows, 2 slots, 4 waves (three blocks per CU);  3: 8 rows, 2 slots, 2 waves.
+  static const int tile = getenv("KDLAE_GDFN_TILE") ? atoi(getenv("KDLAE_GDFN_TILE")) : 1;
+  if (C == 96) {
+    if (tile == 0) return launch_gdfn1<6, 8, 16, 3>(p, s);
+    if (tile == 2) return launch_gdfn1<6, 4, 4, 2>(p, s);
+    if (tile == 3) return launch_gdfn1<6, 2, 8, 2>(p, s);
+    return launch_gdfn1<6, 4, 8, 2>(p, s);
   }
-  return hipGetLastError();
+  if (tile == 0) return launch_gdfn1<3, 8, 16, 3>(p, s);
+  if (tile == 2) return launch_gdfn1<3, 4, 4, 2>(p, s);
+  if (tile == 3) return launch_gdfn1<3, 2, 8, 2>(p, s);
+  return launch_gdfn1<3, 4, 8, 2>(p, s);
 }
 
 }  // namespace kdlae
