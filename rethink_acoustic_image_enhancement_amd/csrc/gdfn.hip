@@ -17,7 +17,7 @@
 //     is multiplied; waits are counted (vmcnt = one chunk's DMAs per wave) and barriers raw, so the
 //     in-flight chunks are never drained.  Nothing else in the loop reads global memory (an
 //     ordinary load would make hipcc drain the DMAs before its use);
-//   * the halo image is lane-linear [pixel][slot] with slot = quad ^ (pixel & 7) applied on the
+//   * the halo image is lane-linear [pixel][slot] with slot = quad ^ (column & 7) applied on the
 //     SOURCE address, so the column reads of the stencil are bank-conflict-free;
 //   * each lane computes the depthwise 3x3 + exact-erf gate for its 4 pixels (one per tile row) and
 //     4 channels — a float4 which IS its B operand for the chunk's 4 MFMA k-steps
@@ -98,6 +98,11 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 __device__ __forceinline__ void dma16(const void* src, f32x4* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds_wave_base, 16, 0, 0);
 }
+// buffer form: voffset per lane, soffset (wave-uniform, SGPR) added outside the VALU; offsets past
+// the descriptor's range land zeros
+__device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t r, f32x4* lds_wave_base, unsigned voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)lds_wave_base, 16, (int)voff, soff, 0, 0);
+}
 
 }  // namespace
 
@@ -133,37 +138,44 @@ __global__ __launch_bounds__(64 * WAVES) void gdfn_out_kernel(GdfnParams p) {
   const long long HW = (long long)p.H * p.W;
   const float* X = p.x + (long long)b * HW * p.ld;
 
-  // per-thread halo sources as 32-bit byte offsets into the image (chunk g adds 128 g bytes);
-  // out-of-image pixels and tail items read the zero line (offset ~0u)
+  // per-thread halo sources as 32-bit byte offsets into the image; chunk g adds 128 g bytes through
+  // the DMA's scalar offset, so issuing a chunk costs no VALU.  Out-of-image pixels and tail items
+  // get an offset past the descriptor's range: the buffer load returns zeros (the conv padding).
   unsigned srco[kRounds];
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
     const int it = (wave + WAVES * j) * 64 + lane;
-    const int px = it >> 3, slot = it & 7, quad = slot ^ (px & 7);
+    const int px = it >> 3, slot = it & 7;
     const int hy = px / kHalo, hx = px - hy * kHalo;
+    const int quad = slot ^ (hx & 7);  // column swizzle: the halo row pitch (18) is even, so a
+                                       // column-only XOR keeps every row's reads conflict-free and
+                                       // leaves the row as an immediate offset
     const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
     const bool ok = it < kStageItems && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-    srco[j] = ok ? (unsigned)(((yy * p.W + xx) * p.ld + 4 * quad) * 4) : ~0u;
+    srco[j] = ok ? (unsigned)(((yy * p.W + xx) * p.ld + 4 * quad) * 4) : kOOB2;
   }
-  const char* Xb = reinterpret_cast<const char*>(X);
-  const f32x4* Wf = reinterpret_cast<const f32x4*>(p.Wp);
-  const f32x4* Dw = reinterpret_cast<const f32x4*>(p.dw);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(X), 0, (int)(HW * p.ld * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.Wp), 0, NT * kch * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.dw), 0, kch * kDwF4 * 16, 0x00020000);
   auto issue = [&](int g) {
     f32x4* sl = lds + (g % kNStage) * kStageSlot;
 #pragma unroll
     for (int j = 0; j < kRounds; ++j) {
       const int k = wave + WAVES * j;
       if (k >= kStagePieces) break;
-      dma16(srco[j] != ~0u ? (const void*)(Xb + srco[j] + 128u * g) : (const void*)p.zeros, sl + 64 * k);
+      dma_buf(rx, sl + 64 * k, srco[j], 128 * g);
     }
     if (wave == WAVES - 1) {
-      dma16(Dw + (size_t)g * kDwF4 + lane, sl + kStageF4);
-      dma16(Dw + (size_t)g * kDwF4 + 64 + lane, sl + kStageF4 + 64);
+      dma_buf(rd, sl + kStageF4, 16u * lane, g * (kDwF4 * 16));
+      dma_buf(rd, sl + kStageF4 + 64, 16u * lane + 1024u, g * (kDwF4 * 16));
     }
     f32x4* wl = wring + (g % kNW) * (64 * NT);
 #pragma unroll
     for (int t = 0; t < NT; ++t)
-      if ((t + 1) % WAVES == wave) dma16(Wf + ((size_t)t * kch + g) * 64 + lane, wl + 64 * t);
+      if ((t + 1) % WAVES == wave) dma_buf(rw, wl + 64 * t, 16u * lane, (t * kch + g) * 1024);
   };
   // wait until only the youngest chunk's DMAs are outstanding, then a raw barrier (a
   // __syncthreads() would wait vmcnt(0) and drain the ring)
@@ -203,6 +215,16 @@ __global__ __launch_bounds__(64 * WAVES) void gdfn_out_kernel(GdfnParams p) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // per-lane halo read offsets (f32x4 units) of the wave's first input row, column tap j, half h:
+  // the other rows are immediate offsets (rr * 18 * 8), so the stencil needs no address VALU
+  int lo[2][3];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int hx = cx + j;
+      lo[h][j] = (RPW * wave * kHalo + hx) * 8 + ((4 * h + q) ^ (hx & 7));
+    }
   // gate(g): depthwise 3x3 (rows 4w..4w+3, column cx, channels 16g+4q..+3 of x1 and x2) + gate
   auto gate = [&](int g, f32x4 (&gb)[RPW]) {
     const f32x4* sl = lds + (g % kNStage) * kStageSlot;
@@ -223,8 +245,7 @@ __global__ __launch_bounds__(64 * WAVES) void gdfn_out_kernel(GdfnParams p) {
         for (int i = 0; i < 3; ++i) wv[i] = dw[(3 * i + j) * 8 + 4 * h + q];
 #pragma unroll
         for (int rr = 0; rr < RPW + 2; ++rr) {
-          const int px = (RPW * wave + rr) * kHalo + cx + j;
-          const f32x4 v = sl[px * 8 + ((4 * h + q) ^ (px & 7))];
+          const f32x4 v = (sl + lo[h][j])[rr * kHalo * 8];
 #pragma unroll
           for (int i = 0; i < 3; ++i) {
             const int r = rr - i;
