@@ -214,8 +214,9 @@ int kdlae_postprocess_u8(const float* out, int B, int C, int Hs, int Ws, int h, 
  * buffers of kdlae_tt_num_floats floats in state_dict order (offsets from kdlae_tt_param_info; each key
  * starts on a 16-byte boundary and the pad floats between keys must be zero);
  * weights are read in their OIHW state_dict layout, so an optimizer update needs no repacking.
- * The DDP gradient all-reduce (base_model.py:76-82) is one collective over the flat gradient
- * buffer, done by the caller between kdlae_tt_backward and kdlae_train_clip_adamw.
+ * The DDP gradient all-reduce (base_model.py:76-82) is done by the caller between the backward and
+ * kdlae_train_clip_adamw: one collective over the flat gradient buffer, or bucketed and overlapped
+ * with the backward through kdlae_tt_backward_marked's gradient-ready marks.
  */
 typedef struct kdlae_tt_handle kdlae_tt_handle;
 
@@ -237,6 +238,18 @@ int kdlae_tt_forward(kdlae_tt_handle* h, const float* theta, const float* img, c
  * gradients; grad (flat, overwritten) receives d loss / d theta.  Inputs get no gradient. */
 int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, const float* dsr, float* grad,
                       void* workspace, size_t workspace_bytes, void* stream);
+/* kdlae_tt_backward plus gradient-ready marks for a bucketed DDP all-reduce that overlaps the backward
+ * (DistributedDataParallel's gradient buckets, reducer.cpp behind base_model.py:76-82): the backward
+ * walks the network deepest-first, i.e. the flat buffer from the end, and records event j when the
+ * suffix [kdlae_tt_mark_lo(h, j), num_floats) of `grad` is final (offsets decrease with j).
+ * kdlae_tt_mark_wait makes another stream wait for event j (enqueue that bucket's all-reduce behind
+ * it); kdlae_tt_mark_sync waits on the host.  Marks stay valid until the next marked backward. */
+int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float* dhq, const float* dsr, float* grad,
+                             void* workspace, size_t workspace_bytes, void* stream);
+int kdlae_tt_mark_count(const kdlae_tt_handle* h);
+int64_t kdlae_tt_mark_lo(const kdlae_tt_handle* h, int j);
+int kdlae_tt_mark_wait(kdlae_tt_handle* h, int j, void* stream);
+int kdlae_tt_mark_sync(kdlae_tt_handle* h, int j);
 
 /* replaces self.cri_pix(pred, self.gt) with L1LossSr(loss_weight=1, reduction='mean') (losses.py:159-170):
  * loss[0] = 0.5 l1(hq) + 0.25 l1(sr) + 0.25 (shadow(hq) + shadow(sr)); dhq / dsr receive its gradient

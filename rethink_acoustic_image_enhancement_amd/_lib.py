@@ -33,7 +33,8 @@ EXPORTS = (
     "asdqe_commit_params", "asdqe_params_numel", "asdqe_pack_device", "asdqe_workspace_bytes", "asdqe_forward",
     "kdlae_padded_size", "kdlae_preprocess_u8", "kdlae_frames_preprocess_u8", "kdlae_postprocess_u8",
     "kdlae_tt_create", "kdlae_tt_destroy", "kdlae_tt_num_params", "kdlae_tt_param_info", "kdlae_tt_num_floats",
-    "kdlae_tt_workspace_bytes", "kdlae_tt_forward", "kdlae_tt_backward",
+    "kdlae_tt_workspace_bytes", "kdlae_tt_forward", "kdlae_tt_backward", "kdlae_tt_backward_marked",
+    "kdlae_tt_mark_count", "kdlae_tt_mark_lo", "kdlae_tt_mark_wait", "kdlae_tt_mark_sync",
     "kdlae_train_l1sr_scratch_floats", "kdlae_train_l1sr", "kdlae_train_adamw_scratch_floats",
     "kdlae_train_clip_adamw", "kdlae_train_mixup", "kdlae_train_ema",
 )
@@ -138,6 +139,12 @@ def lib() -> ctypes.CDLL:
                                    c_void_p, c_void_p, ctypes.c_size_t, c_void_p]
     L.kdlae_tt_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_size_t,
                                     c_void_p]
+    L.kdlae_tt_backward_marked.argtypes = L.kdlae_tt_backward.argtypes
+    L.kdlae_tt_mark_count.argtypes = [c_void_p]
+    L.kdlae_tt_mark_lo.argtypes = [c_void_p, c_int]
+    L.kdlae_tt_mark_lo.restype = c_int64
+    L.kdlae_tt_mark_wait.argtypes = [c_void_p, c_int, c_void_p]
+    L.kdlae_tt_mark_sync.argtypes = [c_void_p, c_int]
     L.kdlae_train_l1sr_scratch_floats.argtypes = []
     L.kdlae_train_l1sr_scratch_floats.restype = c_int64
     L.kdlae_train_l1sr.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
@@ -152,7 +159,7 @@ def lib() -> ctypes.CDLL:
     L.kdlae_train_ema.argtypes = [c_void_p, c_void_p, c_int64, c_float, c_void_p]
     for name in EXPORTS:
         if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes", "_padded_size", "_num_floats",
-                              "_scratch_floats", "_params_numel")):
+                              "_scratch_floats", "_params_numel", "_mark_lo")):
             getattr(L, name).restype = c_int
     _lib = L
     return L

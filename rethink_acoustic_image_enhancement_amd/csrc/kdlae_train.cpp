@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -60,6 +61,15 @@ struct kdlae_tt_handle {
   Saved sv;
   int ws_B = -1, ws_H = -1, ws_W = -1;  // last kdlae_tt_workspace_bytes query (its dry run is cached)
   int64_t ws_bytes = -1;
+  // gradient-ready marks of the last kdlae_tt_backward_marked: mark_slot[m] = index of the event
+  // recorded at backward mark m (-1: not a bucket boundary), mark_lo[j] = first flat offset of the
+  // suffix [mark_lo[j], total) whose gradients are final once event j has completed
+  std::vector<int> mark_slot;
+  std::vector<int64_t> mark_lo;
+  std::vector<hipEvent_t> mark_ev;
+  ~kdlae_tt_handle() {
+    for (hipEvent_t e : mark_ev) (void)hipEventDestroy(e);
+  }
 };
 
 namespace {
@@ -161,6 +171,11 @@ struct Ctx {
   hipStream_t s = nullptr;
   float* splitk = nullptr;
   float* red = nullptr;
+  // gradient-ready marks (kdlae_tt_backward_marked): the dry run records, per key offset, the first
+  // and last mark index at which its gradient was written; the real run records an event per mark
+  std::map<int64_t, std::pair<int, int>>* touch = nullptr;
+  int cur_mark = 0;
+  bool record_marks = false;
 
   float* alloc(size_t n) {
     off = (off + 255) / 256 * 256;
@@ -175,9 +190,30 @@ struct Ctx {
   }
   float* G(const std::string& k) const {
     auto it = h->off.find(k);
-    return it == h->off.end() ? nullptr : gr + it->second;
+    if (it == h->off.end()) return nullptr;
+    if (touch) {
+      auto t = touch->find(it->second);
+      if (t == touch->end()) touch->emplace(it->second, std::make_pair(cur_mark, cur_mark));
+      else t->second.second = cur_mark;
+    }
+    return gr + it->second;
   }
 };
+
+// A point in the backward after which some parameters' gradients are final (one TransformerBlock,
+// one head conv, ...).  kdlae_tt_backward_marked records an event at the marks that close a suffix
+// of the flat buffer, so the caller can all-reduce that suffix while the backward continues.
+int mark(Ctx& c) {
+  if (c.record_marks && !c.dry && c.cur_mark < (int)c.h->mark_slot.size()) {
+    const int j = c.h->mark_slot[c.cur_mark];
+    if (j >= 0) {
+      hipError_t e = hipEventRecord(c.h->mark_ev[j], c.s);
+      if (e != hipSuccess) return fail(KDLAE_EHIP, std::string("hipEventRecord: ") + hipGetErrorString(e));
+    }
+  }
+  ++c.cur_mark;
+  return KDLAE_OK;
+}
 
 #define LAUNCH(x)                                                                                    \
   do {                                                                                               \
@@ -491,7 +527,10 @@ int stage_fwd(Ctx& c, const std::string& name, int n, int C, int heads, int Bn, 
 
 int stage_bwd(Ctx& c, const std::string& name, float* d) {
   const auto& recs = c.h->sv.stages.at(name);
-  for (int i = (int)recs.size() - 1; i >= 0; --i) TRY(block_bwd(c, recs[i], d));
+  for (int i = (int)recs.size() - 1; i >= 0; --i) {
+    TRY(block_bwd(c, recs[i], d));
+    TRY(mark(c));
+  }
   return KDLAE_OK;
 }
 
@@ -601,13 +640,16 @@ int net_bwd(Ctx& c, const float* dhq, const float* dsr, bool has_dsr) {
     LAUNCH(tr::launch_nchw_to_nhwc(dsr, oc, B, 4LL * H * W, dsr_h, oc, 0, c.s));
     float* denh = c.alloc(P1 * 4 * (hc / 2));
     TRY(conv3_bwd(c, "outputen", {s.enh, hc / 2}, {dsr_h, oc}, hc / 2, oc, B, 2 * H, 2 * W, 1, {denh, hc / 2}));
+    TRY(mark(c));
     TRY(stage_bwd(c, "enhance", denh));
     float* dupc = c.alloc(P1 * 2 * hc);
     LAUNCH(tr::launch_shuffle(denh, hc / 2, dupc, 2 * hc, hc / 2, B, H, W, 0, c.s));
     // upen's input (cenc) is recomputed-free: it was saved in the forward
     float* dcen = c.alloc(P1 * hc);
     TRY(conv3_bwd(c, "upen.body.0", {s.cenc, hc}, {dupc, 2 * hc}, hc, 2 * hc, B, H, W, 1, {dcen, hc}));
+    TRY(mark(c));
     TRY(conv3_bwd(c, "cen", {s.hq_h, oc}, {dcen, hc}, oc, hc, B, H, W, 1, {dhq_h, oc}, dhq_h, oc));
+    TRY(mark(c));
   } else if (cf.static_train) {
     // sr unused by the loss: its parameters get zero gradients (grad buffer is zeroed up front)
   }
@@ -616,12 +658,16 @@ int net_bwd(Ctx& c, const float* dhq, const float* dsr, bool has_dsr) {
   if (cf.params_cat) {
     float* dro = c.alloc(P1 * 2 * d);
     TRY(conv3_bwd(c, "output2", {s.ro, 2 * d}, {dhq_h, oc}, 2 * d, oc, B, H, W, 1, {dro, 2 * d}));
+    TRY(mark(c));
     TRY(stage_bwd(c, "refinement_out", dro));
     float* dcatp = c.alloc(P1 * (oc + 1));
     TRY(conv3_bwd(c, "output_param", {s.catp, oc + 1}, {dro, 2 * d}, oc + 1, 2 * d, B, H, W, 2, {dcatp, oc + 1}));
+    TRY(mark(c));
     TRY(conv3_bwd(c, "output", {s.ref, 2 * d}, {dcatp, oc + 1}, 2 * d, oc, B, H, W, 1, {dref, 2 * d}));
+    TRY(mark(c));
   } else {
     TRY(conv3_bwd(c, "output", {s.ref, 2 * d}, {dhq_h, oc}, 2 * d, oc, B, H, W, 1, {dref, 2 * d}));
+    TRY(mark(c));
   }
   TRY(stage_bwd(c, "refinement", dref));
   TRY(stage_bwd(c, "decoder_level1", dref));  // dref now holds d(cat1) = [d up2_1 | d enc1]
@@ -631,40 +677,49 @@ int net_bwd(Ctx& c, const float* dhq, const float* dsr, bool has_dsr) {
   LAUNCH(tr::launch_shuffle(dref, 2 * d, du21, 4 * d, d, B, H2, W2, 0, c.s));
   float* ddec2 = c.alloc(P2 * 2 * d);
   TRY(conv3_bwd(c, "up2_1.body.0", {s.dec2, 2 * d}, {du21, 4 * d}, 2 * d, 4 * d, B, H2, W2, 1, {ddec2, 2 * d}));
+  TRY(mark(c));
   TRY(stage_bwd(c, "decoder_level2", ddec2));
   float* dcat2 = c.alloc(P2 * 4 * d);
   TRY(conv1_bwd(c, "reduce_chan_level2", {s.cat2, 4 * d}, {ddec2, 2 * d}, 4 * d, 2 * d, P2, {dcat2, 4 * d}));
+  TRY(mark(c));
   float* de2 = c.alloc(P2 * 2 * d);
   LAUNCH(tr::launch_copy_cols(dcat2 + 2 * d, 4 * d, de2, 2 * d, 2 * d, P2, 0, c.s));
   float* du32 = c.alloc(P3 * 8 * d);
   LAUNCH(tr::launch_shuffle(dcat2, 4 * d, du32, 8 * d, 2 * d, B, H3, W3, 0, c.s));
   float* ddec3 = c.alloc(P3 * 4 * d);
   TRY(conv3_bwd(c, "up3_2.body.0", {s.dec3, 4 * d}, {du32, 8 * d}, 4 * d, 8 * d, B, H3, W3, 1, {ddec3, 4 * d}));
+  TRY(mark(c));
   TRY(stage_bwd(c, "decoder_level3", ddec3));
   float* dcat3 = c.alloc(P3 * 8 * d);
   TRY(conv1_bwd(c, "reduce_chan_level3", {s.cat3, 8 * d}, {ddec3, 4 * d}, 8 * d, 4 * d, P3, {dcat3, 8 * d}));
+  TRY(mark(c));
   float* de3 = c.alloc(P3 * 4 * d);
   LAUNCH(tr::launch_copy_cols(dcat3 + 4 * d, 8 * d, de3, 4 * d, 4 * d, P3, 0, c.s));
   float* du43 = c.alloc(P4 * 16 * d);
   LAUNCH(tr::launch_shuffle(dcat3, 8 * d, du43, 16 * d, 4 * d, B, H4, W4, 0, c.s));
   float* dlat = c.alloc(P4 * 8 * d);
   TRY(conv3_bwd(c, "up4_3.body.0", {s.lat, 8 * d}, {du43, 16 * d}, 8 * d, 16 * d, B, H4, W4, 1, {dlat, 8 * d}));
+  TRY(mark(c));
   TRY(stage_bwd(c, "latent", dlat));
   // encoder, deepest first; each Downsample's dX accumulates into the skip gradient
   float* ddn3c = c.alloc(P3 * 2 * d);
   LAUNCH(tr::launch_shuffle(dlat, 8 * d, ddn3c, 2 * d, 2 * d, B, H4, W4, 1, c.s));
   TRY(conv3_bwd(c, "down3_4.body.0", {s.enc3, 4 * d}, {ddn3c, 2 * d}, 4 * d, 2 * d, B, H3, W3, 1, {de3, 4 * d}, de3,
                 4 * d));
+  TRY(mark(c));
   TRY(stage_bwd(c, "encoder_level3", de3));
   float* ddn2c = c.alloc(P2 * d);
   LAUNCH(tr::launch_shuffle(de3, 4 * d, ddn2c, d, d, B, H3, W3, 1, c.s));
   TRY(conv3_bwd(c, "down2_3.body.0", {s.enc2, 2 * d}, {ddn2c, d}, 2 * d, d, B, H2, W2, 1, {de2, 2 * d}, de2, 2 * d));
+  TRY(mark(c));
   TRY(stage_bwd(c, "encoder_level2", de2));
   float* ddn1c = c.alloc(P1 * (d / 2));
   LAUNCH(tr::launch_shuffle(de2, 2 * d, ddn1c, d / 2, d / 2, B, H2, W2, 1, c.s));
   TRY(conv3_bwd(c, "down1_2.body.0", {s.enc1, d}, {ddn1c, d / 2}, d, d / 2, B, H, W, 1, {de1, d}, de1, d));
+  TRY(mark(c));
   TRY(stage_bwd(c, "encoder_level1", de1));
   TRY(conv3_bwd(c, "patch_embed.proj", {s.img_h, ic}, {de1, d}, ic, d, B, H, W, 1, {nullptr, 0}));
+  TRY(mark(c));
   return KDLAE_OK;
 }
 
@@ -787,6 +842,81 @@ int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, 
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
   return net_bwd(c, dhq, dsr, has_dsr);
+}
+
+int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float* dhq, const float* dsr, float* grad,
+                             void* ws, size_t ws_bytes, void* stream) {
+  if (!h || !theta || !grad || !ws) return fail(KDLAE_EINVAL_CONFIG, "null argument");
+  if (!h->sv.valid || h->sv.ws != ws)
+    return fail(KDLAE_ESTATE, "kdlae_tt_backward_marked needs a preceding kdlae_tt_forward on the same workspace");
+  const bool has_dsr = h->cfg.static_train && dsr;
+  std::map<int64_t, std::pair<int, int>> touch;
+  int nmarks = 0;
+  {  // size the backward and find, per mark, which suffix of the flat buffer is final there
+    Ctx d;
+    ctx_init(d, h, nullptr, 0, true, nullptr);
+    d.off = h->sv.fwd_end;
+    d.gr = grad;
+    d.touch = &touch;
+    int rc = net_bwd(d, dhq, dsr, has_dsr);
+    if (rc) return rc;
+    if (d.peak > ws_bytes) return fail(KDLAE_ESTATE, "training workspace too small for the backward");
+    nmarks = d.cur_mark;
+  }
+  // mark m closes the suffix [lo, total) when lo = the lowest offset written by mark m and every key
+  // at or above lo is untouched (its gradient is the zero fill) or last written by mark m
+  h->mark_slot.assign(nmarks, -1);
+  h->mark_lo.clear();
+  int64_t prev_lo = h->total;
+  for (int m = 0; m < nmarks; ++m) {
+    int64_t lo = h->total;
+    for (const auto& kv : touch)
+      if (kv.second.first <= m) { lo = kv.first; break; }  // map is offset-ordered: first hit = lowest
+    if (lo >= prev_lo) continue;
+    bool closed = true;
+    for (auto it = touch.lower_bound(lo); it != touch.end(); ++it)
+      if (it->second.second > m) { closed = false; break; }
+    if (!closed) continue;
+    h->mark_slot[m] = (int)h->mark_lo.size();
+    h->mark_lo.push_back(lo);
+    prev_lo = lo;
+  }
+  kdlae::DeviceGuard dg(h->device);
+  while (h->mark_ev.size() < h->mark_lo.size()) {
+    hipEvent_t e;
+    hipError_t er = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (er != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(er));
+    h->mark_ev.push_back(e);
+  }
+  Ctx c;
+  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
+  c.th = theta;
+  c.gr = grad;
+  c.off = h->sv.fwd_end;
+  c.record_marks = true;
+  hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
+  if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
+  return net_bwd(c, dhq, dsr, has_dsr);
+}
+
+int kdlae_tt_mark_count(const kdlae_tt_handle* h) { return h ? (int)h->mark_lo.size() : -1; }
+
+int64_t kdlae_tt_mark_lo(const kdlae_tt_handle* h, int j) {
+  return (h && j >= 0 && j < (int)h->mark_lo.size()) ? h->mark_lo[j] : -1;
+}
+
+int kdlae_tt_mark_wait(kdlae_tt_handle* h, int j, void* stream) {
+  if (!h || j < 0 || j >= (int)h->mark_lo.size()) return fail(KDLAE_EPARAM, "mark index out of range");
+  kdlae::DeviceGuard dg(h->device);
+  hipError_t e = hipStreamWaitEvent((hipStream_t)stream, h->mark_ev[j], 0);
+  return e == hipSuccess ? KDLAE_OK : fail(KDLAE_EHIP, hipGetErrorString(e));
+}
+
+int kdlae_tt_mark_sync(kdlae_tt_handle* h, int j) {
+  if (!h || j < 0 || j >= (int)h->mark_lo.size()) return fail(KDLAE_EPARAM, "mark index out of range");
+  kdlae::DeviceGuard dg(h->device);
+  hipError_t e = hipEventSynchronize(h->mark_ev[j]);
+  return e == hipSuccess ? KDLAE_OK : fail(KDLAE_EHIP, hipGetErrorString(e));
 }
 
 int64_t kdlae_train_l1sr_scratch_floats(void) { return 4 * 1024; }

@@ -26,7 +26,8 @@ import torch.distributed as dist
 
 from . import _lib
 
-__all__ = ["TrainEngine", "TeacherTrainFn", "L1LossSr", "KDLAETrainer", "MixingAugment", "sync_gradients"]
+__all__ = ["TrainEngine", "TeacherTrainFn", "L1LossSr", "KDLAETrainer", "MixingAugment", "sync_gradients",
+           "grad_buckets", "sync_gradients_bucketed"]
 
 
 def _vp(t):
@@ -132,14 +133,20 @@ class TrainEngine:
         self.generation += 1
         return hq, sr
 
-    def backward(self, theta, dhq, dsr, grad):
-        """d loss / d theta into ``grad`` (flat, overwritten) from the output gradients."""
+    def backward(self, theta, dhq, dsr, grad, marked=False):
+        """d loss / d theta into ``grad`` (flat, overwritten) from the output gradients.
+
+        ``marked``: also record the gradient-ready events of ``kdlae_tt_backward_marked``; returns
+        their suffix offsets (decreasing: the backward runs deepest-first, i.e. from the buffer's end)."""
         dhq = dhq.detach().to(torch.float32).contiguous() if dhq is not None else None
         dsr = dsr.detach().to(torch.float32).contiguous() if (dsr is not None and self.static_train) else None
-        rc = self._L.kdlae_tt_backward(self.handle, _vp(theta), _vp(dhq), _vp(dsr), _vp(grad), _vp(self.ws),
-                                       self.ws.numel(), _stream(grad.device))
-        _lib.check(rc, "kdlae_tt_backward")
-        return grad
+        fn = self._L.kdlae_tt_backward_marked if marked else self._L.kdlae_tt_backward
+        rc = fn(self.handle, _vp(theta), _vp(dhq), _vp(dsr), _vp(grad), _vp(self.ws), self.ws.numel(),
+                _stream(grad.device))
+        _lib.check(rc, "kdlae_tt_backward_marked" if marked else "kdlae_tt_backward")
+        if not marked:
+            return grad
+        return [int(self._L.kdlae_tt_mark_lo(self.handle, j)) for j in range(self._L.kdlae_tt_mark_count(self.handle))]
 
 
 class TeacherTrainFn(torch.autograd.Function):
@@ -300,6 +307,75 @@ def sync_gradients(grad: torch.Tensor, group=None) -> float:
     return 1.0 / ws
 
 
+def grad_buckets(mark_los, numel: int, cap_floats: int):
+    """DDP-style gradient buckets over the flat buffer from the backward's gradient-ready marks.
+
+    ``mark_los[j]``: the suffix [lo, numel) is final at mark j (decreasing).  Consecutive marks are
+    merged until a bucket holds ``cap_floats`` (DistributedDataParallel's bucket_cap_mb, 25 MB by
+    default); returns [(mark or None, lo, hi)] covering [0, numel) exactly, back to front.  A bucket
+    waits on its mark's event; None = after the whole backward."""
+    out, hi = [], numel
+    for j, lo in enumerate(mark_los):
+        if lo < hi and hi - lo >= cap_floats:
+            out.append((j, lo, hi))
+            hi = lo
+    if hi > 0:
+        last = len(mark_los) - 1 if mark_los and mark_los[-1] == 0 else None
+        out.append((last, 0, hi))
+    return out
+
+
+def sync_gradients_bucketed(grad: torch.Tensor, buckets, handle=None, group=None) -> float:
+    """The DDP all-reduce overlapped with the backward: bucket (j, lo, hi) of ``grad`` is all-reduced on
+    a communication stream as soon as the backward has recorded gradient-ready event j
+    (``kdlae_tt_mark_wait``), while the backward's later layers still run; the current stream then
+    waits for every bucket.  Returns the 1 / world-size scale, like ``sync_gradients``.  On gloo
+    (host collectives: the multi-process tests) each bucket waits for its event on the host."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1.0
+    ws = dist.get_world_size(group)
+    if ws == 1:
+        return 1.0
+    L = _lib.lib()
+    if grad.is_cuda and dist.get_backend(group) == "nccl":
+        comm = _comm_stream(grad.device)
+        cur = torch.cuda.current_stream(grad.device)
+        works = []
+        for j, lo, hi in buckets:
+            if j is None:
+                comm.wait_stream(cur)
+            else:
+                _lib.check(L.kdlae_tt_mark_wait(handle, j, ctypes.c_void_p(comm.cuda_stream)), "kdlae_tt_mark_wait")
+            with torch.cuda.stream(comm):
+                works.append(dist.all_reduce(grad[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True))
+        for w in works:
+            w.wait()
+        cur.wait_stream(comm)
+        return 1.0 / ws
+    for j, lo, hi in buckets:
+        if grad.is_cuda:
+            if j is None:
+                torch.cuda.synchronize(grad.device)
+            else:
+                _lib.check(L.kdlae_tt_mark_sync(handle, j), "kdlae_tt_mark_sync")
+        part = grad[lo:hi]
+        host = part.cpu() if grad.is_cuda else part
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        if grad.is_cuda:
+            part.copy_(host)
+    return 1.0 / ws
+
+
+_COMM = {}
+
+
+def _comm_stream(device):
+    key = torch.device(device).index
+    if key not in _COMM:
+        _COMM[key] = torch.cuda.Stream(device=device)
+    return _COMM[key]
+
+
 def _position_from_periods(iteration: int, cumulative_period) -> int:
     """get_position_from_periods (Train/basicsr/models/lr_scheduler.py:115-133)."""
     for i, period in enumerate(cumulative_period):
@@ -336,7 +412,8 @@ class KDLAETrainer:
     weight_decay 5e-5, betas (0.2, 0.999); use_grad_clip -> clip_grad_norm_(0.01); L1LossSr."""
 
     def __init__(self, model, lr=1e-5, weight_decay=0.5e-4, betas=(0.2, 0.999), eps=1e-8, use_grad_clip=True,
-                 max_norm=0.01, loss_weight=1.0, group=None, mixing_augs=None, ema_decay=0.0, scheduler=None):
+                 max_norm=0.01, loss_weight=1.0, group=None, mixing_augs=None, ema_decay=0.0, scheduler=None,
+                 bucket_cap_mb=25.0, overlap_grad_reduce=True):
         params = list(model.parameters())
         if not params or params[0].device.type != "cuda":
             raise RuntimeError("KDLAETrainer: move the model to a ROCm device first (no CPU fallback)")
@@ -360,6 +437,11 @@ class KDLAETrainer:
         self.max_norm = max_norm if use_grad_clip else 0.0
         self.loss_weight = loss_weight
         self.group = group
+        # DDP gradient buckets (DistributedDataParallel(bucket_cap_mb=25), base_model.py:76-82):
+        # all-reduced while the backward still runs; overlap_grad_reduce=False = one collective after it
+        self.bucket_cap_floats = max(1, int(bucket_cap_mb * 1024 * 1024 / 4))
+        self.overlap_grad_reduce = overlap_grad_reduce
+        self.buckets = None
         self.step_count = 0
         self.output = None
         self.loss = None
@@ -401,8 +483,13 @@ class KDLAETrainer:
         return {k: self.theta_ema[off:off + n].view(p.shape)
                 for (k, n, off), p in zip(self.engine.keys, self.model.parameters())}
 
-    def forward_backward(self, lq: dict, gt: dict):
-        """preds = net_g(lq); l_pix = cri_pix(preds, gt); l_pix.backward()  (:198-213)."""
+    def _distributed(self) -> bool:
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def forward_backward(self, lq: dict, gt: dict, marked: bool = False):
+        """preds = net_g(lq); l_pix = cri_pix(preds, gt); l_pix.backward()  (:198-213).
+
+        ``marked``: record gradient-ready marks and build ``self.buckets`` for the overlapped all-reduce."""
         eng, L = self.engine, _lib.lib()
         hq, sr = eng.forward(self.theta, lq["img"], lq.get("denoise_rate"))
         self.output = {"hq": hq, "sr": sr}
@@ -418,7 +505,11 @@ class KDLAETrainer:
             dhq.mul_(self.loss_weight)
             if dsr is not None:
                 dsr.mul_(self.loss_weight)
-        eng.backward(self.theta, dhq, dsr, self.grad)
+        if marked:
+            self.buckets = grad_buckets(eng.backward(self.theta, dhq, dsr, self.grad, marked=True), eng.numel,
+                                        self.bucket_cap_floats)
+        else:
+            eng.backward(self.theta, dhq, dsr, self.grad)
         self.loss = self._loss * self.loss_weight
         return self.loss
 
@@ -438,9 +529,14 @@ class KDLAETrainer:
             _lib.check(rc, "kdlae_train_ema")
 
     def optimize_parameters(self, lq: dict, gt: dict):
-        """One full iteration: forward, L1LossSr, backward, DDP all-reduce, clip, AdamW."""
-        loss = self.forward_backward(lq, gt)
-        gscale = sync_gradients(self.grad, self.group)
+        """One full iteration: forward, L1LossSr, backward, DDP all-reduce, clip, AdamW.  With several
+        ranks the all-reduce runs in gradient buckets overlapped with the backward (overlap_grad_reduce)."""
+        if self._distributed() and self.overlap_grad_reduce:
+            loss = self.forward_backward(lq, gt, marked=True)
+            gscale = sync_gradients_bucketed(self.grad, self.buckets, self.engine.handle, self.group)
+        else:
+            loss = self.forward_backward(lq, gt)
+            gscale = sync_gradients(self.grad, self.group)
         self.step(gscale)
         return loss
 

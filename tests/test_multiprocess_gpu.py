@@ -5,7 +5,8 @@ fresh processes (one per rank, as torchrun launches them), rendezvous over gloo 
   single-process bs=4 run bit for bit (every image's reductions are batch-independent).
 * Training: ``KDLAETrainer.optimize_parameters`` with the DDP-style flat-gradient all-reduce
   (``sync_gradients``, base_model.py:76-82) on 2 + 2 images: both ranks end with identical
-  parameters, and the averaged gradient matches the single-process bs=4 gradient.
+  parameters, and the averaged gradient matches the single-process bs=4 gradient; the bucketed
+  all-reduce behind the backward's gradient-ready marks gives the same parameters bit for bit.
 """
 import os
 import socket
@@ -68,6 +69,13 @@ def _worker(rank, world, port, q):
         res["grad_mean"] = (tr.grad * scale).cpu()
         tr.step(scale)
         res["theta"] = tr.theta.detach().cpu()
+        # the same step through optimize_parameters: with two ranks it takes the bucketed all-reduce
+        # driven by the backward's gradient-ready marks (tiny buckets: many collectives)
+        tm2 = _model().train()
+        tr2 = KDLAETrainer(tm2, lr=1e-3, bucket_cap_mb=0.02)
+        tr2.optimize_parameters(lq, {k: v[s:e].cuda() for k, v in gt.items()})
+        res["theta_bucketed"] = tr2.theta.detach().cpu()
+        res["nbuckets"] = len(tr2.buckets)
         q.put((rank, res))
         dist.destroy_process_group()
     except Exception as ex:  # surface the failure in the parent instead of hanging on the queue
@@ -100,6 +108,10 @@ def test_two_processes_share_the_gpu():
         assert isinstance(res[r], dict), res[r]
         assert torch.equal(res[r]["hq"], ref["hq"]) and torch.equal(res[r]["sr"], ref["sr"])
     assert torch.equal(res[0]["theta"], res[1]["theta"])
+    for r in range(2):
+        print(f"rank {r}: {res[r]['nbuckets']} gradient buckets")
+        assert res[r]["nbuckets"] > 3
+        assert torch.equal(res[r]["theta_bucketed"], res[r]["theta"])  # bucketed == one all-reduce
     err = float((res[0]["grad_mean"] - g_ref).abs().max() / g_ref.abs().max())
     print(f"2-rank mean gradient vs single-process bs=4: {err:.3e} of max |g|")
     assert err <= 1e-4

@@ -174,6 +174,58 @@ def test_sync_gradients_gloo_world2():
         np.testing.assert_allclose(vals, mean)
 
 
+def test_grad_buckets_cover_the_buffer():
+    """DDP-style buckets from gradient-ready marks: contiguous, back to front, exactly [0, numel), each
+    closed by a mark whose suffix contains it, merged up to the cap."""
+    from rethink_acoustic_image_enhancement_amd.train import grad_buckets
+    marks = [990, 950, 900, 700, 690, 400, 120, 0]
+    for cap in (1, 30, 100, 250, 5000):
+        bk = grad_buckets(marks, 1000, cap)
+        hi = 1000
+        for j, lo, b_hi in bk:
+            assert b_hi == hi and lo < b_hi
+            if j is not None:
+                assert marks[j] <= lo  # the mark's final suffix covers the bucket
+            hi = lo
+        assert hi == 0
+        assert all(b_hi - lo >= cap for j, lo, b_hi in bk[:-1])
+    assert grad_buckets(marks, 1000, 1) == [(j, lo, hi) for j, (lo, hi) in
+                                            enumerate(zip(marks, [1000] + marks[:-1]))]
+    # a backward whose last mark does not reach offset 0: the remainder waits for the whole backward
+    assert grad_buckets([800, 300], 1000, 100)[-1] == (None, 0, 300)
+
+
+def _bucket_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from rethink_acoustic_image_enhancement_amd.train import grad_buckets, sync_gradients_bucketed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(rank)
+    grad = torch.randn(1000, generator=g)
+    full = grad.clone()
+    dist.all_reduce(full)
+    bk = grad_buckets([990, 950, 900, 700, 690, 400, 120, 0], 1000, 100)
+    scale = sync_gradients_bucketed(grad, bk)
+    q.put((rank, scale, bool(torch.equal(grad, full)), len(bk)))
+    dist.destroy_process_group()
+
+
+def test_sync_gradients_bucketed_gloo_world2():
+    """Bucket-by-bucket all-reduce over gloo equals one all-reduce of the whole buffer, bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, scale, same, nb in res:
+        assert scale == 0.5 and same and nb > 1
+
+
 def test_sync_gradients_single_process_is_identity():
     g = torch.ones(4)
     assert sync_gradients(g) == 1.0
