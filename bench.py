@@ -454,7 +454,9 @@ def main():
         res["per_gpu"] = {"images_per_s": round(ips, 3),
                           "hbm_roof_frac_survey_def": round(ips * 150.70e9 / 8.0e12, 4),
                           "fp32_compute_frac": round(ips * 1.9177e12 / 157.3e12, 4),
-                          "sigma_max_roof_frac": round(ips / 41.8, 4)}  # SURVEY §8d per-op Σmax roof
+                          # SURVEY §8d's per-op Σmax roof (41.8 img/s) prices every aten op's own HBM
+                          # traffic; the fused kernels move less than that model, so >1 is possible
+                          "vs_survey_unfused_sigma_max_roof": round(ips / 41.8, 4)}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"], res["parity"] = cpu_baseline(model, batch, out, args.cpu_threads)
@@ -468,9 +470,9 @@ def pmc_traffic(cls):
     """HBM bytes per launch of a kernel class from the committed rocprofv3 PMC summary
     (profiles/*pmc_traffic*.json, produced by tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE)."""
     import glob
-    def version(path):  # r01_pmc_traffic_v13.json -> (13,): numeric, so v13 sorts after v9
-        m = re.search(r"_v(\d+)\.json$", path)
-        return (int(m.group(1)) if m else -1, path)
+    def version(path):  # r02_pmc_traffic_v3.json -> (2, 3): numeric, round first, so r02 v3 > r01 v16
+        m = re.search(r"r(\d+)_pmc_traffic_v(\d+)\.json$", path)
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), key=version)
     if not files:
