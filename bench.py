@@ -389,8 +389,19 @@ def main():
     roof = None
     if args.probe:
         import ctypes
+        import tempfile
         ms, n, by, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        dump = os.environ.get("KDLAE_PROBE_DUMP")
+        own_dump = dump is None
+        if own_dump:  # per-launch records for the class's per-shape roof (removed afterwards)
+            fd, dump = tempfile.mkstemp(suffix=".csv")
+            os.close(fd)
+            os.environ["KDLAE_PROBE_DUMP"] = dump
         L.kdlae_t_probe_read(eng.handle, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(by), ctypes.byref(fl))
+        launch_roof = per_launch_roof(dump)
+        if own_dump:
+            del os.environ["KDLAE_PROBE_DUMP"]
+            os.unlink(dump)
         L.kdlae_t_probe_arm(eng.handle, 0, 0)
         if n.value:
             sec = ms.value / 1e3
@@ -405,6 +416,8 @@ def main():
             tr = pmc_traffic(args.probe)
             if tr is not None:
                 roof["traffic"], roof["traffic_source"] = tr
+            if launch_roof is not None:
+                roof["per_shape_roof"] = launch_roof
             roof.update({"kernel": PROBE_CLASSES[args.probe], "launches": int(n.value),
                          "avg_launch_us": round(ms.value * 1e3 / n.value, 2),
                          "share_of_step": round(ms.value / 1e3 / elapsed, 4),
@@ -464,6 +477,28 @@ def main():
         print(json.dumps(res), flush=True)
     if distributed:
         dist.destroy_process_group()
+
+
+def per_launch_roof(path):
+    """The class against each launch's own roof: sum over launches of max(FLOPs / MFMA peak,
+    algorithmic bytes / HBM peak), divided by the summed measured time.  A class that mixes
+    MFMA-bound and HBM-bound shapes (the 1x1 GEMMs at K = 48 are HBM-bound) cannot reach its MFMA
+    fraction; this is the fraction of the time its launches would take at their own bound."""
+    import csv
+    try:
+        rows = list(csv.DictReader(open(path)))
+    except OSError:
+        return None
+    if not rows:
+        return None
+    t = sum(float(r["ms"]) for r in rows) / 1e3
+    bound = sum(max(float(r["flops"]) / (PEAK_FP32_TFLOPS * 1e12), float(r["bytes"]) / (PEAK_HBM_GBS * 1e9))
+                for r in rows)
+    mfma_bound = sum(1 for r in rows
+                     if float(r["flops"]) / (PEAK_FP32_TFLOPS * 1e12) >= float(r["bytes"]) / (PEAK_HBM_GBS * 1e9))
+    return {"frac": round(bound / t, 4), "bound_ms": round(bound * 1e3, 2), "measured_ms": round(t * 1e3, 2),
+            "launches_mfma_bound": mfma_bound, "launches_hbm_bound": len(rows) - mfma_bound,
+            "definition": "sum_i max(flops_i / mfma_peak, bytes_i / hbm_peak) / sum_i t_i (HIP events)"}
 
 
 def pmc_traffic(cls):

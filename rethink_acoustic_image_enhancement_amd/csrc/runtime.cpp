@@ -73,6 +73,17 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
   }
   double best = 1e30;
   const bool v2 = gemm_chunk2_enabled();
+  // A/B hook: KDLAE_C3_VARIANT=<NT>x<KG> forces that chunk shape on every implicit 3x3 layer it exists for
+  static const char* c3v = getenv("KDLAE_C3_VARIANT");
+  if (c3v && g.ksize == 3) {
+    int fnt = 0, fkg = 0;
+    if (sscanf(c3v, "%dx%d", &fnt, &fkg) == 2 && (v2 ? gemm_has_variant2(fnt, fkg, true, g.out_mode)
+                                                     : gemm_has_variant(fnt, fkg, true, 2, false, g.out_mode))) {
+      g.NT = fnt;
+      g.KG = fkg;
+      return;
+    }
+  }
   for (int nt : nts)
     for (int kg : kgs) {
       if (v2 ? !gemm_has_variant2(nt, kg, g.ksize == 3, g.out_mode) || (g.has_res && nt * kg > 36)
