@@ -519,6 +519,144 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Fused attention output + FFN input, r02 (C = 48 blocks: one head, one resident weight group):
+//   x1  = x + M v (+ bias_m)        M = W_proj blockdiag(A) per image (attn_fold; :140-144, :160)
+//   out = LN(x1) W_in^T (+ bias)     LayerNorm + ffn.project_in (:161, :99), chunk-interleaved rows
+// in one pass over the pixel tiles.  The M GEMM's accumulator (lane: pixel li, channels 4 lq..+3 of
+// output tile t) IS the A-row layout of the second GEMM (k-group t), so x1 goes from the MFMA
+// accumulators through the residual add and LayerNorm into the project_in MFMAs without leaving
+// registers; it is stored once (the FFN's residual) and never re-read.  The unfused pair wrote x1,
+// then read it back, and its N = 48 GEMM ran at ~4.5 TB/s / 36 TF/s.
+// Numerics: both GEMMs accumulate k-group-major, k-step-minor exactly as gemm_res_kernel does, and
+// x1 = (acc + bias_m) + x in that order, so the result equals the unfused path bit for bit.
+template <int NT, int KG, int NCH>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lq = lane >> 4;
+  const int HW = p.F * p.H * p.W;
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
+  if (t_begin >= t_end) return;
+  constexpr int TP = NT * NCH;       // project_in tiles staged (zero weights past ntiles)
+  f32x4* ml = wlds + TP * KG * 64 + TP * 4;  // M fragments [KG tiles][KG groups][64], then bias_m [KG][4]
+  {
+    const f32x4* wbase = reinterpret_cast<const f32x4*>(p.Wp);
+    const int n4 = p.ntiles * KG * 64;
+    for (int idx = tid; idx < TP * KG * 64; idx += kGemmThreads)
+      wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int idx = tid; idx < TP * 4; idx += kGemmThreads) {
+      const int n = 4 * idx;
+      wlds[TP * KG * 64 + idx] = (p.bias && idx < p.ntiles * 4 && n < p.N)
+                                     ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  auto stage_m = [&](int b) {
+    const f32x4* mb = reinterpret_cast<const f32x4*>(p.Wm + (long long)b * p.wm_img_stride);
+    for (int idx = tid; idx < KG * KG * 64; idx += kGemmThreads) ml[idx] = mb[idx];
+    for (int idx = tid; idx < KG * 4; idx += kGemmThreads)
+      ml[KG * KG * 64 + idx] = p.bias_m ? *reinterpret_cast<const f32x4*>(p.bias_m + 4 * idx) : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  int staged = t_begin / p.tiles_per_img;
+  stage_m(staged);
+  __syncthreads();
+  const unsigned a_bytes = (unsigned)HW * (unsigned)p.lda * 4u;
+  const unsigned o_bytes = (unsigned)HW * (unsigned)p.ldo * 4u;
+  const unsigned r_bytes = (unsigned)HW * (unsigned)p.ldr * 4u;
+  const unsigned o1_bytes = (unsigned)HW * (unsigned)p.ldo1 * 4u;
+  auto tile_voff = [&](int t, unsigned v, unsigned bytes) -> int {
+    return (int)(((t < p.ntiles) ? v : bytes) + 64u * (unsigned)t);
+  };
+  auto rows_of = [&](int tile, int& b, int& row0) {
+    b = tile / p.tiles_per_img;
+    row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
+  };
+  auto load_rows = [&](const float* base, int ld, unsigned bytes, int tile, f32x4 (&dst)[kGemmRT][KG]) {
+    int b, row0;
+    rows_of(tile, b, row0);
+    const __amdgpu_buffer_rsrc_t ra = buf_rsrc(base + (long long)b * HW * ld, bytes);
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r) {
+      const unsigned pix = (unsigned)(row0 + r * 16 + li);
+      const unsigned off = pix < (unsigned)HW ? pix * (unsigned)ld * 4u + 16u * lq : kOOB;
+#pragma unroll
+      for (int g = 0; g < KG; ++g) dst[r][g] = buf_load4(ra, off + 64u * g);
+    }
+  };
+  f32x4 a[kGemmRT][KG], an[kGemmRT][KG];
+  load_rows(p.A, p.lda, a_bytes, t_begin, an);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    int b, row0;
+    rows_of(tile, b, row0);
+    if (b != staged) {  // block-uniform: the tile range crossed into the next image
+      __syncthreads();
+      stage_m(b);
+      __syncthreads();
+      staged = b;
+    }
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r)
+#pragma unroll
+      for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
+    // x of this tile (read before x1 overwrites the same rows, by the same lanes), waited for after
+    // the M GEMM; a one-tile-ahead prefetch of x measured no faster (registers)
+    f32x4 xr[kGemmRT][KG];
+    load_rows(p.R, p.ldr, r_bytes, tile, xr);
+    load_rows(p.A, p.lda, a_bytes, min(tile + 1, t_end - 1), an);  // next tile's v
+    {
+      f32x4 acc1[KG][kGemmRT];
+#pragma unroll
+      for (int t = 0; t < KG; ++t)
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) acc1[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_chunk<KG, KG>(ml, KG, lane, a, acc1);
+      const f32x4* bm = ml + KG * KG * 64;
+      const __amdgpu_buffer_rsrc_t r1 = buf_rsrc(p.out1 + (long long)b * HW * p.ldo1, o1_bytes);
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r) {
+        const unsigned pix = (unsigned)(row0 + r * 16 + li);
+        const unsigned off = pix < (unsigned)HW ? pix * (unsigned)p.ldo1 * 4u + 16u * lq : o1_bytes;
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+          f32x4 v = acc1[g][r] + bm[4 * g + lq];
+          v += xr[r][g];
+          a[r][g] = v;
+          buf_store4(r1, off + 64u * g, v);
+        }
+      }
+    }
+    apply_ln<KG>(p, b, row0, li, HW, a);
+    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
+    unsigned vo[kGemmRT];
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r) {
+      const unsigned pix = (unsigned)(row0 + r * 16 + li);
+      vo[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldo * 4u + 16u * lq : o_bytes;
+    }
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      f32x4 acc[NT][kGemmRT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_chunk<NT, KG>(wlds + (size_t)ch * NT * KG * 64, KG, lane, a, acc);
+      const f32x4* bl = wlds + TP * KG * 64 + ch * NT * 4;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f32x4 bias = bl[4 * t + lq];
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t][r] + bias), ro,
+                                                 tile_voff(ch * NT + t, vo[r], o_bytes), 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Chunked schedule, r02 (deep 1x1 layers with K > the LDS budget, every implicit 3x3 / 3x3x3 conv):
 // the block walks its pixel tiles x k-chunks as one sequence of steps.  Per step:
 //   s_waitcnt vmcnt(0) + barrier   (this step's weights and A rows were issued one step earlier);
@@ -791,6 +929,17 @@ static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_
   X(1, 9, true, 0) X(2, 9, true, 0) X(4, 9, true, 0) X(8, 6, true, 0) X(4, 6, true, 0) X(2, 6, true, 0) \
   X(4, 4, false, 2) X(8, 4, false, 2) X(4, 2, false, 2) X(3, 3, false, 2)
 
+// (NT, KG, NCH) of the fused attention-output + project_in kernel (C = 48: K = 3 groups)
+#define KDLAE_GEMM_ATTN_IN_VARIANTS(X) X(8, 3, 2) X(9, 3, 2) X(6, 3, 3)
+
+bool gemm_attn_in_variant(int NT, int KG, int nch) {
+#define X(a, b, c) \
+  if (NT == a && KG == b && nch == c) return true;
+  KDLAE_GEMM_ATTN_IN_VARIANTS(X)
+#undef X
+  return false;
+}
+
 bool gemm_chunk2_enabled() {
   static const bool off = getenv("KDLAE_GEMM_CHUNK1") != nullptr;  // A/B hook: the r01 chunked kernel
   return !off;
@@ -840,6 +989,33 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
   const bool c3 = p.ksize == 3;
   const bool res = p.group_tiles > 0;
   if (p.ln && !p.stats && (p.kchunks > 1 || p.kgroups > KG)) return hipErrorInvalidValue;  // LN needs whole rows
+  if (p.Wm) {  // fused attention output + LN + GEMM: one resident group, K = N of the M GEMM = C
+    const int nch = (p.ntiles + NT - 1) / NT;
+    const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64 + (size_t)KG * KG * 1024 + (size_t)KG * 64;
+    const long long HW = (long long)p.F * p.H * p.W;
+    const long long mx = HW * std::max({p.lda, p.ldo, p.ldr, p.ldo1}) * 4;
+    if (!res || c3 || p.out_mode || p.group_tiles < p.ntiles || p.kgroups != KG || p.kchunks != 1 || p.relu ||
+        !p.R || !p.out1 || p.stats || mx >= (1LL << 31) || lds > 160 * 1024 || p.lda % 4 || p.ldo % 4 || p.ldr % 4 ||
+        p.ldo1 % 4)
+      return hipErrorInvalidValue;
+#define X(a, b, c)                                                                                            \
+    if (NT == a && KG == b && nch == c) {                                                                     \
+      static size_t attr_lds[64] = {};                                                                        \
+      int dev = 0;                                                                                            \
+      if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;                                  \
+      if (lds > attr_lds[dev]) {                                                                              \
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_attn_in_kernel<a, b, c>),      \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);             \
+        if (e != hipSuccess) return e;                                                                        \
+        attr_lds[dev] = lds;                                                                                  \
+      }                                                                                                       \
+      hipLaunchKernelGGL((gemm_attn_in_kernel<a, b, c>), dim3(grid_x, 1), dim3(kGemmThreads), lds, s, p);    \
+      return hipGetLastError();                                                                               \
+    }
+    KDLAE_GEMM_ATTN_IN_VARIANTS(X)
+#undef X
+    return hipErrorInvalidValue;
+  }
   if (res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && !p.relu && use_res2()) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;

@@ -32,6 +32,7 @@ struct BlockW {
   size_t dwffn = kNone, dwffn_b = kNone;
   bool fused_gdfn = false;  // project_in output chunk-interleaved; dwconv+gate+project_out in one kernel
   bool fused_ffn = false;   // the whole FFN (LN + project_in + dwconv + gate + project_out) in one kernel
+  bool fused_attn_in = false;  // x1 = x + M v, LN and project_in in one GEMM kernel (gemm_attn_in_kernel)
 };
 
 }  // namespace kdlae
@@ -337,6 +338,11 @@ struct Packer {
     choose_variant(b.pout, false);
     // opt-in (KDLAE_FFN_FUSION=1): measured 1.8x slower than project_in GEMM + gdfn_out in r02 v1
     b.fused_ffn = fz && ffn_fused_supported(C, hidS) && getenv("KDLAE_FFN_FUSION") != nullptr;
+    // attention output + FFN input in one pass where project_in is one resident weight group
+    // (C = 48); KDLAE_NO_ATTN_IN_FUSION=1 keeps the two GEMMs (A/B hook)
+    b.fused_attn_in = b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 && b.pin.WPE == 2 &&
+                      gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.ntiles + b.pin.NT - 1) / b.pin.NT) &&
+                      !getenv("KDLAE_NO_ATTN_IN_FUSION");
     return b;
   }
 
@@ -535,9 +541,45 @@ struct Fwd {
     if ((rc = probe_end(2, b.C, 4.0 * P * 4 * b.C, 2.0 * P * (27.0 * b.C + (double)b.C * b.Ch)))) return rc;
     HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
     HIPCHK(launch_attn_fold(buf(pl.red), gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
-    rc = gemm(b.proj_gemm, buf(pl.Mp), (long long)b.C * b.C, View{buf(pl.vbuf), b.C}, Hh, Ww, x, 0, x.p, x.ld, 0,
-              0, b.C);
-    if (rc) return rc;
+    View fpre{buf(pl.fpre), 2 * b.hidS};
+    const bool fuse_in = b.fused_attn_in && !(b.fused_ffn && alt.p);
+    if (fuse_in) {
+      // x1 = x + M v written back into x, LN(x1) -> project_in into fpre, one kernel
+      GemmCall c;
+      c.g = &b.pin;
+      c.W = h->P(b.pin.w);
+      c.bias = h->P(b.pin.bias);
+      c.in = View{buf(pl.vbuf), b.C};
+      c.out = fpre;
+      c.B = B;
+      c.F = 1;
+      c.H = Hh;
+      c.Wd = Ww;
+      c.R = x.p;
+      c.ldr = x.ld;
+      c.ln = ln;
+      c.ln_C = b.C;
+      c.stats_buf = buf(pl.stats);
+      c.Wm = buf(pl.Mp);
+      c.wm_img_stride = (long long)b.C * b.C;
+      c.bias_m = h->P(b.proj_b);
+      c.out1 = x;
+      if ((rc = probe_begin(1, b.C))) return rc;
+      if (h->probe_class == 1)
+        tag = "gemm C" + std::to_string(b.C) + " HW" + std::to_string(HW) + " N" + std::to_string(b.pin.n_true) +
+              " K" + std::to_string(b.C) + " attn_out+ln+project_in v" + std::to_string(b.pin.NT) + "x" +
+              std::to_string(b.pin.KG);
+      if ((rc = run_gemm(c, s))) return rc;
+      const double Pd = (double)P;
+      // read v and x, write x1 and the project_in rows; M per image + W_in; both GEMMs' FLOPs
+      const double bytes = 4.0 * (Pd * 3.0 * b.C + Pd * b.pin.n_true + (double)B * b.C * b.C +
+                                  (double)b.pin.n_true * b.C);
+      if ((rc = probe_end(1, b.C, bytes, 2.0 * Pd * ((double)b.C * b.C + (double)b.C * b.pin.n_true)))) return rc;
+    } else {
+      rc = gemm(b.proj_gemm, buf(pl.Mp), (long long)b.C * b.C, View{buf(pl.vbuf), b.C}, Hh, Ww, x, 0, x.p, x.ld, 0,
+                0, b.C);
+      if (rc) return rc;
+    }
     // --- feed-forward
     if (b.fused_ffn && alt.p) {
       FfnParams fp{};
@@ -564,9 +606,10 @@ struct Fwd {
       return probe_end(3, b.C, 4.0 * P * 3.0 * b.C,
                        2.0 * P * (2.0 * b.hid * b.C + 18.0 * b.hid + (double)b.hid * b.C));
     }
-    View fpre{buf(pl.fpre), 2 * b.hidS};
-    rc = gemm(b.pin, h->P(b.pin.w), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
-    if (rc) return rc;
+    if (!fuse_in) {
+      rc = gemm(b.pin, h->P(b.pin.w), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
+      if (rc) return rc;
+    }
     if (b.fused_gdfn) {
       GdfnParams gd{};
       gd.x = fpre.p;

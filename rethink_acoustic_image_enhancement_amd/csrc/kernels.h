@@ -41,6 +41,11 @@ struct GemmParams {
   int kchunks;
   int group_tiles;                 // resident schedule: output tiles whose weights one block keeps in LDS
   int F, kt;                       // frames per sequence (1 for 2-D) and temporal taps (1, or 3 for Conv3d)
+  // fused attention output (gemm_attn_in_kernel): A = v rows, R = the block input x; the kernel
+  // forms x1 = x + M v (+ bias_m) with the per-image folded projection M (KDLAE_model.py:140-144,
+  // :160), stores x1 to out1, and runs LN + the GEMM on x1 (:161, :99) — x1 never round-trips HBM
+  const float* Wm; long long wm_img_stride; const float* bias_m;
+  float* out1; int ldo1;
 };
 
 struct GramParams {
@@ -86,6 +91,7 @@ struct SmallOutParams {            // 3x3 (ks=3) or pointwise (ks=1) conv with C
   const float* extra;                  // NCHW [B,1,H,W] copied into channel Cout (NHWC mode) or null
 };
 
+bool gemm_attn_in_variant(int NT, int KG, int nch);
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s);
 bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident, int out_mode);
 bool gemm_chunk2_enabled();

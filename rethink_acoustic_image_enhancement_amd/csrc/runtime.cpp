@@ -159,7 +159,7 @@ std::vector<float> ParamStore::flat() const {
 int run_gemm(const GemmCall& c, hipStream_t s) {
   const Gemm& g = *c.g;
   const long long HW = (long long)c.F * c.H * c.Wd;
-  const int ldmax = std::max({c.in.ld, c.out.ld, c.ldr});
+  const int ldmax = std::max({c.in.ld, c.out.ld, c.ldr, c.out1.ld});
   if (HW * ldmax * (c.out_mode == 2 ? 4 : 1) >= (1LL << 31))
     return fail(KDLAE_EINVAL_SHAPE, "image too large for 32-bit in-image offsets");
   GemmParams p{};
@@ -191,6 +191,11 @@ int run_gemm(const GemmCall& c, hipStream_t s) {
   p.total_tiles = c.B * p.tiles_per_img;
   p.kchunks = g.group_tiles ? 1 : (int)ceil_div(g.kgroups, g.KG);
   p.group_tiles = g.group_tiles;
+  p.Wm = c.Wm;
+  p.wm_img_stride = c.wm_img_stride;
+  p.bias_m = c.bias_m;
+  p.out1 = c.out1.p;
+  p.ldo1 = c.out1.ld;
   p.stats = nullptr;
   if (c.ln && (p.kchunks > 1 || g.kgroups * 16 != c.ln_C)) {
     if (!c.stats_buf) return fail(KDLAE_ESTATE, "LN GEMM needs a stats buffer");

@@ -166,6 +166,11 @@ struct GemmCall {
   int relu = 0;
   int ln = 0, ln_C = 0;
   float* stats_buf = nullptr;  // scratch [P][2] used when LN needs precomputed row stats
+  // fused attention output (GemmParams::Wm): in = v, R = x, out1 = where x1 goes (x itself)
+  const float* Wm = nullptr;
+  long long wm_img_stride = 0;
+  const float* bias_m = nullptr;
+  View out1{nullptr, 0};
 };
 int run_gemm(const GemmCall& c, hipStream_t s);
 // Compute units of the current device (256 on MI355X) and the tail-aware GEMM grid split.
