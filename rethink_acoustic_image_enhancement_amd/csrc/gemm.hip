@@ -584,8 +584,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
       for (int g = 0; g < KG; ++g) dst[r][g] = buf_load4(ra, off + 64u * g);
     }
   };
-  f32x4 a[kGemmRT][KG], an[kGemmRT][KG];
-  load_rows(p.A, p.lda, a_bytes, t_begin, an);
+  // v rows are prefetched a tile ahead at K = 48; at K = 96 the extra 48 VGPRs would spill, and the
+  // SIMD partner wave's MFMAs cover the load instead
+  constexpr bool PFV = KG < 6;
+  f32x4 a[kGemmRT][KG];
+  [[maybe_unused]] f32x4 an[kGemmRT][KG];
+  if constexpr (PFV) load_rows(p.A, p.lda, a_bytes, t_begin, an);
   for (int tile = t_begin; tile < t_end; ++tile) {
     int b, row0;
     rows_of(tile, b, row0);
@@ -595,15 +599,20 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
       __syncthreads();
       staged = b;
     }
+    if constexpr (PFV) {
 #pragma unroll
-    for (int r = 0; r < kGemmRT; ++r)
+      for (int r = 0; r < kGemmRT; ++r)
 #pragma unroll
-      for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
+        for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
+    } else {
+      load_rows(p.A, p.lda, a_bytes, tile, a);
+    }
     // x of this tile (read before x1 overwrites the same rows, by the same lanes), waited for after
-    // the M GEMM; a one-tile-ahead prefetch of x measured no faster (registers)
+    // the M GEMM; a one-tile-ahead prefetch of x measured no faster (registers).  At K = 96 the
+    // x rows are loaded after the M GEMM: live across it they would spill
     f32x4 xr[kGemmRT][KG];
-    load_rows(p.R, p.ldr, r_bytes, tile, xr);
-    load_rows(p.A, p.lda, a_bytes, min(tile + 1, t_end - 1), an);  // next tile's v
+    if constexpr (KG < 6) load_rows(p.R, p.ldr, r_bytes, tile, xr);
+    if constexpr (PFV) load_rows(p.A, p.lda, a_bytes, min(tile + 1, t_end - 1), an);  // next tile's v
     {
       f32x4 acc1[KG][kGemmRT];
 #pragma unroll
@@ -611,6 +620,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r) acc1[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
       mfma_chunk<KG, KG>(ml, KG, lane, a, acc1);
+      if constexpr (KG >= 6) load_rows(p.R, p.ldr, r_bytes, tile, xr);
       const f32x4* bm = ml + KG * KG * 64;
       const __amdgpu_buffer_rsrc_t r1 = buf_rsrc(p.out1 + (long long)b * HW * p.ldo1, o1_bytes);
 #pragma unroll
@@ -930,7 +940,7 @@ static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_
   X(4, 4, false, 2) X(8, 4, false, 2) X(4, 2, false, 2) X(3, 3, false, 2)
 
 // (NT, KG, NCH) of the fused attention-output + project_in kernel (C = 48: K = 3 groups)
-#define KDLAE_GEMM_ATTN_IN_VARIANTS(X) X(8, 3, 2) X(9, 3, 2) X(6, 3, 3)
+#define KDLAE_GEMM_ATTN_IN_VARIANTS(X) X(8, 3, 2) X(9, 3, 2) X(6, 3, 3) X(8, 6, 2)
 
 bool gemm_attn_in_variant(int NT, int KG, int nch) {
 #define X(a, b, c) \

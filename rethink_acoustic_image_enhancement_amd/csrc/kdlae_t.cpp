@@ -33,6 +33,10 @@ struct BlockW {
   bool fused_gdfn = false;  // project_in output chunk-interleaved; dwconv+gate+project_out in one kernel
   bool fused_ffn = false;   // the whole FFN (LN + project_in + dwconv + gate + project_out) in one kernel
   bool fused_attn_in = false;  // x1 = x + M v, LN and project_in in one GEMM kernel (gemm_attn_in_kernel)
+  // when project_in needs two resident weight groups (C = 96): the fused kernel runs group 0 (and
+  // forms x1), a plain LN GEMM on x1 runs group 1
+  bool attn_in_split = false;
+  Gemm pin_g0, pin_g1;
 };
 
 }  // namespace kdlae
@@ -340,9 +344,29 @@ struct Packer {
     b.fused_ffn = fz && ffn_fused_supported(C, hidS) && getenv("KDLAE_FFN_FUSION") != nullptr;
     // attention output + FFN input in one pass where project_in is one resident weight group
     // (C = 48); KDLAE_NO_ATTN_IN_FUSION=1 keeps the two GEMMs (A/B hook)
+    const bool no_ai = getenv("KDLAE_NO_ATTN_IN_FUSION") != nullptr;
     b.fused_attn_in = b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 && b.pin.WPE == 2 &&
-                      gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.ntiles + b.pin.NT - 1) / b.pin.NT) &&
-                      !getenv("KDLAE_NO_ATTN_IN_FUSION");
+                      gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.ntiles + b.pin.NT - 1) / b.pin.NT) && !no_ai;
+    // C = 96 (two weight groups): the fused kernel on group 0 + a plain LN GEMM on group 1 measured a
+    // wash (profiles/r02_attn_in_probe.txt: 4637 vs 4598 us at 512^2), so it stays behind
+    // KDLAE_ATTN_IN_SPLIT=1
+    if (!b.fused_attn_in && !no_ai && getenv("KDLAE_ATTN_IN_SPLIT") && b.pin.group_tiles > 0 &&
+        b.pin.group_tiles < b.pin.ntiles && 2 * b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 &&
+        b.pin.WPE == 2 && gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.group_tiles + b.pin.NT - 1) / b.pin.NT)) {
+      const int gt = b.pin.group_tiles;
+      b.pin_g0 = b.pin;
+      b.pin_g0.ntiles = gt;
+      b.pin_g0.N = 16 * gt;
+      b.pin_g0.n_true = (int)((long long)b.pin.n_true * gt / b.pin.ntiles);
+      b.pin_g1 = b.pin;
+      b.pin_g1.w = b.pin.w + (size_t)gt * b.pin.kgroups * 256;
+      if (b.pin.bias != kNone) b.pin_g1.bias = b.pin.bias + (size_t)16 * gt;
+      b.pin_g1.ntiles = b.pin.ntiles - gt;
+      b.pin_g1.N = b.pin.N - 16 * gt;
+      b.pin_g1.n_true = b.pin.n_true - b.pin_g0.n_true;
+      b.pin_g1.group_tiles = b.pin_g1.ntiles;
+      b.fused_attn_in = b.attn_in_split = true;
+    }
     return b;
   }
 
@@ -545,10 +569,11 @@ struct Fwd {
     const bool fuse_in = b.fused_attn_in && !(b.fused_ffn && alt.p);
     if (fuse_in) {
       // x1 = x + M v written back into x, LN(x1) -> project_in into fpre, one kernel
+      const Gemm& g0 = b.attn_in_split ? b.pin_g0 : b.pin;
       GemmCall c;
-      c.g = &b.pin;
-      c.W = h->P(b.pin.w);
-      c.bias = h->P(b.pin.bias);
+      c.g = &g0;
+      c.W = h->P(g0.w);
+      c.bias = h->P(g0.bias);
       c.in = View{buf(pl.vbuf), b.C};
       c.out = fpre;
       c.B = B;
@@ -566,15 +591,20 @@ struct Fwd {
       c.out1 = x;
       if ((rc = probe_begin(1, b.C))) return rc;
       if (h->probe_class == 1)
-        tag = "gemm C" + std::to_string(b.C) + " HW" + std::to_string(HW) + " N" + std::to_string(b.pin.n_true) +
-              " K" + std::to_string(b.C) + " attn_out+ln+project_in v" + std::to_string(b.pin.NT) + "x" +
-              std::to_string(b.pin.KG);
+        tag = "gemm C" + std::to_string(b.C) + " HW" + std::to_string(HW) + " N" + std::to_string(g0.n_true) +
+              " K" + std::to_string(b.C) + " attn_out+ln+project_in v" + std::to_string(g0.NT) + "x" +
+              std::to_string(g0.KG);
       if ((rc = run_gemm(c, s))) return rc;
       const double Pd = (double)P;
       // read v and x, write x1 and the project_in rows; M per image + W_in; both GEMMs' FLOPs
-      const double bytes = 4.0 * (Pd * 3.0 * b.C + Pd * b.pin.n_true + (double)B * b.C * b.C +
-                                  (double)b.pin.n_true * b.C);
-      if ((rc = probe_end(1, b.C, bytes, 2.0 * Pd * ((double)b.C * b.C + (double)b.C * b.pin.n_true)))) return rc;
+      const double bytes = 4.0 * (Pd * 3.0 * b.C + Pd * g0.n_true + (double)B * b.C * b.C +
+                                  (double)g0.n_true * b.C);
+      if ((rc = probe_end(1, b.C, bytes, 2.0 * Pd * ((double)b.C * b.C + (double)b.C * g0.n_true)))) return rc;
+      if (b.attn_in_split) {  // project_in's second weight group on x1 (now in x)
+        rc = gemm(b.pin_g1, h->P(b.pin_g1.w), 0, x, Hh, Ww, View{fpre.p + 16 * b.pin_g0.ntiles, fpre.ld}, 0, nullptr,
+                  0, ln, b.C, b.C);
+        if (rc) return rc;
+      }
     } else {
       rc = gemm(b.proj_gemm, buf(pl.Mp), (long long)b.C * b.C, View{buf(pl.vbuf), b.C}, Hh, Ww, x, 0, x.p, x.ld, 0,
                 0, b.C);
