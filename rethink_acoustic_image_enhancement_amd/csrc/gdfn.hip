@@ -629,7 +629,7 @@ hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
   }
   // r01 schedule.  KDLAE_GDFN_TILE picks the tile height / stage ring / waves:
   //   0: 16 rows, 3 stage slots, 8 waves (one block per CU, 156 KB of LDS; r01's configuration);
-  //   1 (default): 8 rows, 2 slots, 4 waves (69 KB: two independent blocks per CU);
+  //   1 (default): 8 rows (12 at C = 48), 2 slots, 4 waves (69 / 77 KB: two independent blocks per CU);
   //   2: 4 rows, 2 slots, 4 waves (three blocks per CU);  3: 8 rows, 2 slots, 2 waves.
   static const int tile = getenv("KDLAE_GDFN_TILE") ? atoi(getenv("KDLAE_GDFN_TILE")) : 1;
   if (C == 96) {
@@ -641,7 +641,12 @@ hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
   if (tile == 0) return launch_gdfn1<3, 8, 16, 3>(p, s);
   if (tile == 2) return launch_gdfn1<3, 4, 4, 2>(p, s);
   if (tile == 3) return launch_gdfn1<3, 2, 8, 2>(p, s);
-  return launch_gdfn1<3, 4, 8, 2>(p, s);
+  // C = 48 default: 16 x 12 tiles, 3 rows per wave.  77 KB of LDS still fits two blocks per CU (the
+  // 3 KiB W records of NT = 3 leave room), and the halo and W/dw refetch per pixel drop by a third:
+  // C48@1024^2 5.68 -> 5.42 ms, @512^2 1.46 -> 1.42 ms (profiles/r02_gdfn_c48_tile12_probe.txt).
+  // 6: the 16 x 8 tiles of C = 96
+  if (tile == 6) return launch_gdfn1<3, 4, 8, 2>(p, s);
+  return launch_gdfn1<3, 4, 12, 2>(p, s);
 }
 
 }  // namespace kdlae
