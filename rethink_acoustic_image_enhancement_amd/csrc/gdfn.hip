@@ -61,6 +61,10 @@ template <int TH> struct GdTile {
     for (int t = 0; t < NT; ++t) n += ((t + 1) % WAVES == w) ? 1 : 0;
     return n;
   }
+  // halo pieces + the dw block of wave w: one chunk's DMAs when W travels separately (W2)
+  template <int WAVES> static constexpr int stage_dma(int w) {
+    return stage_pieces<WAVES>(w) + (w == WAVES - 1 ? 2 : 0);
+  }
 };
 
 // Exact-erf GELU, 0.5 x (1 + erf(x / sqrt 2)), with erf from Abramowitz & Stegun 7.1.26
@@ -106,13 +110,18 @@ __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t r, f32x4* lds_wav
 
 }  // namespace
 
-template <int NT, int WAVES, int TH, int NSTG>
-__global__ __launch_bounds__(64 * WAVES) void gdfn_out_kernel(GdfnParams p) {
+// W2: the project_out W fragments travel one chunk ahead of their MFMAs in a 2-slot ring of their
+// own (issued after the barrier that retires the slot's previous reader) instead of riding with the
+// stage 2 chunks ahead in a 3-slot ring: one W slot less of LDS, which lets C = 96 use 16 x 12
+// tiles at two blocks per CU (2 x 34 KiB stage + 2 x 6 KiB W = exactly 80 KiB).  Needs NSTG = 2.
+template <int NT, int WAVES, int TH, int NSTG, bool W2 = false>
+__global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnParams p) {
   using T = GdTile<TH>;
   constexpr int kStageItems = T::kStageItems, kStagePieces = T::kStagePieces;
   constexpr int kStageF4 = T::kStageF4, kStageSlot = T::kStageSlot;
   constexpr int kNStage = NSTG;                                // stage ring (halo + dw block)
-  constexpr int kNW = NSTG + 1;  // W ring: chunk c is multiplied in iteration c, chunk c+NSTG issued then
+  constexpr int kNW = W2 ? 2 : NSTG + 1;  // W ring: chunk c is multiplied in iteration c, chunk c+NSTG issued then
+  static_assert(!W2 || NSTG == 2, "the W2 schedule is written for a 2-slot stage ring");
   constexpr int RPW = TH / WAVES;                              // tile rows per wave
   static_assert(RPW * WAVES == TH && NSTG >= 2, "tile rows per wave / ring depth");
   constexpr int kRounds = (kStagePieces + WAVES - 1) / WAVES;  // stage pieces per wave (max)
@@ -172,6 +181,14 @@ __global__ __launch_bounds__(64 * WAVES) void gdfn_out_kernel(GdfnParams p) {
       dma_buf(rd, sl + kStageF4, 16u * lane, g * (kDwF4 * 16));
       dma_buf(rd, sl + kStageF4 + 64, 16u * lane + 1024u, g * (kDwF4 * 16));
     }
+    if constexpr (!W2) {
+      f32x4* wl = wring + (g % kNW) * (64 * NT);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if ((t + 1) % WAVES == wave) dma_buf(rw, wl + 64 * t, 16u * lane, (t * kch + g) * 1024);
+    }
+  };
+  [[maybe_unused]] auto issue_w = [&](int g) {
     f32x4* wl = wring + (g % kNW) * (64 * NT);
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -279,8 +296,46 @@ __global__ __launch_bounds__(64 * WAVES) void gdfn_out_kernel(GdfnParams p) {
     }
   };
 
-  // prologue: chunks 0 .. NSTG-1 in flight; gate(0) once chunk 0 has landed
   f32x4 gb[RPW];
+  if constexpr (W2) {
+    // S0, W0, S1 in flight; gate(0) needs S0 (and iteration 0 W0): wait for all but S1's DMAs
+    issue(0);
+    issue_w(0);
+    if (kch > 1) {
+      issue(1);
+      switch (wave) {
+        case 0: wait_vmcnt<T::template stage_dma<WAVES>(0 % WAVES)>(); break;
+        case 1: wait_vmcnt<T::template stage_dma<WAVES>(1 % WAVES)>(); break;
+        case 2: wait_vmcnt<T::template stage_dma<WAVES>(2 % WAVES)>(); break;
+        case 3: wait_vmcnt<T::template stage_dma<WAVES>(3 % WAVES)>(); break;
+        case 4: wait_vmcnt<T::template stage_dma<WAVES>(4 % WAVES)>(); break;
+        case 5: wait_vmcnt<T::template stage_dma<WAVES>(5 % WAVES)>(); break;
+        case 6: wait_vmcnt<T::template stage_dma<WAVES>(6 % WAVES)>(); break;
+        default: wait_vmcnt<T::template stage_dma<WAVES>(7 % WAVES)>(); break;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      wait_all();
+    }
+    gate(0, gb);
+    for (int g = 0; g + 1 < kch; ++g) {
+      // S(g+1) and W(g) (issued one iteration ago) landed; past the barrier every wave is done with
+      // gate(g) (stage slot g%2) and mfma(g-1) (W slot (g+1)%2)
+      wait_all();
+      if (g + 2 < kch) issue(g + 2);
+      issue_w(g + 1);
+      f32x4 gbn[RPW];
+      gate(g + 1, gbn);
+      mfma_chunk(g, gb);
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) gb[r] = gbn[r];
+    }
+    if (kch > 1) wait_all();  // W(kch-1)
+    mfma_chunk(kch - 1, gb);
+  } else {
+  // prologue: chunks 0 .. NSTG-1 in flight; gate(0) once chunk 0 has landed
 #pragma unroll
   for (int c = 0; c < NSTG; ++c)
     if (c < kch) issue(c);
@@ -301,6 +356,7 @@ __global__ __launch_bounds__(64 * WAVES) void gdfn_out_kernel(GdfnParams p) {
     for (int r = 0; r < RPW; ++r) gb[r] = gbn[r];
   }
   mfma_chunk(kch - 1, gb);
+  }
 
   // epilogue: lane holds output channels 16t + 4q .. +3 of pixel (y0 + 4w + r, x0 + cx)
   // All loads (bias, every row's residual; clamped rows, unconditional) before the first store: vmcnt
@@ -571,22 +627,22 @@ bool gdfn_supported(int C, int hidS) {
   return (C == 48 || C == 96) && hidS % 16 == 0 && hidS <= 256;
 }
 
-template <int NT, int WAVES, int TH, int NSTG>
+template <int NT, int WAVES, int TH, int NSTG, bool W2 = false>
 static hipError_t launch_gdfn1(const GdfnParams& p, hipStream_t s) {
-  const size_t lds = (size_t)(NSTG * GdTile<TH>::kStageSlot + (NSTG + 1) * 64 * NT) * sizeof(f32x4);
+  const size_t lds = (size_t)(NSTG * GdTile<TH>::kStageSlot + (W2 ? 2 : NSTG + 1) * 64 * NT) * sizeof(f32x4);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static size_t attr[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   if (lds > 64 * 1024 && lds > attr[dev]) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gdfn_out_kernel<NT, WAVES, TH, NSTG>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gdfn_out_kernel<NT, WAVES, TH, NSTG, W2>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr[dev] = lds;
   }
   const long long tiles = (long long)p.Bn * ((p.H + TH - 1) / TH) * ((p.W + kTile - 1) / kTile);
   const long long grid = (tiles + 7) / 8 * 8;
-  hipLaunchKernelGGL((gdfn_out_kernel<NT, WAVES, TH, NSTG>), dim3((unsigned)grid), dim3(64 * WAVES), lds, s, p);
+  hipLaunchKernelGGL((gdfn_out_kernel<NT, WAVES, TH, NSTG, W2>), dim3((unsigned)grid), dim3(64 * WAVES), lds, s, p);
   return hipGetLastError();
 }
 
@@ -629,14 +685,19 @@ hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
   }
   // r01 schedule.  KDLAE_GDFN_TILE picks the tile height / stage ring / waves:
   //   0: 16 rows, 3 stage slots, 8 waves (one block per CU, 156 KB of LDS; r01's configuration);
-  //   1 (default): 8 rows (12 at C = 48), 2 slots, 4 waves (69 / 77 KB: two independent blocks per CU);
+  //   1 (default): 12 rows, 2 slots, 4 waves (C = 96 with the 2-slot W ring: 80 KB; C = 48: 77 KB),
+  //      two independent blocks per CU;
   //   2: 4 rows, 2 slots, 4 waves (three blocks per CU);  3: 8 rows, 2 slots, 2 waves.
   static const int tile = getenv("KDLAE_GDFN_TILE") ? atoi(getenv("KDLAE_GDFN_TILE")) : 1;
   if (C == 96) {
     if (tile == 0) return launch_gdfn1<6, 8, 16, 3>(p, s);
     if (tile == 2) return launch_gdfn1<6, 4, 4, 2>(p, s);
     if (tile == 3) return launch_gdfn1<6, 2, 8, 2>(p, s);
-    return launch_gdfn1<6, 4, 8, 2>(p, s);
+    // 8: r02's first two-block layout, 16 x 8 tiles with the 3-slot W ring
+    if (tile == 8) return launch_gdfn1<6, 4, 8, 2>(p, s);
+    // default: 16 x 12 tiles with the W ring 2 slots deep (exactly 80 KiB: two blocks per CU):
+    // C96@512^2 3.52 -> 3.37 ms, @256^2 0.866 -> 0.848 ms (profiles/r02_gdfn_c96_tile12_probe.txt)
+    return launch_gdfn1<6, 4, 12, 2, true>(p, s);
   }
   if (tile == 0) return launch_gdfn1<3, 8, 16, 3>(p, s);
   if (tile == 2) return launch_gdfn1<3, 4, 4, 2>(p, s);
