@@ -134,11 +134,16 @@ __global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnPa
 
   // XCD-aware tile order: logical tiles [k*per, (k+1)*per) run on XCD k, so tiles that share halo
   // rows/columns share an L2.  The grid is padded to a multiple of 8.
+  // With nsplit > 1 the nsplit blocks of one pixel tile (adjacent logical ids: same XCD, so the second
+  // reads the halo from L2) each own NT of the layer's output tiles (C = 384: 2 x 12).
   const int tx_n = (p.W + kTile - 1) / kTile, ty_n = (p.H + TH - 1) / TH;
-  const int ntiles = p.Bn * tx_n * ty_n;
+  const int nsp = p.nsplit > 1 ? p.nsplit : 1;
+  const int ntiles = p.Bn * tx_n * ty_n * nsp;
   const int per = (int)(gridDim.x >> 3);
   int bid = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
   if (bid >= ntiles) return;
+  const int sp = bid % nsp;
+  bid /= nsp;
   const int tx = bid % tx_n;
   bid /= tx_n;
   const int ty = bid % ty_n;
@@ -166,7 +171,8 @@ __global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnPa
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(X), 0, (int)(HW * p.ld * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.Wp), 0, NT * kch * 1024, 0x00020000);
+      const_cast<float*>(p.Wp + (size_t)sp * NT * kch * 256), 0, NT * kch * 1024, 0x00020000);
+  const int n0 = 16 * NT * sp;  // first output channel of this block
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.dw), 0, kch * kDwF4 * 16, 0x00020000);
   auto issue = [&](int g) {
@@ -366,14 +372,15 @@ __global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnPa
   f32x4 bias[NT], res[RPW][NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
-    bias[t] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + 16 * t + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bias[t] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n0 + 16 * t + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int yo = min(y0 + RPW * wave + r, p.H - 1);
     const long long pix = (long long)b * HW + (long long)yo * p.W + xo;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
-      res[r][t] = p.R ? *reinterpret_cast<const f32x4*>(p.R + pix * p.ldr + 16 * t + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+      res[r][t] = p.R ? *reinterpret_cast<const f32x4*>(p.R + pix * p.ldr + n0 + 16 * t + 4 * q)
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
@@ -382,7 +389,7 @@ __global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnPa
     const long long pix = (long long)b * HW + (long long)yo * p.W + xo;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
-      *reinterpret_cast<f32x4*>(p.out + pix * p.ldo + 16 * t + 4 * q) = acc[r][t] + res[r][t] + bias[t];
+      *reinterpret_cast<f32x4*>(p.out + pix * p.ldo + n0 + 16 * t + 4 * q) = acc[r][t] + res[r][t] + bias[t];
   }
 }
 
@@ -624,7 +631,10 @@ void gdfn2_kernel(GdfnParams p, int nunits) {
 }
 
 bool gdfn_supported(int C, int hidS) {
-  return (C == 48 || C == 96) && hidS % 16 == 0 && hidS <= 256;
+  // A/B hooks: C = 192 / 384 back on dwconv_gate + the project_out GEMM
+  if (C == 192 && getenv("KDLAE_NO_GDFN192")) return false;
+  if (C == 384 && getenv("KDLAE_NO_GDFN384")) return false;
+  return (C == 48 || C == 96 || C == 192 || C == 384) && hidS % 16 == 0 && hidS <= (C >= 192 ? 1024 : 256);
 }
 
 template <int NT, int WAVES, int TH, int NSTG, bool W2 = false>
@@ -640,7 +650,8 @@ static hipError_t launch_gdfn1(const GdfnParams& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr[dev] = lds;
   }
-  const long long tiles = (long long)p.Bn * ((p.H + TH - 1) / TH) * ((p.W + kTile - 1) / kTile);
+  const long long tiles = (long long)p.Bn * ((p.H + TH - 1) / TH) * ((p.W + kTile - 1) / kTile) *
+                          (p.nsplit > 1 ? p.nsplit : 1);
   const long long grid = (tiles + 7) / 8 * 8;
   hipLaunchKernelGGL((gdfn_out_kernel<NT, WAVES, TH, NSTG, W2>), dim3((unsigned)grid), dim3(64 * WAVES), lds, s, p);
   return hipGetLastError();
@@ -675,9 +686,25 @@ static bool gdfn2_ok(const GdfnParams& p, int C) {
          (!p.R || hw * p.ldr * 4 < (1LL << 31)) && (size_t)(p.hidS / 16) * ((C / 16) * 64 + 80) * 16 <= 160 * 1024;
 }
 
+static hipError_t launch_gdfn_out_small(const GdfnParams& p, int C, hipStream_t s);
+
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
   if (!gdfn_supported(C, p.hidS) || p.ld != 2 * p.hidS || p.ldo % 4 || (p.R && p.ldr % 4) || !p.zeros)
     return hipErrorInvalidValue;
+  if (C >= 192) {
+    // C = 192 / 384 (r02): 16 x 8 tiles, 2-slot stage ring + 2-slot W ring (2 x 25.5 + 2 x 12 KiB =
+    // 75 KiB: two blocks per CU) and 12 output tiles per block (96 MFMAs per wave and chunk against
+    // the same stencil VALU); C = 384 runs two blocks per pixel tile
+    GdfnParams q = p;
+    q.nsplit = C / 192;
+    return launch_gdfn1<12, 4, 8, 2, true>(q, s);
+  }
+  GdfnParams q = p;
+  q.nsplit = 1;
+  return launch_gdfn_out_small(q, C, s);
+}
+
+static hipError_t launch_gdfn_out_small(const GdfnParams& p, int C, hipStream_t s) {
   if (gdfn2_ok(p, C)) {
     static const int rows = getenv("KDLAE_GDFN2_ROWS") ? atoi(getenv("KDLAE_GDFN2_ROWS")) : 10;
     if (C == 96) return launch_gdfn2<6, 4, 1>(p, s);  // R = 7 spills at NT = 6

@@ -121,6 +121,7 @@ struct GdfnParams {
   float* out; int ldo;
   int Bn, H, W;
   const float* zeros;              // >= 16 B of zeros in device memory (source of out-of-image halo lines)
+  int nsplit;                      // set by launch_gdfn_out: blocks per pixel tile, each owning C/nsplit outputs
 };
 bool gdfn_supported(int C, int hidS);
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s);

@@ -616,22 +616,40 @@ hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------- slot reduction
-__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ partial,
-                                                          float* __restrict__ reduced, int nslots,
-                                                          int slot_floats) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
+// reduced[bh][i] = sum over the nslots partial slots, in a fixed order: wave w of a block sums the
+// slot range [w n / 8, (w+1) n / 8) sequentially for 64 consecutive floats (one 256 B line per
+// load), then lane i adds the 8 wave sums in wave order.  Deterministic and batch-invariant (the
+// slot partition depends on the image size only).  r01's kernel gave each float one thread that
+// walked all slots (160 blocks at 1024^2: a latency-bound 64 us per launch).
+constexpr int kRedWaves = 8;
+__global__ __launch_bounds__(64 * kRedWaves) void gram_reduce_kernel(const float* __restrict__ partial,
+                                                                     float* __restrict__ reduced, int nslots,
+                                                                     int slot_floats) {
+  __shared__ float part[kRedWaves][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int idx = blockIdx.x * 64 + lane;
   const long long bh = blockIdx.y;
-  if (idx >= slot_floats) return;
-  const float* src = partial + bh * nslots * (long long)slot_floats + idx;
+  const int k0 = wave * nslots / kRedWaves, k1 = (wave + 1) * nslots / kRedWaves;
   float s = 0.f;
-  for (int k = 0; k < nslots; ++k) s += src[(long long)k * slot_floats];
-  reduced[bh * slot_floats + idx] = s;
+  if (idx < slot_floats) {
+    const float* src = partial + bh * nslots * (long long)slot_floats + idx;
+#pragma unroll 8
+    for (int k = k0; k < k1; ++k) s += src[(long long)k * slot_floats];
+  }
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && idx < slot_floats) {
+    float t = part[0][lane];
+#pragma unroll
+    for (int w = 1; w < kRedWaves; ++w) t += part[w][lane];
+    reduced[bh * slot_floats + idx] = t;
+  }
 }
 
 hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int heads, int nslots,
                               int slot_floats, hipStream_t s) {
-  dim3 grid((slot_floats + 255) / 256, Bn * heads);
-  hipLaunchKernelGGL(gram_reduce_kernel, grid, dim3(256), 0, s, partial, reduced, nslots, slot_floats);
+  dim3 grid((slot_floats + 63) / 64, Bn * heads);
+  hipLaunchKernelGGL(gram_reduce_kernel, grid, dim3(64 * kRedWaves), 0, s, partial, reduced, nslots, slot_floats);
   return hipGetLastError();
 }
 
