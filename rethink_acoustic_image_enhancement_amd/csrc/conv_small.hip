@@ -1,4 +1,5 @@
-// Direct 3x3 convolutions whose input or output has <= 4 channels (VALU; too thin for MFMA).
+// 3x3 convolutions whose input or output has <= 4 channels: small-in as a K <= 36 MFMA GEMM,
+// small-out on the VALU.
 //
 //   small-in  (Cin <= 4,  Cout % 16 == 0): patch_embed 3->48 (KDLAE_model.py:173),
 //             output_param 4->96 dilation 2 on cat[out, denoise_rate] (:259, :316), cen 3->96 (:265)
@@ -13,75 +14,128 @@ namespace kdlae {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// thread = (16-channel output group, pixel); all lanes of a wave share the group -> LDS broadcast.
-// KT (temporal taps, 1 or 3) is a template parameter so the unrolled tap indexing folds to constants.
-template <int KT>
+// MFMA form (r02): out[p][n] = bias[n] + sum_k W[n][k] im2col[p][k], k = ci * taps + tap (K <= 36,
+// zero past Cin * taps), as v_mfma_f32_16x16x4_f32 with W as the A operand and 16 pixels as B.  Each
+// lane's k index is fixed per k-step (k = 4 s + lane / 16), so its tap offsets and weight fragments
+// are computed once: the W fragments of every output tile (NTO x 9 VGPRs) stay in registers and a
+// k-step costs the lane one gathered load per 16 pixels.  The accumulator of output tile t holds
+// channels 16 t + 4 (lane / 16) .. + 3 of pixel lane % 16 -> one 16 B NHWC store.  A wave walks
+// 64-pixel chunks (4 independent 16-pixel sub-tiles in flight).  r01's VALU kernel read all 16 x 36
+// weights of a thread's output group from LDS per pixel: 1.2 ms per 4M-pixel launch, ~5x its HBM floor.
+template <int KT, int NTO>
 __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
-  extern __shared__ float wsm[];  // [Cout][36] (ci-major then taps, zero past Cin*kt*9) then bias[Cout]
   constexpr int taps = 9 * KT;
+  constexpr int KS = 9;  // k-steps of 4 (K <= 36)
+  const int lane = threadIdx.x & 63, li = lane & 15, lq = lane >> 4;
   const int vh = p.vh ? p.vh : p.H, vw = p.vw ? p.vw : p.W;
-  const int nw = p.Cout * 36;
-  for (int i = threadIdx.x; i < nw; i += 256) {
-    const int co = i / 36, k = i - (i / 36) * 36;
-    wsm[i] = k < p.Cin * taps ? p.w[co * p.Cin * taps + k] : 0.f;
+  const int K = p.Cin * taps;
+  // this lane's k per step: channel, tap offsets (frame, row, column) and the offset from the pixel
+  int kdt[KS], kdy[KS], kdx[KS];
+  long long koff[KS];
+  bool kok[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + lq;
+    kok[s] = k < K;
+    const int kk = kok[s] ? k : 0;
+    const int ci = kk / taps, tap = kk - (kk / taps) * taps;
+    const int t9 = tap % 9;
+    kdt[s] = KT == 3 ? tap / 9 - 1 : 0;
+    kdy[s] = (t9 / 3 - 1) * p.dil;
+    kdx[s] = (t9 % 3 - 1) * p.dil;
+    koff[s] = ci * p.sc + kdt[s] * p.st + kdy[s] * p.sy + kdx[s] * p.sx;
   }
-  for (int i = threadIdx.x; i < p.Cout; i += 256) wsm[nw + i] = p.bias ? p.bias[i] : 0.f;
-  __syncthreads();
+  // W fragments: A[i = out channel li of tile t][k = 4 s + lq]
+  float wf[NTO][KS];
+  f32x4 bq[NTO];
+#pragma unroll
+  for (int t = 0; t < NTO; ++t) {
+    const int co = 16 * t + li;
+    const bool cok = co < p.Cout;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) wf[t][s] = (cok && kok[s]) ? p.w[co * K + 4 * s + lq] : 0.f;
+    const int cb = 16 * t + 4 * lq;
+    bq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (p.bias && cb < p.Cout) bq[t] = f32x4{p.bias[cb], p.bias[cb + 1], p.bias[cb + 2], p.bias[cb + 3]};
+  }
   const int fhw = p.H * p.W;
   const int HW = p.F * fhw;
   const long long P = (long long)p.Bn * HW;
-  const int ngroups = p.Cout / 16;
-  const long long total = P * ngroups;
-  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-    const int og = (int)(idx / P);
-    const long long pix = idx - (long long)og * P;
-    const int b = (int)(pix / HW);
-    const int pl = (int)(pix - (long long)b * HW);
-    const int t0 = pl / fhw;
-    const int rem = pl - t0 * fhw;
-    const int y = rem / p.W, x = rem - (rem / p.W) * p.W;
-    float in[36];
+  const long long nchunks = (P + 63) / 64;
+  const long long wave_id = blockIdx.x * 4LL + (threadIdx.x >> 6);
+  const long long nwaves = gridDim.x * 4LL;
+  for (long long c = wave_id; c < nchunks; c += nwaves) {
+    float bv[4][KS];
+    long long pix[4];
 #pragma unroll
-    for (int k = 0; k < 36; ++k) {
-      const int ci = k / taps, tap = k - (k / taps) * taps;  // taps = 9 (2-D) or 27 (3-D)
-      const int t9 = tap % 9;
-      const int tt = t0 + (KT == 3 ? tap / 9 - 1 : 0);
-      const int yy = y + (t9 / 3 - 1) * p.dil, xx = x + (t9 % 3 - 1) * p.dil;
-      const bool ok = ci < p.Cin && (unsigned)tt < (unsigned)p.F && (unsigned)yy < (unsigned)vh &&
-                      (unsigned)xx < (unsigned)vw;
-      const long long off = ok ? b * p.sb + ci * p.sc + tt * p.st + yy * p.sy + xx * p.sx : 0;
-      float v = p.in[off];
-      if (p.in_sub) v -= p.in_sub[off];
-      in[k] = ok ? v : 0.f;
-    }
-    float* o = p.out + pix * p.ldo + og * 16;
+    for (int j = 0; j < 4; ++j) {
+      pix[j] = c * 64 + 16 * j + li;
+      const long long pc = pix[j] < P ? pix[j] : P - 1;
+      const int b = (int)(pc / HW);
+      const int pl = (int)(pc - (long long)b * HW);
+      const int t0 = pl / fhw;
+      const int rem = pl - t0 * fhw;
+      const int y = rem / p.W, x = rem - (rem / p.W) * p.W;
+      const long long base = b * p.sb + t0 * p.st + y * p.sy + x * p.sx;
 #pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) {
-      f32x4 r;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int co = og * 16 + j4 * 4 + e;
-        const float* wr = wsm + co * 36;
-        float a = wsm[nw + co];
-#pragma unroll
-        for (int k = 0; k < 36; ++k) a = fmaf(in[k], wr[k], a);
-        r[e] = p.relu ? fmaxf(a, 0.f) : a;
+      for (int s = 0; s < KS; ++s) {
+        const int tt = t0 + kdt[s], yy = y + kdy[s], xx = x + kdx[s];
+        const bool ok = kok[s] && (unsigned)tt < (unsigned)p.F && (unsigned)yy < (unsigned)vh &&
+                        (unsigned)xx < (unsigned)vw;
+        const long long off = ok ? base + koff[s] : 0;
+        float v = p.in[off];
+        if (p.in_sub) v -= p.in_sub[off];
+        bv[j][s] = ok ? v : 0.f;
       }
-      *reinterpret_cast<f32x4*>(o + j4 * 4) = r;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 acc[NTO];
+#pragma unroll
+      for (int t = 0; t < NTO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int t = 0; t < NTO; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[t][s], bv[j][s], acc[t], 0, 0, 0);
+      if (pix[j] >= P) continue;
+      float* o = p.out + pix[j] * p.ldo + 4 * lq;
+#pragma unroll
+      for (int t = 0; t < NTO; ++t) {
+        if (16 * t >= p.Cout) continue;
+        f32x4 r = acc[t] + bq[t];
+        if (p.relu) r = f32x4{fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f), fmaxf(r.w, 0.f)};
+        *reinterpret_cast<f32x4*>(o + 16 * t) = r;
+      }
     }
   }
 }
 
+template <int KT>
+static void launch_small_in_nt(const SmallInParams& p, unsigned blocks, hipStream_t s) {
+  const int nto = p.Cout / 16;
+  if (nto <= 2) hipLaunchKernelGGL((conv_small_in_kernel<KT, 2>), dim3(blocks), dim3(256), 0, s, p);
+  else if (nto <= 3) hipLaunchKernelGGL((conv_small_in_kernel<KT, 3>), dim3(blocks), dim3(256), 0, s, p);
+  else if (nto <= 4) hipLaunchKernelGGL((conv_small_in_kernel<KT, 4>), dim3(blocks), dim3(256), 0, s, p);
+  else if (nto <= 6) hipLaunchKernelGGL((conv_small_in_kernel<KT, 6>), dim3(blocks), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((conv_small_in_kernel<KT, 8>), dim3(blocks), dim3(256), 0, s, p);
+}
+
 hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s) {
   if (p.Cin * 9 * p.kt > 36 || p.Cout % 16 || (p.kt != 1 && p.kt != 3)) return hipErrorInvalidValue;
-  const long long total = (long long)p.Bn * p.F * p.H * p.W * (p.Cout / 16);
-  long long blocks = (total + 255) / 256;
-  if (blocks > 16384) blocks = 16384;
-  const size_t lds = (size_t)(p.Cout * 36 + p.Cout) * sizeof(float);
-  if (p.kt == 3)
-    hipLaunchKernelGGL(conv_small_in_kernel<3>, dim3((unsigned)blocks), dim3(256), lds, s, p);
-  else
-    hipLaunchKernelGGL(conv_small_in_kernel<1>, dim3((unsigned)blocks), dim3(256), lds, s, p);
+  const long long chunks = ((long long)p.Bn * p.F * p.H * p.W + 63) / 64;
+  long long blocks = (chunks + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  const int K = p.Cin * 9 * p.kt;
+  for (int co0 = 0; co0 < p.Cout; co0 += 128) {  // up to 8 output tiles per pass
+    SmallInParams q = p;
+    q.w = p.w + (size_t)co0 * K;
+    q.bias = p.bias ? p.bias + co0 : nullptr;
+    q.out = p.out + co0;
+    q.Cout = p.Cout - co0 < 128 ? p.Cout - co0 : 128;
+    if (p.kt == 3) launch_small_in_nt<3>(q, (unsigned)blocks, s);
+    else launch_small_in_nt<1>(q, (unsigned)blocks, s);
+  }
   return hipGetLastError();
 }
 
