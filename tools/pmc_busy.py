@@ -24,6 +24,7 @@ import sys
 CLASSES = [("conv_gemm_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
            ("gemm_res_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
            ("gemm_chunk_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
+           ("gemm_attn_in_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
            ("dwconv_gram", "dwconv_gram (MDTA pass 1: dwconv + MFMA Gram)"),
            ("gdfn_out_kernel", "gdfn_out (fused GDFN tail: dwconv + gate + MFMA project_out)"),
            ("gdfn2_kernel", "gdfn_out (fused GDFN tail: dwconv + gate + MFMA project_out)"),
