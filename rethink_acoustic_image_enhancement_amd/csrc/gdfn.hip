@@ -40,6 +40,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
+#ifndef KDLAE_GELU_PACKED
+#define KDLAE_GELU_PACKED 1
+#endif
+constexpr bool kGeluPacked = KDLAE_GELU_PACKED != 0;  // A/B knob: packed-FP32 GELU gate in gdfn_out
 constexpr int kTile = 16;                          // output tile width (pixels); height TH is a parameter
 constexpr int kHalo = kTile + 2;                   // 18 halo columns
 constexpr int kDwF4 = 128;                         // per-chunk dw block: [9][8] weights, [8] bias, pad
@@ -80,6 +84,27 @@ __device__ __forceinline__ float gelu_erf_g(float x) {
   poly *= t;
   const float e = 1.0f - poly * __expf(-z * z);     // erf(|x| / sqrt 2)
   return 0.5f * x * (1.0f + copysignf(e, x));
+}
+
+// The same GELU on a pair, written on float2 so hipcc emits packed FP32 (v_pk_fma/v_pk_mul: two
+// lanes' worth of the polynomial per instruction); rcp and exp stay per value.  The operations and
+// their order match gelu_erf_g.  Measured (profiles/r02_gdfn_gelu_packed_probe.txt): C96 -1.9%,
+// C48 -1%, C192 +1.5% per launch, so the wide (NT = 12) kernel keeps the scalar form.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_gate2(f32x2 x, f32x2 v) {
+  const f32x2 z = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
+  const f32x2 a = __builtin_elementwise_fma(f32x2{0.3275911f, 0.3275911f}, z, f32x2{1.0f, 1.0f});
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)};
+  f32x2 poly = __builtin_elementwise_fma(f32x2{1.061405429f, 1.061405429f}, t, f32x2{-1.453152027f, -1.453152027f});
+  poly = __builtin_elementwise_fma(poly, t, f32x2{1.421413741f, 1.421413741f});
+  poly = __builtin_elementwise_fma(poly, t, f32x2{-0.284496736f, -0.284496736f});
+  poly = __builtin_elementwise_fma(poly, t, f32x2{0.254829592f, 0.254829592f});
+  poly *= t;
+  const f32x2 nz2 = -z * z;
+  const f32x2 ex = f32x2{__expf(nz2.x), __expf(nz2.y)};
+  const f32x2 e = 1.0f - poly * ex;
+  const f32x2 se = f32x2{copysignf(e.x, x.x), copysignf(e.y, x.y)};
+  return ((0.5f * x) * (1.0f + se)) * v;
 }
 
 typedef unsigned u32x4g __attribute__((ext_vector_type(4)));
@@ -279,10 +304,16 @@ __global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnPa
     }
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
-      gb[r].x = gelu_erf_g(d[0][r].x) * d[1][r].x;
-      gb[r].y = gelu_erf_g(d[0][r].y) * d[1][r].y;
-      gb[r].z = gelu_erf_g(d[0][r].z) * d[1][r].z;
-      gb[r].w = gelu_erf_g(d[0][r].w) * d[1][r].w;
+      if constexpr (kGeluPacked && NT <= 6) {
+        const f32x2 lo = gelu_gate2(f32x2{d[0][r].x, d[0][r].y}, f32x2{d[1][r].x, d[1][r].y});
+        const f32x2 hi = gelu_gate2(f32x2{d[0][r].z, d[0][r].w}, f32x2{d[1][r].z, d[1][r].w});
+        gb[r] = f32x4{lo.x, lo.y, hi.x, hi.y};
+      } else {
+        gb[r].x = gelu_erf_g(d[0][r].x) * d[1][r].x;
+        gb[r].y = gelu_erf_g(d[0][r].y) * d[1][r].y;
+        gb[r].z = gelu_erf_g(d[0][r].z) * d[1][r].z;
+        gb[r].w = gelu_erf_g(d[0][r].w) * d[1][r].w;
+      }
     }
   };
   auto mfma_chunk = [&](int g, const f32x4 (&gb)[RPW]) {
