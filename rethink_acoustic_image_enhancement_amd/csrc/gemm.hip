@@ -906,7 +906,7 @@ static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, si
 #define KDLAE_GEMM_RES2_VARIANTS(X) \
   X(9, 3, 1, true) X(9, 3, 2, true) X(8, 3, 1, true) X(8, 3, 2, true) X(3, 3, 1, true) X(3, 3, 2, true) \
   X(6, 3, 1, true) X(6, 3, 2, true) X(9, 6, 1, true) X(9, 6, 2, true) X(8, 6, 1, true) X(8, 6, 2, true) \
-  X(6, 6, 1, true) X(6, 6, 2, true) X(3, 6, 1, true) X(3, 6, 2, true) X(3, 8, 1, true) X(3, 8, 2, true) \
+  X(6, 6, 1, true) X(6, 6, 2, true) X(6, 6, 3, true) X(3, 6, 1, true) X(3, 6, 2, true) X(3, 8, 1, true) X(3, 8, 2, true) \
   X(6, 8, 1, true) X(6, 8, 2, true) X(6, 12, 1, false) X(6, 12, 2, false) X(8, 12, 1, false) \
   X(8, 12, 2, false) X(3, 12, 1, false) X(3, 12, 2, false) X(6, 16, 1, false) X(3, 16, 1, false)
 

@@ -53,6 +53,12 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
         // while every epilogue load drained the stores; with that fixed, 2 waves measure 10-15%
         // faster on all of them (r01 probe: C48 project_in @1024^2 5864 -> 5099 us)
         double cost = (double)padded / gt + 0.01 * (12 - nt) + (ngroups - 1) * 0.05;
+        // an odd NT leaves each k-group's last tile alone with 2 independent accumulator chains:
+        // C96 qkv (18 tiles) measured 2% faster as 3 chunks of 6 than as 2 chunks of 9 on two boxes
+        // (profiles/r02_gemm_odd_nt_probe.txt); riding that tile along with the first pair instead
+        // measured no gain.  KDLAE_ODD_NT_PEN overrides the penalty (A/B hook)
+        static const double odd_pen = getenv("KDLAE_ODD_NT_PEN") ? atof(getenv("KDLAE_ODD_NT_PEN")) : 0.05;
+        if (nt % 2) cost += odd_pen;
         if (!forced_wpe() && w == 4) cost += 1.0;
         if (cost < best) {
           best = cost;
