@@ -425,7 +425,7 @@ def main():
                          "algorithmic_flops_per_launch": fl.value / n.value})
 
     bs1 = None
-    if not args.no_bs1 and B > 1:
+    if not args.no_bs1 and B > 1 and world == 1:
         # the metric names 1x512x512: single-image latency on the same module and GPU, each forward
         # synchronised (HIP events on the forward's stream), after the throughput measurement
         one = {"img": batch["img"][:1], "denoise_rate": batch["denoise_rate"][:1]}
