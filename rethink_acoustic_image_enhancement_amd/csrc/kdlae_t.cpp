@@ -397,7 +397,10 @@ struct Plan {
 static int nslots_for(int H, int W, int /*B*/, int /*heads*/) {
   if (W % 16 == 0) {
     const int strips = W / 16;
-    const int nseg = std::max(1, std::min(8, (H + 31) / 32));
+    // KDLAE_GRAM_NSEG: A/B hook for the most row segments per strip (default 8; 4 and 16 measured
+    // no better, profiles/r02_gram_nseg_probe.txt)
+    static const int max_seg = getenv("KDLAE_GRAM_NSEG") ? std::max(1, atoi(getenv("KDLAE_GRAM_NSEG"))) : 8;
+    const int nseg = std::max(1, std::min(max_seg, (H + 31) / 32));
     return strips * nseg;
   }
   const int steps = (H * W + 63) / 64;
