@@ -102,6 +102,9 @@ def test_mdd_512_config1():
           LayerNorm_type="BiasFree", ffn_expansion_factor=2.0), (1, 3, 72, 32)),
     (dict(dim=32, heads=[1, 2, 4, 8], num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, params="mul",
           static="train"), (2, 3, 32, 32)),
+    # dim 80: 5-tile patch_embed (a partial small-in tile group) and 160-wide output_param / cen (two
+    # small-in passes of <= 128 outputs); C = 80 / 160 / 320 / 640 take the unfused FFN path
+    (dict(dim=80, heads=[5, 5, 5, 5], num_blocks=[1, 1, 1, 1], num_refinement_blocks=1), (1, 3, 32, 32)),
 ])
 def test_vs_oracle_random_configs(kw, shape):
     """Seeded hash weights/inputs at sizes the oracle finishes in seconds; every ctor branch."""
