@@ -432,7 +432,7 @@ static Plan make_plan(const kdlae_t_handle* h, int B, int H, int W) {
       mq = std::max(mq, P * 3 * b.C);
       mv = std::max(mv, P * b.C);
       mfp = std::max(mfp, P * 2 * b.hidS);
-      mfg = std::max(mfg, P * b.hidS);
+      if (!b.fused_gdfn) mfg = std::max(mfg, P * b.hidS);  // gated tensor: unfused FFN tails only
       mst = std::max(mst, P * 2);
       mpart = std::max(mpart, (long long)B * b.heads * nslots_for(Hh, Ww, B, b.heads) * slot);
       mred = std::max(mred, (long long)B * b.heads * slot);
