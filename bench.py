@@ -3,16 +3,23 @@
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+`--gpus N` (N > 1) without a torchrun environment starts the N rank processes itself (one per GPU,
+torch.distributed.run on 127.0.0.1, the reference's own launcher: Train/train.sh:5) before anything
+touches the GPU, and exits non-zero when fewer than N devices are visible.
+
 One step = one KDLAE-T forward (static="train": hq + sr, params="cat", BiasFree LN, fp32) of
-16 synthetic 512x512 images per GPU (weak scaling: global batch 16*N, images sharded by rank,
-no data-path collective).  Weights are the deterministic hash recipe (random init of the real
-architecture), inputs are hash-uniform images with per-image constant denoise_rate.
+16 synthetic 512x512 images per GPU (weak scaling: global batch 16*N, rank r owns images
+[16r, 16r+16); for N > 1 the step ends with the RCCL all-gather of hq/sr).  Weights
+are the deterministic hash recipe (random init of the real architecture), inputs are
+hash-uniform images with per-image constant denoise_rate.
 
 Printed JSON (rank 0): value = images/s over all ranks (max-over-ranks wall time of exactly K
 steps between barriers + device syncs); roofline of the dominant kernel class measured live with
 HIP events around each of its launches inside the timed steps; cpu_baseline = the CPU oracle
-(oracle/kdlae_oracle.py, test infrastructure) on one image of the same workload, whose output also
-gives the PSNR / max-abs of the GPU result (rank 0, N=1 only).
+(oracle/kdlae_oracle.py, test infrastructure) on one image of the same workload, 1 warm-up + the
+median of 3 timed runs, whose output also gives the PSNR / max-abs of the GPU result
+(rank 0, N=1 only).  The same line carries BASELINE configs[2] (KDLAE-S S8) and configs[3]
+(ASDQE A64) under "s8" / "a64", each with its own value, roofline, cpu_baseline and parity.
 """
 from __future__ import annotations
 
@@ -20,6 +27,8 @@ import argparse
 import json
 import os
 import re
+import socket
+import subprocess
 import sys
 import time
 
@@ -74,10 +83,111 @@ def host_cores():
 
 
 def make_inputs(first: int, n: int, H: int, W: int):
+    """Images [first, first + n) of the global synthetic batch (keyed by global index, so every
+    rank's shard is the matching slice of the single-process batch)."""
     imgs = np.stack([hash_images(f"img16:{first + i}", (3, H, W)) for i in range(n)])
     rates = (hash_uniform("rate16", first + n)[first:] + 1.0) * 0.5
     rate = np.broadcast_to(rates.astype(np.float32)[:, None, None, None], (n, 1, H, W)).copy()
     return torch.from_numpy(imgs), torch.from_numpy(rate)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list, need_gpus: bool = True) -> int:
+    """Run this script as n rank processes under torch.distributed.run (one process per GPU,
+    LOCAL_RANK -> device) and return its exit code.  Called before any GPU call; the parent only
+    counts devices (torch.cuda.device_count() does not initialise HIP) and waits."""
+    if need_gpus:
+        visible = torch.cuda.device_count()
+        if visible < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {visible}", file=sys.stderr, flush=True)
+            return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def timed_steps(step, steps: int, distributed: bool, dev):
+    """Exactly `steps` calls of `step` bracketed by a barrier + device sync on both sides.
+    Returns (max-over-ranks seconds, this rank's seconds, last output)."""
+    _sync(dev)
+    if distributed:
+        dist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = step()
+    _sync(dev)
+    local = time.perf_counter() - t0
+    elapsed = local
+    if distributed:
+        dist.barrier()
+        t = torch.tensor([local], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, local, out
+
+
+def cpu_timed(fn, runs: int = 3):
+    """BASELINE.md CPU-baseline procedure: one untimed warm-up call, then the median of `runs`
+    timed calls.  Returns (warm-up output, median seconds, sorted timings)."""
+    out = fn()
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return out, ts[len(ts) // 2], ts
+
+
+def bench_standin(args, world, rank):
+    """CPU rehearsal of the N-rank path (gloo, no GPU): the T16 sharding, timing and gather with a
+    per-image stand-in for the forward.  Each rank sleeps rank-dependent time per step so the
+    max-over-ranks timing is observable.  Used by tests/test_bench_launch.py."""
+    from rethink_acoustic_image_enhancement_amd.shard import gather_outputs
+
+    dev = torch.device("cpu")
+    B, H = args.batch or 16, args.size or 16
+    img, rate = make_inputs(rank * B, B, H, H)
+    delay = 0.01 * rank
+
+    def step():
+        hq = img * 2 + rate
+        time.sleep(delay)
+        return gather_outputs(hq) if world > 1 else hq
+
+    for _ in range(args.warmup):
+        step()
+    elapsed, local, full = timed_steps(step, args.steps, world > 1, dev)
+    info = [{"rank": rank, "first": rank * B, "last": rank * B + B - 1, "local_s": local}]
+    if world > 1:
+        info = [None] * world
+        dist.all_gather_object(info, {"rank": rank, "first": rank * B, "last": rank * B + B - 1, "local_s": local})
+    if rank == 0:
+        gimg, grate = make_inputs(0, world * B, H, H)
+        res = {"metric": METRIC + " [CPU stand-in rehearsal]", "value": round(world * B * args.steps / elapsed, 3),
+               "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(elapsed / args.steps * 1e3, 3), "elapsed_s": elapsed,
+               "config": {"global_batch": world * B, "per_gpu_batch": B},
+               "standin": {"ranks": info, "gather_equal": bool(torch.equal(full, gimg * 2 + grate))}}
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 S_KW = dict(inp_channels=1, out_channels=1, residual=True, hidden_channels=[16, 32, 64])  # KDLAE-S.ipynb:106
@@ -110,11 +220,12 @@ def asdqe_flops(ci, d, B, H, W):
     return f
 
 
-def bench_secondary(args, world, rank, dev, distributed):
-    """S8 (KDLAE-S bs=8 4x512x512) and A64 (ASDQE bs=64 256x256): BASELINE.json configs[2], [3]."""
-    if args.workload == "s8":
-        B = args.batch or 8
-        Fr, H, W = 4, args.size or 512, args.size or 512
+def bench_secondary(args, world, rank, dev, distributed, workload, batch=0, size=0, cpu=True):
+    """S8 (KDLAE-S bs=8 4x512x512) and A64 (ASDQE bs=64 256x256): BASELINE.json configs[2], [3].
+    Returns the result dict (rank 0 prints it, or nests it in the T16 line)."""
+    if workload == "s8":
+        B = batch or 8
+        Fr, H, W = 4, size or 512, size or 512
         model = KDLAE_student(**S_KW)
         x = torch.from_numpy(np.stack([hash_images(f"s8:{rank * B + i}", (Fr, H, W)) for i in range(B)]))
         inputs = (x.to(dev),)
@@ -122,8 +233,8 @@ def bench_secondary(args, world, rank, dev, distributed):
         workload = f"KDLAE-S forward bs={B}/GPU {Fr}x{H}x{W} fp32 (hidden [16,32,64], residual)"
         metric = "samples/sec KDLAE-S 4-frame 512x512 fp32 (BASELINE configs[2])"
     else:
-        B = args.batch or 64
-        H = W = args.size or 256
+        B = batch or 64
+        H = W = size or 256
         model = DenoiseRatePredictor(**A_KW)
         g = torch.from_numpy(np.stack([hash_images(f"a64gt:{rank * B + i}", (3, H, W)) for i in range(B)]))
         lq = (g + 0.1 * torch.from_numpy(hash_uniform("a64n", g.numel()).astype(np.float32)).view_as(g)).clamp(0, 1)
@@ -143,34 +254,28 @@ def bench_secondary(args, world, rank, dev, distributed):
             o = model(*inputs)
             return gather_outputs(o) if gather else o
 
-    out = None
     for _ in range(args.warmup):
-        out = step()
-    torch.cuda.synchronize(dev)
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
-        out = step()
-    ev1.record()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    dev_ms = ev0.elapsed_time(ev1)
-    if distributed:
-        dist.barrier()
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        step()
     # the whole forward runs on torch's current stream, so torch events bracket every launch
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed():
+        ev0.record()
+        for _ in range(args.steps):
+            o = step()
+        ev1.record()
+        return o
+
+    elapsed, _, out = timed_steps(timed, 1, distributed, dev)
+    dev_ms = ev0.elapsed_time(ev1)
+    if distributed:  # the gathered outputs: this rank's shard is rows [rank*B, rank*B + B)
+        out = out[rank * B:(rank + 1) * B]
     ach = flops * args.steps / (dev_ms / 1e3) / 1e12
     roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": "whole forward (all launches)",
             "algorithmic_flops_per_step": flops}
     total = world * B * args.steps
-    res = {"metric": metric, "value": round(total / elapsed, 3), "unit": "images/s" if args.workload == "a64"
+    res = {"metric": metric, "value": round(total / elapsed, 3), "unit": "images/s" if workload == "a64"
            else "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (hash-uniform inputs, hash weights)",
@@ -178,34 +283,29 @@ def bench_secondary(args, world, rank, dev, distributed):
                       "parallelism": f"dp{world} (batch-sharded" + (", RCCL all-gather of outputs in every step)"
                                                                    if gather else ", no data-path collective)")},
            "roofline": roof}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and cpu:
         threads, tdesc = host_cores() if not args.cpu_threads else (args.cpu_threads, "--cpu-threads")
         torch.set_num_threads(threads)
         sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-        # bounded sample: whole samples of the workload until >= 10 s of CPU work (at most B)
-        n, dt, ref = 0, 0.0, None
-        while n < B and dt < 10.0:
-            t0 = time.perf_counter()
-            with torch.no_grad():
-                if args.workload == "s8":
-                    from oracle.kdlae_oracle import StudentCfg, student_forward
-                    r = student_forward(sd, inputs[0][n:n + 1].cpu(), StudentCfg(**S_KW))
-                else:
-                    from oracle.asdqe_oracle import AsdqeCfg, asdqe_forward
-                    r = asdqe_forward(sd, inputs[0][n:n + 1].cpu(), inputs[1][n:n + 1].cpu(), AsdqeCfg(**A_KW))
-            dt += time.perf_counter() - t0
-            ref = r if ref is None else torch.cat([ref, r])
-            n += 1
+        # bounded sample of the same workload (~2-3 s of CPU work per pass): the first n samples
+        n = min(B, 4 if workload == "s8" else 32)
+        if workload == "s8":
+            from oracle.kdlae_oracle import StudentCfg, student_forward
+            xs = inputs[0][:n].cpu()
+            fn = lambda: student_forward(sd, xs, StudentCfg(**S_KW))  # noqa: E731
+        else:
+            from oracle.asdqe_oracle import AsdqeCfg, asdqe_forward
+            lqs, gts = inputs[0][:n].cpu(), inputs[1][:n].cpu()
+            fn = lambda: asdqe_forward(sd, lqs, gts, AsdqeCfg(**A_KW))  # noqa: E731
+        with torch.no_grad():
+            ref, med, ts = cpu_timed(fn)
         got = out[:n].cpu()
-        res["cpu_baseline"] = {"value": round(n / dt, 5), "unit": res["unit"], "cores": threads, "kind": "port",
+        res["cpu_baseline"] = {"value": round(n / med, 5), "unit": res["unit"], "cores": threads, "kind": "port",
                                "cores_from": tdesc,
-                               "sample": f"first {n} samples of the workload batch, torch-CPU oracle, {threads} "
-                                         f"threads, {dt:.1f} s"}
+                               "sample": f"first {n} samples of the workload batch in one call, torch-CPU oracle, "
+                                         f"{threads} threads: 1 warm-up + median of 3 ({', '.join(f'{t:.2f}' for t in ts)} s)"}
         res["parity"] = {"vs": f"CPU oracle, samples 0..{n - 1}", "max_abs": float((got - ref).abs().max())}
-    if rank == 0:
-        print(json.dumps(res), flush=True)
-    if distributed:
-        dist.destroy_process_group()
+    return res
 
 
 def bench_train(args, world, rank, dev, distributed):
@@ -327,20 +427,45 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0 = the host cores this process may use, see host_cores)")
     ap.add_argument("--no-bs1", action="store_true", help="t16: skip the single-image latency line")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="t16: skip the S8 / A64 lines (BASELINE configs[2], [3]) nested in the output")
+    ap.add_argument("--cpu-standin", action="store_true",
+                    help="CPU rehearsal of the N-rank launch/shard/timing path (gloo, stand-in forward; tests)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the ranks before anything here touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], need_gpus=not args.cpu_standin))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(3)
     distributed = world > 1
+    if args.cpu_standin:
+        if distributed:
+            dist.init_process_group("gloo")
+        return bench_standin(args, world, rank)
     if distributed:
+        if torch.cuda.device_count() < world:
+            print(f"bench.py: WORLD_SIZE={world} but {torch.cuda.device_count()} visible GPUs", file=sys.stderr)
+            sys.exit(3)
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     if args.workload == "train":
         return bench_train(args, world, rank, dev, distributed)
     if args.workload != "t16":
-        return bench_secondary(args, world, rank, dev, distributed)
+        res = bench_secondary(args, world, rank, dev, distributed, args.workload, args.batch, args.size,
+                              cpu=not args.no_cpu_baseline)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if distributed:
+            dist.destroy_process_group()
+        return
     H = W = args.size or 512
     B = args.batch or 16
 
@@ -365,26 +490,15 @@ def main():
     L = _lib.lib()
     if args.probe:
         L.kdlae_t_probe_arm(eng.handle, args.probe, args.probe_level)  # creates the event pool in warmup
-    out = None
     for _ in range(args.warmup):
-        out = step()
+        step()
     torch.cuda.synchronize(dev)
     if args.probe:
         L.kdlae_t_probe_arm(eng.handle, args.probe, args.probe_level)
 
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if distributed:
-        dist.barrier()
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, _, out = timed_steps(step, args.steps, distributed, dev)
+    if gather:  # this rank's own images of the gathered batch (for the parity leg)
+        out = {k: (v[rank * B:(rank + 1) * B] if v is not None else None) for k, v in out.items()}
 
     roof = None
     if args.probe:
@@ -495,6 +609,15 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"], res["parity"] = cpu_baseline(model, batch, out, args.cpu_threads)
+    if not args.no_secondary and not args.batch and not args.size:
+        # BASELINE configs[2] / [3] timed in the same run (their own weights, inputs and buffers)
+        del model, batch, out, eng
+        torch.cuda.empty_cache()
+        for wl in ("s8", "a64"):
+            sec = bench_secondary(args, world, rank, dev, distributed, wl, cpu=not args.no_cpu_baseline)
+            keep = ("metric", "value", "unit", "ms_per_step", "config", "roofline", "cpu_baseline", "parity")
+            res[wl] = {k: sec[k] for k in keep if k in sec}
+            torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if distributed:
@@ -551,19 +674,17 @@ def cpu_baseline(model, batch, out, threads):
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     img = batch["img"][:1].cpu()
     rate = batch["denoise_rate"][:1].cpu()
-    t0 = time.perf_counter()
     with torch.no_grad():
-        ref = teacher_forward(sd, img, rate, TeacherCfg(**KW))
-    dt = time.perf_counter() - t0
+        ref, med, ts = cpu_timed(lambda: teacher_forward(sd, img, rate, TeacherCfg(**KW)))
     hq, sr = out["hq"][:1].cpu(), out["sr"][:1].cpu()
     parity = {"vs": "CPU oracle, image 0", "hq_max_abs": float((hq - ref["hq"]).abs().max()),
               "sr_max_abs": float((sr - ref["sr"]).abs().max()),
               "hq_psnr_db": round(psnr(hq, ref["hq"]), 2), "sr_psnr_db": round(psnr(sr, ref["sr"]), 2)}
-    base = {"value": round(1.0 / dt, 5), "unit": "images/s", "cores": threads, "kind": "port",
+    base = {"value": round(1.0 / med, 5), "unit": "images/s", "cores": threads, "kind": "port",
             "cores_from": tdesc,
             "sample": f"1 image 1x3x{img.shape[-2]}x{img.shape[-1]} (image 0 of the bench batch), "
-                      f"torch-CPU oracle, {threads} threads, {dt:.1f} s (one timed run, no warm-up: "
-                      "the sample is bounded to ~30 s of CPU work)"}
+                      f"torch-CPU oracle, {threads} threads: 1 warm-up + median of 3 "
+                      f"({', '.join(f'{t:.1f}' for t in ts)} s)"}
     return base, parity
 
 
