@@ -230,7 +230,7 @@ def bench_secondary(args, world, rank, dev, distributed, workload, batch=0, size
         x = torch.from_numpy(np.stack([hash_images(f"s8:{rank * B + i}", (Fr, H, W)) for i in range(B)]))
         inputs = (x.to(dev),)
         flops = student_flops(S_KW["hidden_channels"], B, Fr, H, W)
-        workload = f"KDLAE-S forward bs={B}/GPU {Fr}x{H}x{W} fp32 (hidden [16,32,64], residual)"
+        desc = f"KDLAE-S forward bs={B}/GPU {Fr}x{H}x{W} fp32 (hidden [16,32,64], residual)"
         metric = "samples/sec KDLAE-S 4-frame 512x512 fp32 (BASELINE configs[2])"
     else:
         B = batch or 64
@@ -240,7 +240,7 @@ def bench_secondary(args, world, rank, dev, distributed, workload, batch=0, size
         lq = (g + 0.1 * torch.from_numpy(hash_uniform("a64n", g.numel()).astype(np.float32)).view_as(g)).clamp(0, 1)
         inputs = (lq.to(dev), g.to(dev))
         flops = asdqe_flops(3, 16, B, H, W)
-        workload = f"ASDQE forward bs={B}/GPU 3x{H}x{W} fp32 (dim 16, eval)"
+        desc = f"ASDQE forward bs={B}/GPU 3x{H}x{W} fp32 (dim 16, eval)"
         metric = "images/sec ASDQE 256x256 fp32 (BASELINE configs[3])"
     load_hash_weights(model)
     model = model.to(dev).eval()
@@ -279,7 +279,7 @@ def bench_secondary(args, world, rank, dev, distributed, workload, batch=0, size
            else "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (hash-uniform inputs, hash weights)",
-           "config": {"workload": workload, "global_batch": world * B, "per_gpu_batch": B,
+           "config": {"workload": desc, "global_batch": world * B, "per_gpu_batch": B,
                       "parallelism": f"dp{world} (batch-sharded" + (", RCCL all-gather of outputs in every step)"
                                                                    if gather else ", no data-path collective)")},
            "roofline": roof}

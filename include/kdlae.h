@@ -16,6 +16,14 @@
  * Error handling: every call returns KDLAE_OK (0) or one of the codes
  * below; kdlae_last_error() returns a thread-local message describing the
  * last failure on the calling thread.
+ *
+ * Environment: the library reads two variables, neither of which changes
+ * results.  KDLAE_DEBUG (comma-separated flags, read when a KDLAE-T handle
+ * first packs its weights) selects between kernel schedules that produce
+ * the same bits: "no_attn_in_fusion" keeps the attention-output GEMM and the
+ * LN + ffn.project_in GEMM separate for C = 48 blocks; "attn_in_split" fuses
+ * the C = 96 blocks' first project_in weight group as well.  KDLAE_PROBE_DUMP
+ * names a CSV file kdlae_t_probe_read writes per-launch timings to.
  */
 #ifndef KDLAE_H_
 #define KDLAE_H_

@@ -331,10 +331,8 @@ int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int 
   const int d = h->cfg.dim, m = 3 * d, ci = h->cfg.in_channels;
   const int Hp = pl.Hp, Wp = pl.Wp;
   int rc;
-  static const bool no_c16 = getenv("KDLAE_NO_C16") != nullptr;
-  static const bool no_lds = getenv("KDLAE_NO_CONV_LDS") != nullptr;
   auto conv = [&](const Gemm& g, View in, View o, int Hh, int Ww, int relu) {
-    if (!no_c16 && g.kt == 1 && g.ksize == 3 && g.ntiles == 1 && g.cg_per_tap == 1 && g.kgroups == 9 &&
+    if (g.kt == 1 && g.ksize == 3 && g.ntiles == 1 && g.cg_per_tap == 1 && g.kgroups == 9 &&
         g.out_mode == 0) {
       // 16 -> 16 channels: LDS-tiled kernel with VGPR-resident weights (conv3d_c16.hip)
       Conv3dC16Params q{};
@@ -353,7 +351,7 @@ int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int 
       HIPCHK(launch_conv3d_c16(q, s));
       return (int)KDLAE_OK;
     }
-    if (!no_lds && g.ksize == 3 && g.out_mode == 0 && g.kt == 1 && conv_lds_supported(g.kt, g.ntiles, g.cg_per_tap * 16)) {
+    if (g.ksize == 3 && g.out_mode == 0 && g.kt == 1 && conv_lds_supported(g.kt, g.ntiles, g.cg_per_tap * 16)) {
       // LDS-tiled implicit GEMM (conv_lds.hip): halo staged once, no per-tap L1 re-reads
       ConvLdsParams q{};
       q.in = in.p;

@@ -425,246 +425,7 @@ __global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnPa
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// r02 schedule ("gdfn2"): no LDS halo, no per-chunk barrier.  A persistent grid of one 4-wave
-// block per CU; after one barrier that stages every chunk's project_out W fragments and dw block
-// in LDS (C = 96: 96 + 20 KiB), each WAVE runs on its own: it owns strips of 16 columns x R rows and,
-// per hidden chunk g, walks the strip's R + 2 input rows top to bottom:
-//   * the three column-shifted 16-pixel rows of x1 and x2 (6 buffer loads, 16 B per lane; rows and
-//     columns outside the image fall outside the descriptor and load zeros = the conv's padding)
-//     are prefetched two input rows ahead, straight into VGPRs (the shifted loads hit the L1/L2
-//     lines of the centre load, so HBM sees each 128 B pixel line about once);
-//   * input row k adds its 3 x 3 taps into the running depthwise sums of output rows k-2..k;
-//   * output row r is complete after input row r+2, gated at r+3 and multiplied (24 MFMAs for
-//     C = 96) at r+4, so the stencil VALU of one row, the gate of the row before and the MFMAs of
-//     the row before that are independent instruction streams the scheduler interleaves.  The
-//     last two rows' gate/MFMA are carried into the next chunk's first two input rows.
-// One wave per SIMD with up to 512 VGPRs: the accumulators of the strip (R x C/16 float4), the
-// three prefetched rows and the chunk's dw weights stay in registers.  r01's kernel spent about a
-// third of its wave cycles parked on the per-chunk barrier / DMA waits (profiles/r02_pmc_*).
-// DPP lane shift of one float.  The empty asm keeps each component a separate scalar: hipcc
-// (ROCm 7.2, -O3) otherwise merges the four update_dpp calls of a float4 into ONE v_mov_b32_dpp of
-// the x component and copies it into y, z and w (wrong results; seen in the ISA of gdfn2 and of a
-// 10-line reproducer, tools/micro/dpp_probe.hip documents the lane mapping).
-template <int CTRL>
-__device__ __forceinline__ float dpp1(float old, float v) {
-  int o = __builtin_bit_cast(int, old), x = __builtin_bit_cast(int, v);
-  asm("" : "+v"(x));
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(o, x, CTRL, 0xf, 0xf, false));
-}
-template <int CTRL>
-__device__ __forceinline__ f32x4 dpp4(const f32x4& old, const f32x4& v) {
-  return f32x4{dpp1<CTRL>(old.x, v.x), dpp1<CTRL>(old.y, v.y), dpp1<CTRL>(old.z, v.z), dpp1<CTRL>(old.w, v.w)};
-}
-
-template <int NT, int R, int WPS>
-__global__ __launch_bounds__(256 * WPS) __attribute__((amdgpu_waves_per_eu(WPS, WPS)))
-void gdfn2_kernel(GdfnParams p, int nunits) {
-  constexpr int K = R + 2;             // input rows per strip and chunk
-  constexpr int PD = WPS == 1 ? 2 : 1;  // rows prefetched ahead (the second wave of a SIMD hides more)
-  constexpr int NS = PD + 1;           // row slots
-  static_assert(K % NS == 0, "the prefetch slots must line up at chunk boundaries");
-  // one wave per SIMD (512 VGPRs): the chunk's dw taps stay in registers; two waves per SIMD
-  // (256 VGPRs): they are re-read from LDS where they are used.  W fragments: always from LDS.
-  constexpr bool kWRegs = WPS == 1;
-  constexpr int WAVES = 4 * WPS;
-  extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
-  const int kch = p.hidS >> 4;
-  f32x4* wl = lds;                          // [kch][NT][64] project_out fragments, chunk-major
-  f32x4* dl = lds + kch * NT * 64;          // [kch][80]     dw taps [9][8] + bias [8]
-  {
-    const f32x4* Wf = reinterpret_cast<const f32x4*>(p.Wp);  // [NT][kch][64]
-    const f32x4* Dw = reinterpret_cast<const f32x4*>(p.dw);  // [kch][128]
-    for (int i = threadIdx.x; i < kch * NT * 64; i += 64 * WAVES) {
-      const int g = i / (NT * 64), rem = i - g * (NT * 64);
-      wl[i] = Wf[((size_t)(rem >> 6) * kch + g) * 64 + (rem & 63)];
-    }
-    for (int i = threadIdx.x; i < kch * 80; i += 64 * WAVES) {
-      const int g = i / 80;
-      dl[i] = Dw[(size_t)g * 128 + (i - g * 80)];
-    }
-  }
-  __syncthreads();
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int li = lane & 15, lq = lane >> 4;
-  const int sx_n = (p.W + 15) >> 4, sy_n = (p.H + R - 1) / R;
-  // XCD-aware split: XCD k (blocks k, k+8, ...) takes a contiguous range of strips, so the strips
-  // whose halos overlap run at the same time under one L2
-  const int per_xcd = (nunits + 7) >> 3;
-  const int u_begin = (int)(blockIdx.x & 7) * per_xcd;
-  const int u_end = min(u_begin + per_xcd, nunits);
-  const int wstride = (int)(gridDim.x >> 3) * WAVES;
-  const unsigned row_bytes = (unsigned)p.W * (unsigned)p.ld * 4u;
-  const unsigned img_bytes = (unsigned)p.H * row_bytes;
-  constexpr unsigned kFar = 0x40000000u;  // row or column offset outside the image (img_bytes <= 2^30)
-
-  for (int u = u_begin + (int)(blockIdx.x >> 3) * WAVES + wave; u < u_end; u += wstride) {
-    const int sc = u % sx_n, t2 = u / sx_n;
-    const int sr = t2 % sy_n, b = t2 / sy_n;
-    const int x0 = sc * 16, y0 = sr * R;
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(p.x + (long long)b * p.H * p.W * p.ld), 0, (int)img_bytes, 0x00020000);
-    // centre column (lane li <-> column x0+li) and the two edge columns (lane 0 <-> x0-1,
-    // lane 15 <-> x0+16; the other lanes' edge offsets fall outside the descriptor)
-    const int xc = x0 + li, xe = li == 0 ? x0 - 1 : (li == 15 ? x0 + 16 : -1);
-    const unsigned ccoff = ((unsigned)xc < (unsigned)p.W ? (unsigned)xc * (unsigned)p.ld * 4u : kFar) + 16u * lq;
-    const unsigned ecoff = ((unsigned)xe < (unsigned)p.W ? (unsigned)xe * (unsigned)p.ld * 4u : kFar) + 16u * lq;
-    // input row k (0..K-1 <-> image row y0-1+k) of chunk g: x1 (h=0) and x2 (h=1), centre and edge
-    auto load_row = [&](int g, int k, f32x4 (&dst)[2][2]) {
-      const int yy = y0 - 1 + k;
-      const unsigned so = ((unsigned)yy < (unsigned)p.H ? (unsigned)yy * row_bytes : kFar) + 128u * (unsigned)g;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        dst[h][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(ccoff + so + 64u * h), 0, 0));
-        dst[h][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(ecoff + so + 64u * h), 0, 0));
-      }
-    };
-    f32x4 acc[R][NT];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 xs[NS][2][2];
-#pragma unroll
-    for (int k = 0; k < PD; ++k) load_row(0, k, xs[k]);
-    // carried from the previous chunk: the depthwise sums of row R-1 (not yet gated) and the gated
-    // row R-2 (not yet multiplied); zeros before chunk 0, so the carried MFMAs add nothing
-    f32x4 dpend[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    f32x4 gpend = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto gate4 = [](const f32x4& a, const f32x4& v) {
-      return f32x4{gelu_erf_g(a.x) * v.x, gelu_erf_g(a.y) * v.y, gelu_erf_g(a.z) * v.z, gelu_erf_g(a.w) * v.w};
-    };
-    auto mfma_row = [&](const f32x4 (&wf)[NT], const f32x4& gb, f32x4 (&ac)[NT]) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) ac[t] = mfma4(wf[t][e], gb[e], ac[t]);
-    };
-    for (int g = 0; g < kch; ++g) {
-      const f32x4* dwl = dl + g * 80;
-      const int gp = g > 0 ? g - 1 : 0;
-      [[maybe_unused]] f32x4 wdw[9][2];
-      if constexpr (kWRegs) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int tap = 0; tap < 9; ++tap) wdw[tap][h] = dwl[tap * 8 + 4 * h + lq];
-      }
-      // tap (row i, column c) of x_h, from registers or (opaque pointer: no hoisting) from LDS
-      auto tapw = [&](const f32x4* dwk, int i, int c, int h) -> f32x4 {
-        if constexpr (kWRegs) return wdw[3 * i + c][h];
-        else return dwk[(3 * i + c) * 8 + 4 * h + lq];
-      };
-      auto mfma_lds = [&](auto prev, const f32x4& gbv, f32x4 (&ac)[NT]) {
-        constexpr bool kPrev = decltype(prev)::value;
-        const f32x4* wk = wl + (kPrev ? gp : g) * NT * 64 + lane;
-        asm("" : "+v"(wk));  // W fragments are read where used (not hoisted into 24 live VGPRs)
-        f32x4 w[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) w[t] = wk[64 * t];
-        mfma_row(w, gbv, ac);
-      };
-      f32x4 d[R][2];      // depthwise sums per output row (only a window of 3 is live)
-      f32x4 gb[R];        // gated rows
-      f32x4 gq;           // gated carried row R-1
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        // prefetch input row k+PD (of this chunk, or the first rows of the next; the last chunk re-reads)
-        if (k + PD < K) load_row(g, k + PD, xs[(k + PD) % NS]);
-        else load_row(g + 1 < kch ? g + 1 : g, k + PD - K, xs[(k + PD) % NS]);
-        const f32x4* dwk = dwl;
-        if constexpr (!kWRegs) asm("" : "+v"(dwk));
-        const f32x4 bdw[2] = {dwk[72 + lq], dwk[76 + lq]};
-        // column neighbours by DPP within each 16-lane row (= one channel quad): row_shr:1 gives
-        // lane i the value of lane i-1, lane 0 keeps the edge load (column x0-1); row_shl:1 alike
-        f32x4 v[2][3];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          v[h][1] = xs[k % NS][h][0];
-          v[h][0] = dpp4<0x111>(xs[k % NS][h][1], v[h][1]);
-          v[h][2] = dpp4<0x101>(xs[k % NS][h][1], v[h][1]);
-        }
-        // stencil: input row k -> output rows k - i (tap row i)
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const int r = k - i;
-          if (r < 0 || r >= R) continue;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            f32x4 s = (i == 0) ? bdw[h] : d[r][h];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              const f32x4 w = tapw(dwk, i, c, h);
-              s.x = fmaf(v[h][c].x, w.x, s.x);
-              s.y = fmaf(v[h][c].y, w.y, s.y);
-              s.z = fmaf(v[h][c].z, w.z, s.z);
-              s.w = fmaf(v[h][c].w, w.w, s.w);
-            }
-            d[r][h] = s;
-          }
-        }
-        // the previous chunk's last rows
-        if (k == 0) {
-          gq = gate4(dpend[0], dpend[1]);
-          mfma_lds(std::true_type{}, gpend, acc[R - 2]);
-        }
-        if (k == 1) mfma_lds(std::true_type{}, gq, acc[R - 1]);
-        // this chunk: gate row k-3, multiply row k-4
-        if (k - 3 >= 0 && k - 3 < R) gb[k - 3] = gate4(d[k - 3][0], d[k - 3][1]);
-        if (k - 4 >= 0 && k - 4 < R) mfma_lds(std::false_type{}, gb[k - 4], acc[k - 4]);
-      }
-      dpend[0] = d[R - 1][0];
-      dpend[1] = d[R - 1][1];
-      gpend = gb[R - 2];
-    }
-    {  // drain the last chunk's carried rows
-      const int gl = kch - 1;
-      f32x4 wf[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) wf[t] = wl[(gl * NT + t) * 64 + lane];
-      const f32x4 gq = gate4(dpend[0], dpend[1]);
-      mfma_row(wf, gpend, acc[R - 2]);
-      mfma_row(wf, gq, acc[R - 1]);
-    }
-    // epilogue: every residual (and the bias) loaded before the first store (vmcnt retires in order)
-    const int xo = x0 + li;
-    const unsigned o_bytes = (unsigned)p.H * (unsigned)p.W * (unsigned)p.ldo * 4u;
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        p.out + (long long)b * p.H * p.W * p.ldo, 0, (int)o_bytes, 0x00020000);
-    f32x4 bias[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-      bias[t] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + 16 * t + 4 * lq) : f32x4{0.f, 0.f, 0.f, 0.f};
-    if (p.R) {
-      const unsigned r_bytes = (unsigned)p.H * (unsigned)p.W * (unsigned)p.ldr * 4u;
-      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(p.R + (long long)b * p.H * p.W * p.ldr), 0, (int)r_bytes, 0x00020000);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int yo = y0 + r;
-        const unsigned off = (yo < p.H && xo < p.W) ? ((unsigned)(yo * p.W + xo) * (unsigned)p.ldr + 4u * lq) * 4u : kOOB2;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          acc[r][t] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(off + 64u * t), 0, 0));
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int yo = y0 + r;
-      const unsigned off = (yo < p.H && xo < p.W) ? ((unsigned)(yo * p.W + xo) * (unsigned)p.ldo + 4u * lq) * 4u : kOOB2;
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4g, acc[r][t] + bias[t]), ro, (int)(off + 64u * t), 0, 0);
-    }
-  }
-}
-
 bool gdfn_supported(int C, int hidS) {
-  // A/B hooks: C = 192 / 384 back on dwconv_gate + the project_out GEMM
-  if (C == 192 && getenv("KDLAE_NO_GDFN192")) return false;
-  if (C == 384 && getenv("KDLAE_NO_GDFN384")) return false;
   return (C == 48 || C == 96 || C == 192 || C == 384) && hidS % 16 == 0 && hidS <= (C >= 192 ? 1024 : 256);
 }
 
@@ -688,35 +449,6 @@ static hipError_t launch_gdfn1(const GdfnParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int NT, int R, int WPS>
-static hipError_t launch_gdfn2(const GdfnParams& p, hipStream_t s) {
-  static size_t attr[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  const int kch = p.hidS / 16;
-  const size_t lds = (size_t)kch * (NT * 64 + 80) * sizeof(f32x4);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (lds > attr[dev]) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gdfn2_kernel<NT, R, WPS>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr[dev] = lds;
-  }
-  const long long units = (long long)p.Bn * ((p.H + R - 1) / R) * ((p.W + 15) / 16);
-  if (units >= (1LL << 31)) return hipErrorInvalidValue;
-  const int grid = std::max(8, device_cu_count() / 8 * 8);  // persistent: one block per CU
-  hipLaunchKernelGGL((gdfn2_kernel<NT, R, WPS>), dim3((unsigned)grid), dim3(256 * WPS), lds, s, p, (int)units);
-  return hipGetLastError();
-}
-
-// gdfn2 needs each image's x (and out / residual) under 2^30 bytes (offset sentinels) and W/dw in LDS
-static bool gdfn2_ok(const GdfnParams& p, int C) {
-  const long long hw = (long long)p.H * p.W;
-  static const bool on = getenv("KDLAE_GDFN2") != nullptr;  // opt-in until it beats r01's kernel
-  return on && hw * p.ld * 4 <= (1LL << 30) && hw * p.ldo * 4 < (1LL << 31) &&
-         (!p.R || hw * p.ldr * 4 < (1LL << 31)) && (size_t)(p.hidS / 16) * ((C / 16) * 64 + 80) * 16 <= 160 * 1024;
-}
-
 static hipError_t launch_gdfn_out_small(const GdfnParams& p, int C, hipStream_t s);
 
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
@@ -736,35 +468,15 @@ hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s) {
 }
 
 static hipError_t launch_gdfn_out_small(const GdfnParams& p, int C, hipStream_t s) {
-  if (gdfn2_ok(p, C)) {
-    static const int rows = getenv("KDLAE_GDFN2_ROWS") ? atoi(getenv("KDLAE_GDFN2_ROWS")) : 10;
-    if (C == 96) return launch_gdfn2<6, 4, 1>(p, s);  // R = 7 spills at NT = 6
-    return rows == 4 ? launch_gdfn2<3, 4, 1>(p, s) : rows == 7 ? launch_gdfn2<3, 7, 1>(p, s) : launch_gdfn2<3, 10, 1>(p, s);
-  }
-  // r01 schedule.  KDLAE_GDFN_TILE picks the tile height / stage ring / waves:
-  //   0: 16 rows, 3 stage slots, 8 waves (one block per CU, 156 KB of LDS; r01's configuration);
-  //   1 (default): 12 rows, 2 slots, 4 waves (C = 96 with the 2-slot W ring: 80 KB; C = 48: 77 KB),
-  //      two independent blocks per CU;
-  //   2: 4 rows, 2 slots, 4 waves (three blocks per CU);  3: 8 rows, 2 slots, 2 waves.
-  static const int tile = getenv("KDLAE_GDFN_TILE") ? atoi(getenv("KDLAE_GDFN_TILE")) : 1;
-  if (C == 96) {
-    if (tile == 0) return launch_gdfn1<6, 8, 16, 3>(p, s);
-    if (tile == 2) return launch_gdfn1<6, 4, 4, 2>(p, s);
-    if (tile == 3) return launch_gdfn1<6, 2, 8, 2>(p, s);
-    // 8: r02's first two-block layout, 16 x 8 tiles with the 3-slot W ring
-    if (tile == 8) return launch_gdfn1<6, 4, 8, 2>(p, s);
-    // default: 16 x 12 tiles with the W ring 2 slots deep (exactly 80 KiB: two blocks per CU):
-    // C96@512^2 3.52 -> 3.37 ms, @256^2 0.866 -> 0.848 ms (profiles/r02_gdfn_c96_tile12_probe.txt)
-    return launch_gdfn1<6, 4, 12, 2, true>(p, s);
-  }
-  if (tile == 0) return launch_gdfn1<3, 8, 16, 3>(p, s);
-  if (tile == 2) return launch_gdfn1<3, 4, 4, 2>(p, s);
-  if (tile == 3) return launch_gdfn1<3, 2, 8, 2>(p, s);
-  // C = 48 default: 16 x 12 tiles, 3 rows per wave.  77 KB of LDS still fits two blocks per CU (the
-  // 3 KiB W records of NT = 3 leave room), and the halo and W/dw refetch per pixel drop by a third:
+  // C = 96: 16 x 12 tiles with the W ring 2 slots deep (exactly 80 KiB: two blocks per CU):
+  // C96@512^2 3.52 -> 3.37 ms, @256^2 0.866 -> 0.848 ms (profiles/r02_gdfn_c96_tile12_probe.txt).
+  // Measured and dropped (profiles/r02_gdfn_tile_variants_probe.txt, r02_gdfn_variants2_probe.txt,
+  // r02_gdfn2_vs_gdfn1_probe.txt): 16 x 16 tiles with 3 stage slots at one block per CU (r01),
+  // 16 x 4 / 16 x 8 tiles, 2-wave blocks, and a barrier-free persistent strip schedule.
+  if (C == 96) return launch_gdfn1<6, 4, 12, 2, true>(p, s);
+  // C = 48: 16 x 12 tiles, 3 rows per wave.  77 KB of LDS still fits two blocks per CU (the 3 KiB W
+  // records of NT = 3 leave room), and the halo and W/dw refetch per pixel drop by a third:
   // C48@1024^2 5.68 -> 5.42 ms, @512^2 1.46 -> 1.42 ms (profiles/r02_gdfn_c48_tile12_probe.txt).
-  // 6: the 16 x 8 tiles of C = 96
-  if (tile == 6) return launch_gdfn1<3, 4, 8, 2>(p, s);
   return launch_gdfn1<3, 4, 12, 2>(p, s);
 }
 

@@ -861,7 +861,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
   X(6, 6, false, 0, true, 2, true) X(3, 6, false, 0, true, 2, true) X(3, 8, false, 0, true, 2, true) \
   X(6, 8, false, 0, true, 2, true) X(6, 12, false, 0, false, 2, true) X(8, 12, false, 0, false, 2, true) \
   X(3, 12, false, 0, false, 2, true) X(6, 16, false, 0, false, 2, true) X(3, 16, false, 0, false, 2, true) \
-  X(4, 3, false, 0, true, 4, true) X(3, 3, false, 0, true, 4, true) \
   X(3, 3, false, 0, false, 2, false) X(6, 6, false, 0, false, 2, false) X(9, 12, false, 0, false, 2, false) \
   X(8, 12, false, 0, false, 2, false) X(6, 12, false, 0, false, 2, false) X(3, 12, false, 0, false, 2, false) \
   X(6, 16, false, 0, false, 2, false) X(3, 16, false, 0, false, 2, false) \
@@ -950,11 +949,6 @@ bool gemm_attn_in_variant(int NT, int KG, int nch) {
   return false;
 }
 
-bool gemm_chunk2_enabled() {
-  static const bool off = getenv("KDLAE_GEMM_CHUNK1") != nullptr;  // A/B hook: the r01 chunked kernel
-  return !off;
-}
-
 bool gemm_has_variant2(int NT, int KG, bool conv3, int out_mode) {
 #define X(a, b, c, o) \
   if (NT == a && KG == b && conv3 == c && out_mode == o) return true;
@@ -990,11 +984,6 @@ static hipError_t launch_chunk2(const GemmParams& p, int grid_x, int grid_y, hip
   return hipGetLastError();
 }
 
-static bool use_res2() {
-  static const bool off = getenv("KDLAE_GEMM_RES1") != nullptr;  // A/B hook: the r01 resident kernel
-  return !off;
-}
-
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s) {
   const bool c3 = p.ksize == 3;
   const bool res = p.group_tiles > 0;
@@ -1026,7 +1015,7 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
 #undef X
     return hipErrorInvalidValue;
   }
-  if (res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && !p.relu && use_res2()) {
+  if (res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && !p.relu) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;
     const int nch = (p.group_tiles + NT - 1) / NT;
@@ -1056,7 +1045,7 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
     lds = (size_t)NT * KG * 1024 + (size_t)NT * 64;
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (!res && gemm_chunk2_enabled() && gemm_has_variant2(NT, KG, c3, p.out_mode) && p.lda % 4 == 0) {
+  if (!res && gemm_has_variant2(NT, KG, c3, p.out_mode) && p.lda % 4 == 0) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long osz = p.out_mode == 2 ? 4 * HW : (p.out_mode == 1 ? HW / 4 : HW);
     const bool fits = HW * p.lda * 4 < (1LL << 31) && osz * p.ldo * 4 < (1LL << 31) &&

@@ -311,10 +311,8 @@ int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int 
   float* tB = buf(pl.tB);
   const DeviceWeights& D = h->dw;
   int rc;
-  static const bool no_c16 = getenv("KDLAE_NO_C16") != nullptr;
-  static const bool no_lds = getenv("KDLAE_NO_CONV_LDS") != nullptr;
   auto conv = [&](const Gemm& g, View in, View o, int Hh, int Ww, int relu) {
-    if (!no_c16 && g.kt == 3 && g.ntiles == 1 && g.cg_per_tap == 1 && g.kgroups == 27) {
+    if (g.kt == 3 && g.ntiles == 1 && g.cg_per_tap == 1 && g.kgroups == 27) {
       // 16 -> 16 channels: LDS-tiled kernel with the weights held in VGPRs (conv3d_c16.hip)
       Conv3dC16Params q{};
       q.in = in.p;
@@ -332,7 +330,7 @@ int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int 
       HIPCHK(launch_conv3d_c16(q, s));
       return (int)KDLAE_OK;
     }
-    if (!no_lds && g.ksize == 3 && g.out_mode == 0 && g.kt == 3 && conv_lds_supported(g.kt, g.ntiles, g.cg_per_tap * 16)) {
+    if (g.ksize == 3 && g.out_mode == 0 && g.kt == 3 && conv_lds_supported(g.kt, g.ntiles, g.cg_per_tap * 16)) {
       // LDS-tiled implicit GEMM (conv_lds.hip): halo staged once, no per-tap L1 re-reads
       ConvLdsParams q{};
       q.in = in.p;

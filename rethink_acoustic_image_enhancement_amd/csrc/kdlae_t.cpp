@@ -31,7 +31,6 @@ struct BlockW {
   size_t dwqkv = kNone, dwqkv_b = kNone, proj = kNone, proj_b = kNone, temp = kNone;
   size_t dwffn = kNone, dwffn_b = kNone;
   bool fused_gdfn = false;  // project_in output chunk-interleaved; dwconv+gate+project_out in one kernel
-  bool fused_ffn = false;   // the whole FFN (LN + project_in + dwconv + gate + project_out) in one kernel
   bool fused_attn_in = false;  // x1 = x + M v, LN and project_in in one GEMM kernel (gemm_attn_in_kernel)
   // when project_in needs two resident weight groups (C = 96): the fused kernel runs group 0 (and
   // forms x1), a plain LN GEMM on x1 runs group 1
@@ -302,7 +301,7 @@ struct Packer {
     // FFN: project_in rows [x1 (hid) | x2 (hid)].  Unfused: stored [x1 padded to hidS | x2 padded
     // to hidS] for the gate kernel.  Fused (gdfn.hip): chunk-interleaved, 16 channels of x1 then the
     // same 16 of x2 per 32-channel chunk, so each chunk of a pixel is one 128 B line.
-    b.fused_gdfn = gdfn_supported(C, hidS) && !getenv("KDLAE_NO_GDFN_FUSION");
+    b.fused_gdfn = gdfn_supported(C, hidS);
     const bool fz = b.fused_gdfn;
     auto rmap = [hid, hidS, fz](int n) -> int {
       if (fz) {
@@ -340,17 +339,15 @@ struct Packer {
     b.pout = pointwise(p + ".ffn.project_out", C, hid, hidS, C, [](int n) { return n; }, "", c.bias, false);
     b.pout.has_res = true;  // x += project_out(...) (unfused path)
     choose_variant(b.pout, false);
-    // opt-in (KDLAE_FFN_FUSION=1): measured 1.8x slower than project_in GEMM + gdfn_out in r02 v1
-    b.fused_ffn = fz && ffn_fused_supported(C, hidS) && getenv("KDLAE_FFN_FUSION") != nullptr;
     // attention output + FFN input in one pass where project_in is one resident weight group
-    // (C = 48); KDLAE_NO_ATTN_IN_FUSION=1 keeps the two GEMMs (A/B hook)
-    const bool no_ai = getenv("KDLAE_NO_ATTN_IN_FUSION") != nullptr;
+    // (C = 48); debug flag no_attn_in_fusion keeps the two GEMMs (bit-identity test)
+    const bool no_ai = debug_flag("no_attn_in_fusion");
     b.fused_attn_in = b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 && b.pin.WPE == 2 &&
                       gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.ntiles + b.pin.NT - 1) / b.pin.NT) && !no_ai;
     // C = 96 (two weight groups): the fused kernel on group 0 + a plain LN GEMM on group 1 measured a
-    // wash (profiles/r02_attn_in_probe.txt: 4637 vs 4598 us at 512^2), so it stays behind
-    // KDLAE_ATTN_IN_SPLIT=1
-    if (!b.fused_attn_in && !no_ai && getenv("KDLAE_ATTN_IN_SPLIT") && b.pin.group_tiles > 0 &&
+    // wash (profiles/r02_attn_in_probe.txt: 4637 vs 4598 us at 512^2), so it stays behind the
+    // attn_in_split debug flag (bit-identity test)
+    if (!b.fused_attn_in && !no_ai && debug_flag("attn_in_split") && b.pin.group_tiles > 0 &&
         b.pin.group_tiles < b.pin.ntiles && 2 * b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 &&
         b.pin.WPE == 2 && gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.group_tiles + b.pin.NT - 1) / b.pin.NT)) {
       const int gt = b.pin.group_tiles;
@@ -392,15 +389,13 @@ struct Plan {
 // Partial Gram slots per (image, head).  The slot partition depends on the image size only, never on
 // the batch: image i of a batch then sums its Gram in exactly the order it does alone (bit-identical
 // batch invariance).  Row-sweep kernel (W % 16 == 0): 16-column strips x at most 8 row segments of
-// at least 32 rows (512^2: 64 rows, the 2-row halo costs 3%; 1024^2: 128 rows); generic kernel:
-// 64-pixel steps grouped 16 per slot.
+// at least 32 rows (512^2: 64 rows, the 2-row halo costs 3%; 1024^2: 128 rows; 4 and 16 segments
+// measured no better, profiles/r02_gram_nseg_probe.txt); generic kernel: 64-pixel steps grouped 16
+// per slot.
 static int nslots_for(int H, int W, int /*B*/, int /*heads*/) {
   if (W % 16 == 0) {
     const int strips = W / 16;
-    // KDLAE_GRAM_NSEG: A/B hook for the most row segments per strip (default 8; 4 and 16 measured
-    // no better, profiles/r02_gram_nseg_probe.txt)
-    static const int max_seg = getenv("KDLAE_GRAM_NSEG") ? std::max(1, atoi(getenv("KDLAE_GRAM_NSEG"))) : 8;
-    const int nseg = std::max(1, std::min(max_seg, (H + 31) / 32));
+    const int nseg = std::max(1, std::min(8, (H + 31) / 32));
     return strips * nseg;
   }
   const int steps = (H * W + 63) / 64;
@@ -532,11 +527,9 @@ struct Fwd {
     return probe_end(1, probeC, bytes, 2.0 * P * g.n_true * g.k_true);
   }
 
-  // One TransformerBlock in place on x, except that with the fully fused FFN (ffn.hip) the block's
-  // output lands in `alt` (*swapped = true): the FFN reads x's 3x3 halo, so it cannot write x.
-  int block(const BlockW& b, View x, View alt, bool* swapped, int Hh, int Ww) {
+  // One TransformerBlock (:159-163) in place on x.
+  int block(const BlockW& b, View x, int Hh, int Ww) {
     const int HW = Hh * Ww;
-    *swapped = false;
     const int ln = h->cfg.layernorm_biasfree ? 1 : 2;
     const long long P = (long long)B * HW;
     int rc;
@@ -559,7 +552,7 @@ struct Fwd {
     gp.H = Hh;
     gp.W = Ww;
     gp.nslots = nslots_for(Hh, Ww, B, b.heads);
-    gp.zeros = getenv("KDLAE_NO_GRAM_RING") ? nullptr : h->P(h->zeros);
+    gp.zeros = h->P(h->zeros);
     const int CT = b.Ch / 16;
     gp.slot_floats = CT * CT * 256 + 2 * b.Ch;
     if ((rc = probe_begin(2, b.C))) return rc;
@@ -569,7 +562,7 @@ struct Fwd {
     HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
     HIPCHK(launch_attn_fold(buf(pl.red), gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
     View fpre{buf(pl.fpre), 2 * b.hidS};
-    const bool fuse_in = b.fused_attn_in && !(b.fused_ffn && alt.p);
+    const bool fuse_in = b.fused_attn_in;
     if (fuse_in) {
       // x1 = x + M v written back into x, LN(x1) -> project_in into fpre, one kernel
       const Gemm& g0 = b.attn_in_split ? b.pin_g0 : b.pin;
@@ -614,31 +607,6 @@ struct Fwd {
       if (rc) return rc;
     }
     // --- feed-forward
-    if (b.fused_ffn && alt.p) {
-      FfnParams fp{};
-      fp.x = x.p;
-      fp.ldx = x.ld;
-      fp.y = alt.p;
-      fp.ldy = alt.ld;
-      fp.Win = h->P(b.pin.w);
-      fp.bin = h->P(b.pin.bias);
-      fp.dw = h->P(b.dwffn);
-      fp.Wout = h->P(b.pout.w);
-      fp.bout = h->P(b.pout.bias);
-      fp.C = b.C;
-      fp.hidS = b.hidS;
-      fp.ln = ln;
-      fp.Bn = B;
-      fp.H = Hh;
-      fp.W = Ww;
-      if ((rc = probe_begin(3, b.C))) return rc;
-      tag = "ffn C" + std::to_string(b.C) + " hid" + std::to_string(b.hid) + " HW" + std::to_string(HW);
-      HIPCHK(launch_ffn_fused(fp, s));
-      *swapped = true;
-      // algorithmic: read x (+ its residual use) and write y; every FFN FLOP (SURVEY 8d model)
-      return probe_end(3, b.C, 4.0 * P * 3.0 * b.C,
-                       2.0 * P * (2.0 * b.hid * b.C + 18.0 * b.hid + (double)b.hid * b.C));
-    }
     if (!fuse_in) {
       rc = gemm(b.pin, h->P(b.pin.w), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
       if (rc) return rc;
@@ -684,22 +652,11 @@ struct Fwd {
     return gemm(b.pout, h->P(b.pout.w), 0, View{buf(pl.fg), b.hidS}, Hh, Ww, x, 0, x.p, x.ld, 0, 0, b.C);
   }
 
-  // Blocks of a stage ping-pong between x and a dense scratch view (the unfused FFN's pre-gate
-  // buffer, free when the FFN is fused) whenever the fused FFN runs; an odd number of swaps ends
-  // with one strided copy back into x.
   int stage(const std::vector<BlockW>& st, View x, int Hh, int Ww) {
-    View cur = x;
-    View alt{nullptr, 0};
     for (const BlockW& b : st) {
-      View other = alt;
-      if (b.fused_ffn) other = (cur.p == x.p) ? View{buf(pl.fpre), b.C} : x;
-      bool swapped = false;
-      int rc = block(b, cur, other, &swapped, Hh, Ww);
+      int rc = block(b, x, Hh, Ww);
       if (rc) return rc;
-      if (swapped) cur = other;
     }
-    if (cur.p != x.p && !st.empty())
-      HIPCHK(launch_copy_view(cur.p, cur.ld, x.p, x.ld, st[0].C, (long long)B * Hh * Ww, s));
     return KDLAE_OK;
   }
 

@@ -94,7 +94,6 @@ struct SmallOutParams {            // 3x3 (ks=3) or pointwise (ks=1) conv with C
 bool gemm_attn_in_variant(int NT, int KG, int nch);
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s);
 bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident, int out_mode);
-bool gemm_chunk2_enabled();
 bool gemm_has_variant2(int NT, int KG, bool conv3, int out_mode);  // r02 chunked kernel
 hipError_t launch_ln_stats(const float* x, int ld, int C, long long P, float* stats, hipStream_t s);
 hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s);
@@ -125,24 +124,6 @@ struct GdfnParams {
 };
 bool gdfn_supported(int C, int hidS);
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s);
-
-// Fully fused FeedForward (ffn.hip): y = x + project_out(gate(dw3x3(project_in(LN(x))))).
-// x and y must be different buffers (the 3x3 halo of a tile reads x that neighbouring tiles
-// would otherwise already have overwritten).
-struct FfnParams {
-  const float* x; int ldx;         // block input (NHWC view)
-  float* y; int ldy;               // block output
-  const float* Win;                // project_in fragments [2 hidS/16][C/16][64][4], chunk-interleaved rows
-  const float* bin;                // folded project_in bias [2 hidS] (same row order) or null
-  const float* dw;                 // per-chunk depthwise blocks (GdfnParams::dw layout)
-  const float* Wout;               // project_out fragments [C/16][hidS/16][64][4]
-  const float* bout;               // [C] or null
-  int C, hidS, ln;                 // ln: 1 BiasFree, 2 WithBias
-  int Bn, H, W;
-};
-bool ffn_fused_supported(int C, int hidS);
-hipError_t launch_ffn_fused(const FfnParams& p, hipStream_t s);
-hipError_t launch_copy_view(const float* src, int ld_src, float* dst, int ld_dst, int C, long long P, hipStream_t s);
 
 // Pre/post-processing around the forward (pipeline.hip)
 struct PreParams {

@@ -616,7 +616,10 @@ hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------- slot reduction
-// reduced[bh][i] = sum over the nslots partial slots, in a fixed order: wave w of a block sums the
+// reduced[bh][i] = sum over the nslots partial slots, in a fixed order and in float64 (each slot is
+// an f32 sum over <= 1024 pixels; the HW-long sum over slots is where f32 loses the most: torch's
+// f32 q.k^T over all HW pixels is what puts the reference's own f32 output 3e-3 from its f64 output
+// on the config-1 MDD input, profiles/r03_config1_precision.txt): wave w of a block sums the
 // slot range [w n / 8, (w+1) n / 8) sequentially for 64 consecutive floats (one 256 B line per
 // load), then lane i adds the 8 wave sums in wave order.  Deterministic and batch-invariant (the
 // slot partition depends on the image size only).  r01's kernel gave each float one thread that
@@ -625,24 +628,24 @@ constexpr int kRedWaves = 8;
 __global__ __launch_bounds__(64 * kRedWaves) void gram_reduce_kernel(const float* __restrict__ partial,
                                                                      float* __restrict__ reduced, int nslots,
                                                                      int slot_floats) {
-  __shared__ float part[kRedWaves][64];
+  __shared__ double part[kRedWaves][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int idx = blockIdx.x * 64 + lane;
   const long long bh = blockIdx.y;
   const int k0 = wave * nslots / kRedWaves, k1 = (wave + 1) * nslots / kRedWaves;
-  float s = 0.f;
+  double s = 0.0;
   if (idx < slot_floats) {
     const float* src = partial + bh * nslots * (long long)slot_floats + idx;
 #pragma unroll 8
-    for (int k = k0; k < k1; ++k) s += src[(long long)k * slot_floats];
+    for (int k = k0; k < k1; ++k) s += (double)src[(long long)k * slot_floats];
   }
   part[wave][lane] = s;
   __syncthreads();
   if (wave == 0 && idx < slot_floats) {
-    float t = part[0][lane];
+    double t = part[0][lane];
 #pragma unroll
     for (int w = 1; w < kRedWaves; ++w) t += part[w][lane];
-    reduced[bh * slot_floats + idx] = t;
+    reduced[bh * slot_floats + idx] = (float)t;
   }
 }
 

@@ -15,19 +15,24 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+bool debug_flag(const char* name) {
+  const char* e = getenv("KDLAE_DEBUG");
+  if (!e) return false;
+  const std::string s(e), n(name);
+  size_t i = 0;
+  while (i <= s.size()) {
+    size_t j = s.find(',', i);
+    if (j == std::string::npos) j = s.size();
+    if (s.compare(i, j - i, n) == 0 && j - i == n.size()) return true;
+    i = j + 1;
+  }
+  return false;
+}
+
 // Tile-shape selection.  Resident schedule when a variant with KG == kgroups exists: the weights
 // are split into groups that fit the LDS budget (one group per grid.y), and NT (accumulator tiles
 // per pass) minimises padding inside a group.  Otherwise the chunked schedule over (NT, KG).
 static constexpr int kLdsBudgetKB = 152;
-
-// KDLAE_GEMM_WPE=2|4 forces one occupancy class where a variant exists (A/B measurement hook).
-static int forced_wpe() {
-  static int v = [] {
-    const char* e = getenv("KDLAE_GEMM_WPE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 
 void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
   static const int nts[] = {1, 2, 3, 4, 6, 8, 9, 12};
@@ -37,8 +42,7 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
   if (g.ksize == 1) {
     int best_nt = 0, best_w = 2;
     double best = 1e30;
-    for (int w : {2, 4}) {
-      if (forced_wpe() && forced_wpe() != w) continue;
+    for (int w : {2}) {
       // two resident blocks per CU at 4 waves/SIMD -> half the LDS budget each
       const int budget_kb = w == 4 ? 76 : kLdsBudgetKB;
       const int budget = std::max(1, budget_kb / g.kgroups);
@@ -56,10 +60,8 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
         // an odd NT leaves each k-group's last tile alone with 2 independent accumulator chains:
         // C96 qkv (18 tiles) measured 2% faster as 3 chunks of 6 than as 2 chunks of 9 on two boxes
         // (profiles/r02_gemm_odd_nt_probe.txt); riding that tile along with the first pair instead
-        // measured no gain.  KDLAE_ODD_NT_PEN overrides the penalty (A/B hook)
-        static const double odd_pen = getenv("KDLAE_ODD_NT_PEN") ? atof(getenv("KDLAE_ODD_NT_PEN")) : 0.05;
-        if (nt % 2) cost += odd_pen;
-        if (!forced_wpe() && w == 4) cost += 1.0;
+        // measured no gain
+        if (nt % 2) cost += 0.05;
         if (cost < best) {
           best = cost;
           best_nt = nt;
@@ -78,23 +80,9 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
     }
   }
   double best = 1e30;
-  const bool v2 = gemm_chunk2_enabled();
-  // A/B hook: KDLAE_C3_VARIANT=<NT>x<KG> forces that chunk shape on every implicit 3x3 layer it exists for
-  static const char* c3v = getenv("KDLAE_C3_VARIANT");
-  if (c3v && g.ksize == 3) {
-    int fnt = 0, fkg = 0;
-    if (sscanf(c3v, "%dx%d", &fnt, &fkg) == 2 && (v2 ? gemm_has_variant2(fnt, fkg, true, g.out_mode)
-                                                     : gemm_has_variant(fnt, fkg, true, 2, false, g.out_mode))) {
-      g.NT = fnt;
-      g.KG = fkg;
-      return;
-    }
-  }
   for (int nt : nts)
     for (int kg : kgs) {
-      if (v2 ? !gemm_has_variant2(nt, kg, g.ksize == 3, g.out_mode) || (g.has_res && nt * kg > 36)
-             : !gemm_has_variant(nt, kg, g.ksize == 3, 2, false, g.out_mode))
-        continue;
+      if (!gemm_has_variant2(nt, kg, g.ksize == 3, g.out_mode) || (g.has_res && nt * kg > 36)) continue;
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
       // every k-chunk restages weights behind two barriers; every n-chunk re-reads A.

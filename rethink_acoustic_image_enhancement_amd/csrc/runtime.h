@@ -17,6 +17,10 @@ namespace kdlae {
 
 extern thread_local std::string g_err;
 int fail(int code, const std::string& msg);
+// Debug switches, read when a handle builds its layer plan: KDLAE_DEBUG is a comma-separated list
+// of flag names (include/kdlae.h lists them).  They select between kernel schedules that give the
+// same bits (the GPU tests compare them); nothing else in the library reads the environment.
+bool debug_flag(const char* name);
 
 #define HIPCHK(x)                                                                                  \
   do {                                                                                             \

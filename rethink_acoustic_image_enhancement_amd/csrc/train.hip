@@ -500,11 +500,6 @@ static void launch_t(const TGemm& g, int kchunk, int flags, int rm, dim3 grid, h
 }
 
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
-// KDLAE_TGEMM_GENERIC=1 routes everything through the generic kernel (A/B comparisons)
-static bool getenv_generic() {
-  static const bool on = getenv("KDLAE_TGEMM_GENERIC") != nullptr;
-  return on;
-}
 
 #ifndef KDLAE_SPLITK_BLOCKS
 #define KDLAE_SPLITK_BLOCKS 2048
@@ -555,7 +550,7 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   const bool xcd = splits == 1 && batch == 1 && tiles >= 64;
   if (xcd) flags |= 8;
   dim3 grid(xcd ? (tiles + 7) / 8 * 8 : tiles, splits, (unsigned)batch);
-  if (g.amode == 0 && g.bmode == 0 && (flags & 3) == 3 && !getenv_generic()) {
+  if (g.amode == 0 && g.bmode == 0 && (flags & 3) == 3) {
     const bool akc = g.sak == 1, bnc = g.sbn == 1;
 #define LEAN(a, b, r) hipLaunchKernelGGL((tgemm_lean_kernel<a, b, r>), grid, dim3(256), 0, s, g, kchunk, flags)
     if (rm == 2) {
@@ -567,11 +562,6 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
     }
 #undef LEAN
   } else if (g.amode == 0 && g.bmode == 0) {
-    static const bool log = getenv("KDLAE_TGEMM_LOG") != nullptr;  // shapes that miss the lean kernel
-    if (log)
-      fprintf(stderr, "tgemm-generic M=%d N=%d K=%d batch=%lld sam=%lld sak=%lld sbk=%lld sbn=%lld A%%16=%d B%%16=%d flags=%d splits=%d\n",
-              g.M, g.N, g.K, batch, (long long)g.sam, (long long)g.sak, (long long)g.sbk, (long long)g.sbn,
-              (int)((uintptr_t)g.A & 15), (int)((uintptr_t)g.B & 15), flags, splits);
     launch_t<0, 0>(g, kchunk, flags, rm, grid, s);
   }
   else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, flags, rm, grid, s);
@@ -936,7 +926,7 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(const float* __restric
 
 hipError_t launch_dw_fwd(const float* in, int ldi, const float* w, const float* b, int flip, int C, int Bn, int H,
                          int W, float* out, int ldo, hipStream_t s) {
-  if (ldi % 4 == 0 && ldo % 4 == 0 && ldi >= (C + 3) / 4 * 4 && !getenv("KDLAE_DW_ROW")) {
+  if (ldi % 4 == 0 && ldo % 4 == 0 && ldi >= (C + 3) / 4 * 4) {
     // QB = 8 quads (32 channels) when 16-quad groups would leave more dead lanes
     const int Cq = (C + 3) / 4;
     const bool q8 = ((Cq + 7) / 8) * 8 < ((Cq + 15) / 16) * 16;

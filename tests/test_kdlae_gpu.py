@@ -74,11 +74,16 @@ def test_rand_512_full_size():
 
 
 def test_mdd_512_config1():
-    """Config 1 (MDD sonar sample 512x512, denoise_rate 0.6).  This input is ill-conditioned in
-    fp32: the reference's OWN fp32 result is ~3e-3 max-abs from its fp64 result (near-black regions
-    drive BiasFree LN towards x / sqrt(1e-5)).  So the bar here is: our distance to the reference's
-    fp64 output is no worse than 1.5x the reference fp32's own distance to it, and stays <= 1e-3 in
-    the mean; plus PSNR >= 60 dB against the reference fp32 output."""
+    """Config 1 (MDD sonar sample 512x512, denoise_rate 0.6).
+
+    The reference's OWN fp32 output is 3.1e-3 (hq) / 3.4e-3 (sr) max-abs from its fp64 output on
+    this input, so no fp32 implementation that sums in a different order can be held to 1e-3 of the
+    reference fp32 numbers.  profiles/r03_config1_precision.txt localises that error: it comes from
+    torch's fp32 q.k^T / norm reductions over all HW pixels in MDTA (with those in fp64 the fp32
+    forward is 5e-4 from fp64).  The HIP path sums 1024-pixel slots in fp32 and the slots in fp64
+    (csrc/mdta.hip gram_reduce), so the bar is: ours is strictly closer to the reference fp64
+    output than the reference fp32 is, on every compared map, and <= 1e-3 of it on the fixture
+    subsample; PSNR >= 60 dB against the reference fp32 output."""
     d, _ = load_fixture("t_mdd_512")
     d, out, sub = _run_512("t_mdd_512", mdd_input_tensor(d))
     for k, r32, r64 in (("hq", "hq_sub", "hq64_sub"), ("sr", "sr_sub", "sr64_sub"),
@@ -89,7 +94,8 @@ def test_mdd_512_config1():
         mean_ours = float((ours - ref64).abs().mean())
         print(f"t_mdd_512 {k}: ours-vs-fp64 {e_ours:.3e} (mean {mean_ours:.2e}), ref32-vs-fp64 {e_ref:.3e}, "
               f"ours-vs-ref32 {float((ours - ref32).abs().max()):.3e}")
-        assert e_ours <= max(1.5 * e_ref, TOL), (k, e_ours, e_ref)
+        assert e_ours <= e_ref, (k, e_ours, e_ref)
+        assert e_ours <= TOL, (k, e_ours)
         assert mean_ours <= TOL
         assert psnr(sub[k], ref32.float()) >= 60.0
 
@@ -140,15 +146,15 @@ def test_batch_invariance_and_determinism():
 @pytest.mark.parametrize("ln,split", [("BiasFree", False), ("WithBias", False), ("BiasFree", True)])
 def test_fused_attention_input_equals_unfused_bit_for_bit(ln, split, monkeypatch):
     """gemm_attn_in_kernel (x1 = x + M v, LN, project_in in one pass: the C = 48 blocks; with
-    KDLAE_ATTN_IN_SPLIT also the C = 96 blocks' first project_in weight group) gives the same bits as
+    KDLAE_DEBUG=attn_in_split also the C = 96 blocks' first project_in weight group) gives the same bits as
     the separate attention-output GEMM + LN/project_in GEMM it replaces."""
     kw = dict(dim=48, LayerNorm_type=ln, num_blocks=[2, 1, 1, 1], num_refinement_blocks=1, bias=ln == "WithBias")
     img = torch.from_numpy(hash_images("fai", (2, 3, 64, 80)))
     rate = torch.from_numpy(hash_images("fair", (2, 1, 64, 80)))
     if split:
-        monkeypatch.setenv("KDLAE_ATTN_IN_SPLIT", "1")
+        monkeypatch.setenv("KDLAE_DEBUG", "attn_in_split")
     fused = _run(_model(kw), img, rate)
-    monkeypatch.setenv("KDLAE_NO_ATTN_IN_FUSION", "1")  # read when a new handle builds its blocks
+    monkeypatch.setenv("KDLAE_DEBUG", "no_attn_in_fusion")  # read when a new handle builds its blocks
     unfused = _run(_model(kw), img, rate)
     assert torch.equal(fused["hq"], unfused["hq"]) and torch.equal(fused["sr"], unfused["sr"])
 

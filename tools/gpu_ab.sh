@@ -14,9 +14,9 @@ for nv in ${VARIANTS:-default=default}; do
     echo "$n: $(tail -1 gpurun_out/ab/gputest_$n.log)"
   fi
   for c in ${PROBE:-1}; do
-    KDLAE_PROBE_DUMP=gpurun_out/ab/probe_c${c}_$n.csv timeout -k 10 200 python -u bench.py --steps 2 --warmup 1 --probe $c --no-cpu-baseline --no-bs1 > gpurun_out/ab/probe_c${c}_$n.json 2> gpurun_out/ab/probe_c${c}_$n.err || exit $?
+    KDLAE_PROBE_DUMP=gpurun_out/ab/probe_c${c}_$n.csv timeout -k 10 200 python -u bench.py --steps 2 --warmup 1 --probe $c --no-cpu-baseline --no-bs1 --no-secondary > gpurun_out/ab/probe_c${c}_$n.json 2> gpurun_out/ab/probe_c${c}_$n.err || exit $?
   done
-  timeout -k 10 200 python -u bench.py --steps 5 --warmup 2 --probe 0 --no-cpu-baseline --no-bs1 > gpurun_out/ab/bench_$n.json 2> gpurun_out/ab/bench_$n.err || exit $?
+  timeout -k 10 200 python -u bench.py --steps 5 --warmup 2 --probe 0 --no-cpu-baseline --no-bs1 --no-secondary > gpurun_out/ab/bench_$n.json 2> gpurun_out/ab/bench_$n.err || exit $?
   echo "$n: $(head -c 150 gpurun_out/ab/bench_$n.json)"
   for e in ${envs//,/ }; do unset "${e%%=*}"; done
 done

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out/mall
 for B in 1 4 16; do
   for c in 1 3; do
-    KDLAE_PROBE_DUMP=gpurun_out/mall/probe_c${c}_b$B.csv timeout -k 10 200 python -u bench.py --batch $B --steps 2 --warmup 1 --probe $c --no-cpu-baseline --no-bs1 > gpurun_out/mall/b${B}_c$c.json 2> gpurun_out/mall/b${B}_c$c.err || exit $?
+    KDLAE_PROBE_DUMP=gpurun_out/mall/probe_c${c}_b$B.csv timeout -k 10 200 python -u bench.py --batch $B --steps 2 --warmup 1 --probe $c --no-cpu-baseline --no-bs1 --no-secondary > gpurun_out/mall/b${B}_c$c.json 2> gpurun_out/mall/b${B}_c$c.err || exit $?
   done
 done
 echo DONE
