@@ -67,6 +67,11 @@ struct kdlae_tt_handle {
   std::vector<int> mark_slot;
   std::vector<int64_t> mark_lo;
   std::vector<hipEvent_t> mark_ev;
+  // the marks and the backward's workspace peak depend only on (has_dsr, B, H, W, forward end):
+  // cached, so a training step does not repeat the host-side dry run
+  int mk_dsr = -1, mk_B = -1, mk_H = -1, mk_W = -1;
+  size_t mk_fwd_end = 0, mk_peak = 0;
+  std::vector<int64_t> mk_keys;  // offsets of every key the backward writes (dry run), sorted
   ~kdlae_tt_handle() {
     for (hipEvent_t e : mark_ev) (void)hipEventDestroy(e);
   }
@@ -483,7 +488,8 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   float* ck = c.alloc((size_t)Bn * heads * Ch);
   float* dtp = c.alloc((size_t)Bn * heads);
   LAUNCH(tr::launch_attn_bwd(r.G, r.sumsq, c.W(p + ".attn.temperature"), r.A, dA, Bn, C, heads, Mq, cq, ck, dtp, c.s));
-  LAUNCH(tr::launch_part_reduce(dtp, Bn, heads, 1, c.G(p + ".attn.temperature"), 0, 1.f, c.s));
+  float* gtemp = c.G(p + ".attn.temperature");  // outside LAUNCH: the dry run must record the write
+  LAUNCH(tr::launch_part_reduce(dtp, Bn, heads, 1, gtemp, 0, 1.f, c.s));
   {
     tr::TGemm g;  // dq[p,i] = sum_j Mq[i,j] k[p,j] + cq[i] q[p,i]
     g.A = r.qkvd + C; g.sam = C3; g.sak = 1; g.bA1 = HW * C3; g.bA2 = Ch;
@@ -850,37 +856,52 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
   if (!h->sv.valid || h->sv.ws != ws)
     return fail(KDLAE_ESTATE, "kdlae_tt_backward_marked needs a preceding kdlae_tt_forward on the same workspace");
   const bool has_dsr = h->cfg.static_train && dsr;
-  std::map<int64_t, std::pair<int, int>> touch;
-  int nmarks = 0;
-  {  // size the backward and find, per mark, which suffix of the flat buffer is final there
-    Ctx d;
-    ctx_init(d, h, nullptr, 0, true, nullptr);
-    d.off = h->sv.fwd_end;
-    d.gr = grad;
-    d.touch = &touch;
-    int rc = net_bwd(d, dhq, dsr, has_dsr);
-    if (rc) return rc;
-    if (d.peak > ws_bytes) return fail(KDLAE_ESTATE, "training workspace too small for the backward");
-    nmarks = d.cur_mark;
+  const bool cached = h->mk_dsr == (int)has_dsr && h->mk_B == h->sv.B && h->mk_H == h->sv.H && h->mk_W == h->sv.W &&
+                      h->mk_fwd_end == h->sv.fwd_end;
+  if (!cached) {
+    std::map<int64_t, std::pair<int, int>> touch;
+    int nmarks = 0;
+    {  // size the backward and find, per mark, which suffix of the flat buffer is final there
+      Ctx d;
+      ctx_init(d, h, nullptr, 0, true, nullptr);
+      d.off = h->sv.fwd_end;
+      d.gr = grad;
+      d.touch = &touch;
+      int rc = net_bwd(d, dhq, dsr, has_dsr);
+      if (rc) return rc;
+      nmarks = d.cur_mark;
+      h->mk_peak = d.peak;
+    }
+    // mark m closes the suffix [lo, total) when lo = the lowest offset written by mark m and every
+    // key at or above lo is untouched (its gradient is the zero fill) or last written by mark m.
+    // One pass from the end of the flat buffer: closed[m] <=> max over keys >= lo of last-write <= m
+    h->mark_slot.assign(nmarks, -1);
+    h->mark_lo.clear();
+    h->mk_keys.clear();
+    std::vector<int64_t> first_lo(nmarks, h->total);  // lowest offset first written at or before mark m
+    for (const auto& kv : touch) {
+      h->mk_keys.push_back(kv.first);
+      for (int m = kv.second.first; m < nmarks && kv.first < first_lo[m]; ++m) first_lo[m] = kv.first;
+    }
+    int64_t prev_lo = h->total;
+    for (int m = 0; m < nmarks; ++m) {
+      const int64_t lo = first_lo[m];
+      if (lo >= prev_lo) continue;
+      bool closed = true;
+      for (auto it = touch.lower_bound(lo); it != touch.end(); ++it)
+        if (it->second.second > m) { closed = false; break; }
+      if (!closed) continue;
+      h->mark_slot[m] = (int)h->mark_lo.size();
+      h->mark_lo.push_back(lo);
+      prev_lo = lo;
+    }
+    h->mk_dsr = (int)has_dsr;
+    h->mk_B = h->sv.B;
+    h->mk_H = h->sv.H;
+    h->mk_W = h->sv.W;
+    h->mk_fwd_end = h->sv.fwd_end;
   }
-  // mark m closes the suffix [lo, total) when lo = the lowest offset written by mark m and every key
-  // at or above lo is untouched (its gradient is the zero fill) or last written by mark m
-  h->mark_slot.assign(nmarks, -1);
-  h->mark_lo.clear();
-  int64_t prev_lo = h->total;
-  for (int m = 0; m < nmarks; ++m) {
-    int64_t lo = h->total;
-    for (const auto& kv : touch)
-      if (kv.second.first <= m) { lo = kv.first; break; }  // map is offset-ordered: first hit = lowest
-    if (lo >= prev_lo) continue;
-    bool closed = true;
-    for (auto it = touch.lower_bound(lo); it != touch.end(); ++it)
-      if (it->second.second > m) { closed = false; break; }
-    if (!closed) continue;
-    h->mark_slot[m] = (int)h->mark_lo.size();
-    h->mark_lo.push_back(lo);
-    prev_lo = lo;
-  }
+  if (h->mk_peak > ws_bytes) return fail(KDLAE_ESTATE, "training workspace too small for the backward");
   kdlae::DeviceGuard dg(h->device);
   while (h->mark_ev.size() < h->mark_lo.size()) {
     hipEvent_t e;
@@ -894,9 +915,19 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
   c.gr = grad;
   c.off = h->sv.fwd_end;
   c.record_marks = true;
+  std::map<int64_t, std::pair<int, int>> written;  // what the real run writes, checked against the marks
+  c.touch = &written;
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
-  return net_bwd(c, dhq, dsr, has_dsr);
+  int rc = net_bwd(c, dhq, dsr, has_dsr);
+  if (rc) return rc;
+  // every gradient the launches wrote must have been seen by the dry run the marks came from (a
+  // write it missed could be all-reduced before it lands)
+  std::vector<int64_t> real;
+  for (const auto& kv : written) real.push_back(kv.first);
+  if (real != h->mk_keys)
+    return fail(KDLAE_ESTATE, "internal: gradient-ready marks disagree with the keys the backward writes");
+  return KDLAE_OK;
 }
 
 int kdlae_tt_mark_count(const kdlae_tt_handle* h) { return h ? (int)h->mark_lo.size() : -1; }

@@ -205,8 +205,10 @@ __syncthreads();
 __host__ __device__ constexpr int gram_waves(int ct) {
   return ct == 1 ? 3 : ct == 2 ? 6 : ct == 3 ? 9 : ct == 4 ? 12 : ct == 5 ? 15 : ct == 6 ? 9 : ct == 7 ? 7 : 12;
 }
+// Ch = 96 ring: 10 waves (one block per CU) measured 2.3% faster per launch than 9 in alternating
+// same-box runs (profiles/r02_gram_ring6_waves10_probe.txt); 11 waves were slower
 #ifndef KDLAE_RING6_WAVES
-#define KDLAE_RING6_WAVES 9
+#define KDLAE_RING6_WAVES 10
 #endif
 // waves per block for the LDS-DMA ring kernel (one block per CU at CT = 6)
 #ifndef KDLAE_RING3_WAVES

@@ -352,17 +352,31 @@ def sync_gradients_bucketed(grad: torch.Tensor, buckets, handle=None, group=None
             w.wait()
         cur.wait_stream(comm)
         return 1.0 / ws
+    if not grad.is_cuda:
+        for _, lo, hi in buckets:
+            dist.all_reduce(grad[lo:hi], op=dist.ReduceOp.SUM, group=group)
+        return 1.0 / ws
+    # gloo on device gradients: the same event-ordered schedule as RCCL, with each bucket staged
+    # through pinned host memory by a stream-ordered copy on the communication stream (so a bucket
+    # leaves the device when its event fires, not after the whole backward)
+    comm = _comm_stream(grad.device)
+    cur = torch.cuda.current_stream(grad.device)
+    staged = []
     for j, lo, hi in buckets:
-        if grad.is_cuda:
-            if j is None:
-                torch.cuda.synchronize(grad.device)
-            else:
-                _lib.check(L.kdlae_tt_mark_sync(handle, j), "kdlae_tt_mark_sync")
-        part = grad[lo:hi]
-        host = part.cpu() if grad.is_cuda else part
+        if j is None:
+            comm.wait_stream(cur)
+        else:
+            _lib.check(L.kdlae_tt_mark_wait(handle, j, ctypes.c_void_p(comm.cuda_stream)), "kdlae_tt_mark_wait")
+        host = torch.empty(hi - lo, dtype=grad.dtype, pin_memory=True)
+        with torch.cuda.stream(comm):
+            host.copy_(grad[lo:hi], non_blocking=True)
+        comm.synchronize()  # this bucket's event wait and copy only
         dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-        if grad.is_cuda:
-            part.copy_(host)
+        with torch.cuda.stream(comm):
+            grad[lo:hi].copy_(host, non_blocking=True)
+        staged.append(host)
+    cur.wait_stream(comm)
+    comm.synchronize()  # the pinned staging buffers outlive their copies
     return 1.0 / ws
 
 

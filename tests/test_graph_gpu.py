@@ -93,3 +93,48 @@ def test_student_and_asdqe_graph_replay():
     torch.cuda.synchronize()
     with torch.no_grad():
         assert torch.equal(score, am(lq, gt))
+
+
+def test_module_replays_its_own_graph_for_repeated_shapes():
+    """KDLAE_teacher.hip_graphs (default): the second call of a shape captures, later calls replay.
+    Replayed outputs equal the launch-by-launch forward bit for bit, follow new inputs and in-place
+    weight updates, are fresh tensors (no aliasing between calls), and survive a workspace regrowth
+    (a larger shape reallocates the workspace: the stale graph must be re-captured, not replayed)."""
+    kw = dict(dim=48, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, LayerNorm_type="BiasFree")
+    m = KDLAE_teacher(**kw)
+    load_hash_weights(m)
+    m = m.to(DEV).eval()
+    assert m.hip_graphs
+
+    def run(img, rate, graphs=True):
+        m.hip_graphs = graphs
+        with torch.no_grad():
+            out = m({"img": img, "denoise_rate": rate})
+        m.hip_graphs = True
+        return out
+
+    img = torch.from_numpy(hash_images("mg_a", (1, 3, 64, 48))).to(DEV)
+    rate = torch.full((1, 1, 64, 48), 0.6, device=DEV)
+    ref = run(img, rate, graphs=False)
+    outs = [run(img, rate) for _ in range(3)]  # eager, capture, replay
+    assert len(m._graphs) == 1
+    for o in outs:
+        assert torch.equal(o["hq"], ref["hq"]) and torch.equal(o["sr"], ref["sr"])
+    assert outs[1]["hq"].data_ptr() != outs[2]["hq"].data_ptr()
+    img2 = torch.from_numpy(hash_images("mg_b", (1, 3, 64, 48))).to(DEV)
+    o2 = run(img2, torch.full_like(rate, 0.3))
+    assert torch.equal(o2["hq"], run(img2, torch.full_like(rate, 0.3), graphs=False)["hq"])
+    assert torch.equal(outs[2]["hq"], ref["hq"])  # an earlier result is untouched by the replay
+    with torch.no_grad():
+        for p in m.parameters():
+            p.data.mul_(0.9)
+    o3 = run(img2, torch.full_like(rate, 0.3))
+    assert torch.equal(o3["sr"], run(img2, torch.full_like(rate, 0.3), graphs=False)["sr"])
+    # a larger shape regrows the workspace; the 64x48 graph must not replay into the freed buffer
+    big = torch.from_numpy(hash_images("mg_c", (2, 3, 96, 96))).to(DEV)
+    brate = torch.full((2, 1, 96, 96), 0.5, device=DEV)
+    for _ in range(3):
+        ob = run(big, brate)
+    assert torch.equal(ob["hq"], run(big, brate, graphs=False)["hq"])
+    o4 = run(img2, torch.full_like(rate, 0.3))
+    assert torch.equal(o4["hq"], run(img2, torch.full_like(rate, 0.3), graphs=False)["hq"])

@@ -81,23 +81,23 @@ def test_mdd_512_config1():
     reference fp32 numbers.  profiles/r03_config1_precision.txt localises that error: it comes from
     torch's fp32 q.k^T / norm reductions over all HW pixels in MDTA (with those in fp64 the fp32
     forward is 5e-4 from fp64).  The HIP path sums 1024-pixel slots in fp32 and the slots in fp64
-    (csrc/mdta.hip gram_reduce), so the bar is: ours is strictly closer to the reference fp64
-    output than the reference fp32 is, on every compared map, and <= 1e-3 of it on the fixture
-    subsample; PSNR >= 60 dB against the reference fp32 output."""
+    (csrc/mdta.hip gram_reduce).  The bar, per output over every fixture sample (the [::8, ::8]
+    subsample plus one full row): ours is at least 25% closer to the reference fp64 output than the
+    reference fp32 is in max-abs, and no farther in the mean; PSNR >= 60 dB against the reference fp32."""
     d, _ = load_fixture("t_mdd_512")
     d, out, sub = _run_512("t_mdd_512", mdd_input_tensor(d))
-    for k, r32, r64 in (("hq", "hq_sub", "hq64_sub"), ("sr", "sr_sub", "sr64_sub"),
-                        ("hq_row", "hq_row257", "hq64_row257"), ("sr_row", "sr_row515", "sr64_row515")):
-        ref32, ref64 = torch.from_numpy(d[r32]).double(), torch.from_numpy(d[r64]).double()
-        ours = sub[k].double()
+    for k, row, r32, r64, w32, w64 in (("hq", "hq_row", "hq_sub", "hq64_sub", "hq_row257", "hq64_row257"),
+                                       ("sr", "sr_row", "sr_sub", "sr64_sub", "sr_row515", "sr64_row515")):
+        ours = torch.cat([sub[k].double().flatten(), sub[row].double().flatten()])
+        ref32 = torch.cat([torch.from_numpy(d[r32]).double().flatten(), torch.from_numpy(d[w32]).double().flatten()])
+        ref64 = torch.cat([torch.from_numpy(d[r64]).double().flatten(), torch.from_numpy(d[w64]).double().flatten()])
         e_ours, e_ref = float((ours - ref64).abs().max()), float((ref32 - ref64).abs().max())
-        mean_ours = float((ours - ref64).abs().mean())
-        print(f"t_mdd_512 {k}: ours-vs-fp64 {e_ours:.3e} (mean {mean_ours:.2e}), ref32-vs-fp64 {e_ref:.3e}, "
-              f"ours-vs-ref32 {float((ours - ref32).abs().max()):.3e}")
-        assert e_ours <= e_ref, (k, e_ours, e_ref)
-        assert e_ours <= TOL, (k, e_ours)
-        assert mean_ours <= TOL
-        assert psnr(sub[k], ref32.float()) >= 60.0
+        m_ours, m_ref = float((ours - ref64).abs().mean()), float((ref32 - ref64).abs().mean())
+        print(f"t_mdd_512 {k}: ours-vs-fp64 max {e_ours:.3e} mean {m_ours:.2e}; ref32-vs-fp64 max {e_ref:.3e} "
+              f"mean {m_ref:.2e}; ours-vs-ref32 max {float((ours - ref32).abs().max()):.3e}")
+        assert e_ours <= 0.75 * e_ref, (k, e_ours, e_ref)
+        assert m_ours <= m_ref, (k, m_ours, m_ref)
+        assert psnr(sub[k], torch.from_numpy(d[r32])) >= 60.0
 
 
 @pytest.mark.parametrize("kw,shape", [

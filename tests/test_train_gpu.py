@@ -247,6 +247,49 @@ def test_marked_backward_equals_backward_and_marks_close_suffixes(cfg):
     assert len(fine) == len(los)
 
 
+def test_mark_events_fire_after_their_suffix_is_final():
+    """The invariant the overlapped all-reduce relies on: once gradient-ready event j has
+    completed, grad[mark_lo(j):] already holds its final values.  A side stream waits on every event
+    (kdlae_tt_mark_wait) and copies the suffix at that moment, while the backward is still running on
+    the main stream; every snapshot must equal the finished gradient.  (A mark that fired early would
+    be caught whenever the side stream copies before the late write lands; the copies are issued while
+    the backward is still in flight — a spin kernel holds the GPU while the host enqueues — which the
+    test checks.)"""
+    m = _model(dict(LayerNorm_type="BiasFree"))
+    B, H, W = 2, 128, 128
+    img = torch.from_numpy(hash_images("img:markev", (B, 3, H, W))).to(DEV)
+    rate = torch.full((B, 1, H, W), 0.6, device=DEV)
+    gt = {"hq": img.clamp(0.2, 0.8), "sr": torch.nn.functional.interpolate(img, scale_factor=2).clamp(0.2, 0.8)}
+    tr = KDLAETrainer(m)
+    inp = {"img": img, "denoise_rate": rate}
+    tr.forward_backward(inp, gt, marked=True)  # first call: the library sizes / caches the marks
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    h = tr.engine.handle
+    n = L.kdlae_tt_mark_count(h)
+    los = [int(L.kdlae_tt_mark_lo(h, j)) for j in range(n)]
+    snaps = [torch.empty(tr.engine.numel - lo, device=DEV) for lo in los]
+    side = torch.cuda.Stream(device=DEV)
+    done = torch.cuda.Event()
+    tr.grad.fill_(float("nan"))  # a snapshot of a not-yet-zeroed or unwritten range shows up as NaN
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)  # hold the GPU while the host enqueues the step and the snapshots
+    tr.forward_backward(inp, gt, marked=True)
+    done.record()
+    for j, lo in enumerate(los):
+        _lib.check(L.kdlae_tt_mark_wait(h, j, ctypes.c_void_p(side.cuda_stream)), "kdlae_tt_mark_wait")
+        with torch.cuda.stream(side):
+            snaps[j].copy_(tr.grad[lo:], non_blocking=True)
+    in_flight = not done.query()  # the snapshots were enqueued before the backward finished
+    torch.cuda.synchronize()
+    final = tr.grad
+    assert torch.isfinite(final).all()
+    bad = [j for j, lo in enumerate(los) if not torch.equal(snaps[j], final[lo:])]
+    print(f"{n} marks, snapshots enqueued while the backward was in flight: {in_flight}")
+    assert not bad, f"marks {bad[:5]} fired before their suffix was final"
+    assert in_flight
+
+
 def test_full_size_step_properties():
     """KDLAET.yml patch setting (6 x 128^2, full network): deterministic gradients, finite values,
     loss decreasing over a few AdamW steps on a fixed batch."""

@@ -5,7 +5,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-cov}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 1000 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u -m pytest $R/tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
+timeout -k 10 1000 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u -m pytest $R/tests -m gpu -v -rP --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; }
 tail -1 $O/gputest.log
 grep "t_mdd_512" $O/gputest.log | head -4
 cd $R
