@@ -19,7 +19,7 @@
  *
  * Environment: the library reads two variables, neither of which changes
  * results.  KDLAE_DEBUG (comma-separated flags, read when a KDLAE-T handle
- * first packs its weights) selects between kernel schedules that produce
+ * builds its pack program: kdlae_t_prepare or the first pack) selects between kernel schedules that produce
  * the same bits: "no_attn_in_fusion" keeps the attention-output GEMM and the
  * LN + ffn.project_in GEMM separate for C = 48 blocks; "attn_in_split" fuses
  * the C = 96 blocks' first project_in weight group as well.  KDLAE_PROBE_DUMP
@@ -85,6 +85,11 @@ int kdlae_t_destroy(kdlae_t_handle* h);
 int kdlae_t_num_params(const kdlae_t_handle* h);
 int kdlae_t_param_info(const kdlae_t_handle* h, int index, const char** name, int64_t* numel);
 int64_t kdlae_t_params_numel(const kdlae_t_handle* h);
+/* Builds and uploads the handle's pack program (device allocation + one synchronous copy; the
+ * program depends on the config only).  Optional: the first pack_device / commit_params does it
+ * otherwise.  Call it once before capturing forwards into a HIP graph, so that no call inside the
+ * capture allocates or synchronises. */
+int kdlae_t_prepare(kdlae_t_handle* h);
 int kdlae_t_pack_device(kdlae_t_handle* h, const float* params, int64_t numel, void* stream);
 int kdlae_t_set_param(kdlae_t_handle* h, const char* name, const float* host_data, int64_t numel);
 int kdlae_t_commit_params(kdlae_t_handle* h, void* stream);
@@ -136,6 +141,7 @@ int kdlae_s_destroy(kdlae_s_handle* h);
 int kdlae_s_num_params(const kdlae_s_handle* h);
 int kdlae_s_param_info(const kdlae_s_handle* h, int index, const char** name, int64_t* numel);
 int64_t kdlae_s_params_numel(const kdlae_s_handle* h);
+int kdlae_s_prepare(kdlae_s_handle* h);  /* as kdlae_t_prepare */
 int kdlae_s_pack_device(kdlae_s_handle* h, const float* params, int64_t numel, void* stream);
 int kdlae_s_set_param(kdlae_s_handle* h, const char* name, const float* host_data, int64_t numel);
 int kdlae_s_commit_params(kdlae_s_handle* h, void* stream);
@@ -169,6 +175,7 @@ int asdqe_destroy(asdqe_handle* h);
 int asdqe_num_params(const asdqe_handle* h);
 int asdqe_param_info(const asdqe_handle* h, int index, const char** name, int64_t* numel);
 int64_t asdqe_params_numel(const asdqe_handle* h);
+int asdqe_prepare(asdqe_handle* h);  /* as kdlae_t_prepare */
 int asdqe_pack_device(asdqe_handle* h, const float* params, int64_t numel, void* stream);
 int asdqe_set_param(asdqe_handle* h, const char* name, const float* host_data, int64_t numel);
 int asdqe_commit_params(asdqe_handle* h, void* stream);

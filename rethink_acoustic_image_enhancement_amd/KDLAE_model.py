@@ -141,6 +141,9 @@ class _Engine:
             names.append((name.value.decode(), int(numel.value)))
         self.keys = names
         self.numel = int(getattr(L, prefix + "_params_numel")(h))
+        # the pack program (device allocation + synchronous upload) is built here, so no forward —
+        # and no HIP-graph capture of one — allocates or synchronises inside the library
+        _lib.check(getattr(L, prefix + "_prepare")(h), prefix + "_prepare")
 
     def _sources(self, module: nn.Module, device) -> list:
         tensors = list(module.parameters()) + list(module.buffers())

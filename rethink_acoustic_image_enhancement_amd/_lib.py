@@ -23,14 +23,14 @@ ERRORS = {0: "OK", 1: "EINVAL_SHAPE", 2: "EINVAL_CONFIG", 3: "EHIP", 4: "EPARAM"
 EXPORTS = (
     "kdlae_last_error", "kdlae_abi_version",
     "kdlae_t_create", "kdlae_t_destroy", "kdlae_t_num_params", "kdlae_t_param_info",
-    "kdlae_t_set_param", "kdlae_t_commit_params", "kdlae_t_params_numel", "kdlae_t_pack_device",
+    "kdlae_t_set_param", "kdlae_t_commit_params", "kdlae_t_params_numel", "kdlae_t_prepare", "kdlae_t_pack_device",
     "kdlae_t_workspace_bytes", "kdlae_t_forward",
     "kdlae_t_probe_arm", "kdlae_t_probe_read",
     "kdlae_s_create", "kdlae_s_destroy", "kdlae_s_num_params", "kdlae_s_param_info",
-    "kdlae_s_set_param", "kdlae_s_commit_params", "kdlae_s_params_numel", "kdlae_s_pack_device",
+    "kdlae_s_set_param", "kdlae_s_commit_params", "kdlae_s_params_numel", "kdlae_s_prepare", "kdlae_s_pack_device",
     "kdlae_s_workspace_bytes", "kdlae_s_forward",
     "asdqe_create", "asdqe_destroy", "asdqe_num_params", "asdqe_param_info", "asdqe_set_param",
-    "asdqe_commit_params", "asdqe_params_numel", "asdqe_pack_device", "asdqe_workspace_bytes", "asdqe_forward",
+    "asdqe_commit_params", "asdqe_params_numel", "asdqe_prepare", "asdqe_pack_device", "asdqe_workspace_bytes", "asdqe_forward",
     "kdlae_padded_size", "kdlae_preprocess_u8", "kdlae_frames_preprocess_u8", "kdlae_postprocess_u8",
     "kdlae_tt_create", "kdlae_tt_destroy", "kdlae_tt_num_params", "kdlae_tt_param_info", "kdlae_tt_num_floats",
     "kdlae_tt_workspace_bytes", "kdlae_tt_forward", "kdlae_tt_backward", "kdlae_tt_backward_marked",
@@ -91,6 +91,7 @@ def lib() -> ctypes.CDLL:
         getattr(L, pre + "_params_numel").argtypes = [c_void_p]
         getattr(L, pre + "_params_numel").restype = c_int64
         getattr(L, pre + "_pack_device").argtypes = [c_void_p, c_void_p, c_int64, c_void_p]
+        getattr(L, pre + "_prepare").argtypes = [c_void_p]
     L.kdlae_t_workspace_bytes.argtypes = [c_void_p, c_int, c_int, c_int]
     L.kdlae_t_workspace_bytes.restype = c_int64
     L.kdlae_t_forward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,

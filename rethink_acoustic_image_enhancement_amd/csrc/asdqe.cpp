@@ -293,6 +293,11 @@ int asdqe_commit_params(asdqe_handle* h, void* stream) {
   return KDLAE_OK;
 }
 
+int asdqe_prepare(asdqe_handle* h) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  return build_program_a(h);
+}
+
 int asdqe_pack_device(asdqe_handle* h, const float* params, int64_t numel, void* stream) {
   if (!h) return fail(KDLAE_ESTATE, "null handle");
   if (numel != h->ps.total)

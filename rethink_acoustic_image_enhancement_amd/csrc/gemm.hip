@@ -467,7 +467,11 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       for (int r = 0; r < kGemmRT; ++r)
 #pragma unroll
         for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
+#if defined(KDLAE_GEMM_ABL_NOLOAD)
+      (void)0;  // ablation (timing only, wrong results): every tile reuses the first tile's A rows
+#else
       load_rows(min(tile + 1, t_end - 1), an);  // unconditional: same op count on every path
+#endif
     } else {
       load_rows(tile, a);
     }
@@ -509,6 +513,10 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
         for (int r = 0; r < kGemmRT; ++r) {
           f32x4 v = acc[t][r] + bias;
           if constexpr (HASR) v += res[t][r];
+#if defined(KDLAE_GEMM_ABL_NOSTORE)
+          // ablation (timing only, wrong results): stores only when a never-true runtime condition holds
+          if (p.kt == -7)
+#endif
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro, tile_voff(ch * NT + t, vo[r], o_bytes),
                                                  0, 0);
         }

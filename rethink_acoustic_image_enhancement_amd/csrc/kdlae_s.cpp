@@ -269,12 +269,17 @@ int kdlae_s_commit_params(kdlae_s_handle* h, void* stream) {
   return KDLAE_OK;
 }
 
+int kdlae_s_prepare(kdlae_s_handle* h) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  return build_program_s(h);
+}
+
 int kdlae_s_pack_device(kdlae_s_handle* h, const float* params, int64_t numel, void* stream) {
   if (!h) return fail(KDLAE_ESTATE, "null handle");
   if (numel != h->ps.total)
     return fail(KDLAE_EPARAM, "flat parameter vector has " + std::to_string(numel) + " floats, expected " +
                                   std::to_string(h->ps.total));
-  int rc = build_program_s(h);
+  int rc = build_program_s(h);  // no-op after kdlae_s_prepare
   if (rc) return rc;
   DeviceGuard g(h->device);
   if ((rc = h->dw.run(params, reinterpret_cast<hipStream_t>(stream)))) return rc;

@@ -877,6 +877,11 @@ int kdlae_t_commit_params(kdlae_t_handle* h, void* stream) {
   return KDLAE_OK;
 }
 
+int kdlae_t_prepare(kdlae_t_handle* h) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  return build_program(h);
+}
+
 int kdlae_t_pack_device(kdlae_t_handle* h, const float* params, int64_t numel, void* stream) {
   if (!h) return fail(KDLAE_ESTATE, "null handle");
   if (numel != h->ps.total)

@@ -210,6 +210,10 @@ __host__ __device__ constexpr int gram_waves(int ct) {
 #ifndef KDLAE_RING6_WAVES
 #define KDLAE_RING6_WAVES 10
 #endif
+// A/B: the ring kernel's stencil window rolls in registers across rows (1 new ring row per row)
+#ifndef KDLAE_GRAM_ROLL
+#define KDLAE_GRAM_ROLL 0
+#endif
 // waves per block for the LDS-DMA ring kernel (one block per CU at CT = 6)
 #ifndef KDLAE_RING3_WAVES
 #define KDLAE_RING3_WAVES 9
@@ -497,6 +501,23 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
         }
       }
     };
+#if KDLAE_GRAM_ROLL
+    // rows r-1 and r of the window of stencil(r) are rows r-1, r of stencil(r-1)'s window already in
+    // registers: shift, and read only ring row r+1 (6 LDS reads per job instead of 18)
+    auto roll_win = [&](int r) {
+      const float* rp = ringf + ((r + 1) % R::NSlot) * R::RowF4 * 4 + 4 * lq * PS + li;
+#pragma unroll
+      for (int j = 0; j < JPW; ++j) {
+        const int co = part[j] * Ch + ctj[j] * 16;
+#pragma unroll
+        for (int c6 = 0; c6 < 6; ++c6) {
+          win[j][0][c6] = win[j][1][c6];
+          win[j][1][c6] = win[j][2][c6];
+          win[j][2][c6] = rp[c6 * PS + co];
+        }
+      }
+    };
+#endif
     auto stencil = [&](int r, int sb, int s) {
 #pragma unroll
       for (int j = 0; j < JPW; ++j) {
@@ -547,7 +568,11 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
           kv[k][s] = ks[buf * 16 * S + lp * S + 16 * jj + li];
         }
       }
+#if KDLAE_GRAM_ROLL
+      if (st) roll_win(y + 1);
+#else
       if (st) load_win(y + 1);
+#endif
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
 #pragma unroll

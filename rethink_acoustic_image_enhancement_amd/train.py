@@ -325,6 +325,25 @@ def grad_buckets(mark_los, numel: int, cap_floats: int):
     return out
 
 
+def allreduce_buckets_rccl(grad: torch.Tensor, buckets, handle, group=None) -> None:
+    """RCCL leg of ``sync_gradients_bucketed``: each bucket's SUM all-reduce is enqueued on the
+    communication stream behind its gradient-ready event; the current stream waits for all of them."""
+    L = _lib.lib()
+    comm = _comm_stream(grad.device)
+    cur = torch.cuda.current_stream(grad.device)
+    works = []
+    for j, lo, hi in buckets:
+        if j is None:
+            comm.wait_stream(cur)
+        else:
+            _lib.check(L.kdlae_tt_mark_wait(handle, j, ctypes.c_void_p(comm.cuda_stream)), "kdlae_tt_mark_wait")
+        with torch.cuda.stream(comm):
+            works.append(dist.all_reduce(grad[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for w in works:
+        w.wait()
+    cur.wait_stream(comm)
+
+
 def sync_gradients_bucketed(grad: torch.Tensor, buckets, handle=None, group=None) -> float:
     """The DDP all-reduce overlapped with the backward: bucket (j, lo, hi) of ``grad`` is all-reduced on
     a communication stream as soon as the backward has recorded gradient-ready event j
@@ -338,19 +357,7 @@ def sync_gradients_bucketed(grad: torch.Tensor, buckets, handle=None, group=None
         return 1.0
     L = _lib.lib()
     if grad.is_cuda and dist.get_backend(group) == "nccl":
-        comm = _comm_stream(grad.device)
-        cur = torch.cuda.current_stream(grad.device)
-        works = []
-        for j, lo, hi in buckets:
-            if j is None:
-                comm.wait_stream(cur)
-            else:
-                _lib.check(L.kdlae_tt_mark_wait(handle, j, ctypes.c_void_p(comm.cuda_stream)), "kdlae_tt_mark_wait")
-            with torch.cuda.stream(comm):
-                works.append(dist.all_reduce(grad[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True))
-        for w in works:
-            w.wait()
-        cur.wait_stream(comm)
+        allreduce_buckets_rccl(grad, buckets, handle, group)
         return 1.0 / ws
     if not grad.is_cuda:
         for _, lo, hi in buckets:
