@@ -366,35 +366,6 @@ __global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnPa
       f32x4 gbn[RPW];
       gate(g + 1, gbn);
       mfma_chunk(g, gb);
-#if defined(KDLAE_GDFN_SGB) && KDLAE_GDFN_SGB > 0
-      // spread the chunk's MFMAs through the next chunk's stencil/gate VALU instead of the
-      // compiler's cluster of MFMAs at the top of the loop (A/B)
-      constexpr int kMf = NT * RPW * 4;
-      if constexpr (KDLAE_GDFN_SGB == 1) {
-        __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);  // the W fragment reads
-#pragma unroll
-        for (int i = 0; i < kMf; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        }
-      } else if constexpr (KDLAE_GDFN_SGB == 2) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-        for (int i = 0; i < kMf; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-        }
-      } else {
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-        for (int i = 0; i < kMf / 2; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 9, 0);
-        }
-      }
-#endif
 #pragma unroll
       for (int r = 0; r < RPW; ++r) gb[r] = gbn[r];
     }

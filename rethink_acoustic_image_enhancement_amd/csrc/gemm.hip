@@ -467,11 +467,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       for (int r = 0; r < kGemmRT; ++r)
 #pragma unroll
         for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
-#if defined(KDLAE_GEMM_ABL_NOLOAD)
-      (void)0;  // ablation (timing only, wrong results): every tile reuses the first tile's A rows
-#else
       load_rows(min(tile + 1, t_end - 1), an);  // unconditional: same op count on every path
-#endif
     } else {
       load_rows(tile, a);
     }
@@ -486,6 +482,73 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       vo[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldo * 4u + 16u * lq + 64u * g0 : o_bytes;
       vr[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldr * 4u + 16u * lq + 64u * g0 : r_bytes;
     }
+    if constexpr (KG == 6) {
+    // K = 96: unit-major chunk body.  Each tile pair is accumulated over every k-group and stored
+    // before the next pair starts, so a pair's stores issue beside the next pair's MFMAs instead of
+    // in one burst after all of them (r03 ablation: dropping the stores sped the K = 96 shapes up
+    // 12-44%); only 4 accumulators are live.  Same per-tile summation order (k-group outer, k-step
+    // inner) as mfma_chunk: bit-identical outputs.  Measured -2..-4% on the KG = 6 shapes; slower for
+    // KG = 3 (+14%, HBM-bound) and KG = 12 (+2%), which keep the chunk-major body
+    // (profiles/r03_gemm_ab_probe.txt).
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const f32x4* wl = wlds + (size_t)ch * NT * KG * 64;
+      const f32x4* bl = wlds + TP * KG * 64 + ch * NT * 4;
+      constexpr int NU = (NT + 1) / 2;
+      f32x4 c0 = wl[lane];
+      f32x4 c1 = NT > 1 ? wl[KG * 64 + lane] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int t = 2 * u;
+        [[maybe_unused]] f32x4 rs[2][kGemmRT];
+        if constexpr (HASR) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int r = 0; r < kGemmRT; ++r)
+              rs[q][r] = (t + q < NT)
+                             ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             rr, tile_voff(ch * NT + t + q, vr[r], r_bytes), 0, 0))
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        f32x4 a0[kGemmRT], a1[kGemmRT];
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) a0[r] = a1[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+          // the next (tile pair, k-group)'s W fragments, read before this one's MFMAs
+          const int ng = g + 1 < KG ? g + 1 : 0;
+          const int nt = g + 1 < KG ? t : t + 2;
+          f32x4 n0 = c0, n1 = c1;
+          if (nt < NT) {
+            n0 = wl[(nt * KG + ng) * 64 + lane];
+            if (nt + 1 < NT) n1 = wl[((nt + 1) * KG + ng) * 64 + lane];
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int r = 0; r < kGemmRT; ++r) {
+              a0[r] = mfma4(c0[s], a[r][g][s], a0[r]);
+              if (t + 1 < NT) a1[r] = mfma4(c1[s], a[r][g][s], a1[r]);
+            }
+          c0 = n0;
+          c1 = n1;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (t + q >= NT) continue;
+          const f32x4 bias = bl[4 * (t + q) + lq];
+#pragma unroll
+          for (int r = 0; r < kGemmRT; ++r) {
+            f32x4 v = (q == 0 ? a0[r] : a1[r]) + bias;
+            if constexpr (HASR) v += rs[q][r];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
+                                                   tile_voff(ch * NT + t + q, vo[r], o_bytes), 0, 0);
+          }
+        }
+      }
+    }
+    } else {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
       [[maybe_unused]] f32x4 res[NT][kGemmRT];
@@ -513,15 +576,12 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
         for (int r = 0; r < kGemmRT; ++r) {
           f32x4 v = acc[t][r] + bias;
           if constexpr (HASR) v += res[t][r];
-#if defined(KDLAE_GEMM_ABL_NOSTORE)
-          // ablation (timing only, wrong results): stores only when a never-true runtime condition holds
-          if (p.kt == -7)
-#endif
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro, tile_voff(ch * NT + t, vo[r], o_bytes),
                                                  0, 0);
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
+    }
     }
   }
 }

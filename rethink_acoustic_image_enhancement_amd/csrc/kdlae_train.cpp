@@ -11,6 +11,8 @@
 // The same code runs in a dry mode (no launches) to size it, so the size is exact.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -72,6 +74,12 @@ struct kdlae_tt_handle {
   int mk_dsr = -1, mk_B = -1, mk_H = -1, mk_W = -1;
   size_t mk_fwd_end = 0, mk_peak = 0;
   std::vector<int64_t> mk_keys;  // offsets of every key the backward writes (dry run), sorted
+  // KDLAE_DEBUG=train_trace: per-launch event pairs of the current call, dumped to KDLAE_PROBE_DUMP
+  struct TraceRec {
+    std::string tag;
+    hipEvent_t a, b;
+  };
+  std::vector<TraceRec> trace;
   ~kdlae_tt_handle() {
     for (hipEvent_t e : mark_ev) (void)hipEventDestroy(e);
   }
@@ -181,6 +189,9 @@ struct Ctx {
   std::map<int64_t, std::pair<int, int>>* touch = nullptr;
   int cur_mark = 0;
   bool record_marks = false;
+  // launch trace (diagnostics only: KDLAE_DEBUG=train_trace); tag = the layer being sequenced
+  std::vector<kdlae_tt_handle::TraceRec>* trace = nullptr;
+  std::string tag;
 
   float* alloc(size_t n) {
     off = (off + 255) / 256 * 256;
@@ -220,10 +231,29 @@ int mark(Ctx& c) {
   return KDLAE_OK;
 }
 
+hipEvent_t trace_begin(Ctx& c) {
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) == hipSuccess) (void)hipEventRecord(e, c.s);
+  return e;
+}
+
+void trace_end(Ctx& c, hipEvent_t a, const char* what) {
+  hipEvent_t b = nullptr;
+  if (!a || hipEventCreate(&b) != hipSuccess) return;
+  (void)hipEventRecord(b, c.s);
+  std::string w(what);
+  const size_t paren = w.find('(');
+  if (paren != std::string::npos) w.resize(paren);
+  if (w.rfind("tr::", 0) == 0) w = w.substr(4);
+  c.trace->push_back({c.tag + "," + w, a, b});
+}
+
 #define LAUNCH(x)                                                                                    \
   do {                                                                                               \
     if (!c.dry) {                                                                                    \
+      hipEvent_t ta_ = c.trace ? trace_begin(c) : nullptr;                                           \
       hipError_t e_ = (x);                                                                           \
+      if (c.trace) trace_end(c, ta_, #x);                                                            \
       if (e_ != hipSuccess) return fail(KDLAE_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     }                                                                                                \
   } while (0)
@@ -234,6 +264,20 @@ int mark(Ctx& c) {
   } while (0)
 
 inline int ld4(int n) { return (n + 3) / 4 * 4; }
+
+// one tgemm launch; `what` (+ the shape) labels it in the launch trace
+int gemm(Ctx& c, const tr::TGemm& g, size_t cap, const std::string& what) {
+  if (c.trace) {
+    const std::string keep = c.tag;
+    c.tag += " " + what + " M" + std::to_string(g.M) + " N" + std::to_string(g.N) + " K" + std::to_string(g.K) + " z" +
+             std::to_string(g.nz1 * g.nz2);
+    LAUNCH(tr::launch_tgemm(g, cap, c.s));
+    c.tag = keep;
+    return KDLAE_OK;
+  }
+  LAUNCH(tr::launch_tgemm(g, cap, c.s));
+  return KDLAE_OK;
+}
 
 int nblk_for(long long rows, long long ncols, int maxb = 1024) {
   long long nb = rows / 128;
@@ -259,7 +303,7 @@ int conv1(Ctx& c, const std::string& n, V x, int Cin, int Cout, long long P, V o
   g.bias = c.W(n + ".bias");
   g.R = R; g.srm = ldr; g.srn = 1;
   g.M = (int)P; g.N = Cout; g.K = Cin;
-  LAUNCH(tr::launch_tgemm(g, 0, c.s));
+  TRY(gemm(c, g, 0, n + " fwd"));
   return KDLAE_OK;
 }
 
@@ -280,7 +324,7 @@ int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long l
   g.C = c.G(n + ".weight"); g.scm = Cin; g.scn = 1;
   g.M = Cout; g.N = Cin; g.K = (int)P;
   g.partial = c.splitk;
-  LAUNCH(tr::launch_tgemm(g, kSplitCap, c.s));
+  TRY(gemm(c, g, kSplitCap, n + " dW"));
   TRY(bias_grad(c, dy, Cout, P, c.G(n + ".bias")));
   if (dx.p) {
     tr::TGemm d;
@@ -289,7 +333,7 @@ int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long l
     d.C = dx.p; d.scm = dx.ld; d.scn = 1;
     d.R = R; d.srm = ldr; d.srn = 1;
     d.M = (int)P; d.N = Cin; d.K = Cout;
-    LAUNCH(tr::launch_tgemm(d, 0, c.s));
+    TRY(gemm(c, d, 0, n + " dX"));
   }
   return KDLAE_OK;
 }
@@ -304,7 +348,7 @@ int conv3(Ctx& c, const std::string& n, V x, int Cin, int Cout, int Bn, int H, i
   g.R = R; g.srm = ldr; g.srn = 1;
   g.M = Bn * H * W; g.N = Cout; g.K = 9 * Cin;
   g.Bn = Bn; g.H = H; g.W = W; g.dil = dil;
-  LAUNCH(tr::launch_tgemm(g, 0, c.s));
+  TRY(gemm(c, g, 0, n + " fwd3"));
   return KDLAE_OK;
 }
 
@@ -319,7 +363,7 @@ int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn
   g.M = Cout; g.N = Cin; g.K = (int)P;
   g.Bn = Bn; g.H = H; g.W = W; g.dil = dil;
   g.partial = c.splitk;
-  LAUNCH(tr::launch_tgemm(g, kSplitCap, c.s));
+  TRY(gemm(c, g, kSplitCap, n + " dW3"));
   TRY(bias_grad(c, dy, Cout, P, c.G(n + ".bias")));
   if (dx.p) {
     tr::TGemm d;  // transposed conv: flipped taps, channels swapped
@@ -329,7 +373,7 @@ int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn
     d.R = R; d.srm = ldr; d.srn = 1;
     d.M = (int)P; d.N = Cin; d.K = 9 * Cout;
     d.Bn = Bn; d.H = H; d.W = W; d.dil = dil;
-    LAUNCH(tr::launch_tgemm(d, 0, c.s));
+    TRY(gemm(c, d, 0, n + " dX3"));
   }
   return KDLAE_OK;
 }
@@ -341,6 +385,7 @@ int block_fwd(Ctx& c, BlockRec& r) {
   const long long HW = (long long)r.H * r.W, P = Bn * HW;
   const int bf = cf.layernorm_biasfree;
   const std::string& p = r.p;
+  c.tag = p;
   r.xn1 = c.alloc(P * C);
   r.st1 = c.alloc(2 * P);
   LAUNCH(tr::launch_ln_fwd(r.x, C, c.W(p + ".norm1.body.weight"), c.W(p + ".norm1.body.bias"), C, P, bf, r.xn1, C,
@@ -366,7 +411,7 @@ int block_fwd(Ctx& c, BlockRec& r) {
     g.C = r.G; g.scm = Ch; g.scn = 1; g.bC1 = (long long)heads * Ch * Ch; g.bC2 = (long long)Ch * Ch;
     g.M = Ch; g.N = Ch; g.K = (int)HW; g.nz1 = Bn; g.nz2 = heads;
     g.partial = c.splitk;
-    LAUNCH(tr::launch_tgemm(g, kSplitCap, c.s));
+    TRY(gemm(c, g, kSplitCap, "gram"));
   }
   r.A = c.alloc(mats);
   LAUNCH(tr::launch_attn_softmax(r.G, r.sumsq, c.W(p + ".attn.temperature"), Bn, C, heads, r.A, c.s));
@@ -377,7 +422,7 @@ int block_fwd(Ctx& c, BlockRec& r) {
     g.B = r.A; g.sbk = 1; g.sbn = Ch; g.bB1 = (long long)heads * Ch * Ch; g.bB2 = (long long)Ch * Ch;
     g.C = r.ao; g.scm = C; g.scn = 1; g.bC1 = HW * C; g.bC2 = Ch;
     g.M = (int)HW; g.N = Ch; g.K = Ch; g.nz1 = Bn; g.nz2 = heads;
-    LAUNCH(tr::launch_tgemm(g, 0, c.s));
+    TRY(gemm(c, g, 0, "av"));
   }
   r.x1 = c.alloc(P * C);
   TRY(conv1(c, p + ".attn.project_out", {r.ao, C}, C, C, P, {r.x1, C}, r.x, C));
@@ -446,6 +491,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   const int C = r.C, C3 = 3 * C, hid = r.hid, heads = r.heads, Ch = C / heads, Bn = r.Bn;
   const long long HW = (long long)r.H * r.W, P = Bn * HW;
   const std::string& p = r.p;
+  c.tag = p;
   const size_t mark = c.off;
   // ffn (KDLAE_model.py:101-106)
   const int L2 = ld4(2 * hid), L1 = ld4(hid);
@@ -473,7 +519,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
     g.C = dA; g.scm = Ch; g.scn = 1; g.bC1 = (long long)heads * Ch * Ch; g.bC2 = (long long)Ch * Ch;
     g.M = Ch; g.N = Ch; g.K = (int)HW; g.nz1 = Bn; g.nz2 = heads;
     g.partial = c.splitk;
-    LAUNCH(tr::launch_tgemm(g, kSplitCap, c.s));
+    TRY(gemm(c, g, kSplitCap, "dA"));
   }
   {
     tr::TGemm g;  // dv[p,j] = sum_i dao[p,i] A[i,j]
@@ -481,7 +527,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
     g.B = r.A; g.sbk = Ch; g.sbn = 1; g.bB1 = (long long)heads * Ch * Ch; g.bB2 = (long long)Ch * Ch;
     g.C = dqkvd + 2 * C; g.scm = C3; g.scn = 1; g.bC1 = HW * C3; g.bC2 = Ch;
     g.M = (int)HW; g.N = Ch; g.K = Ch; g.nz1 = Bn; g.nz2 = heads;
-    LAUNCH(tr::launch_tgemm(g, 0, c.s));
+    TRY(gemm(c, g, 0, "dv"));
   }
   float* Mq = c.alloc(mats);
   float* cq = c.alloc((size_t)Bn * heads * Ch);
@@ -498,13 +544,13 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
     g.R = r.qkvd; g.srm = C3; g.srn = 1; g.bR1 = HW * C3; g.bR2 = Ch;
     g.rs = cq; g.brs1 = (long long)heads * Ch; g.brs2 = Ch;
     g.M = (int)HW; g.N = Ch; g.K = Ch; g.nz1 = Bn; g.nz2 = heads;
-    LAUNCH(tr::launch_tgemm(g, 0, c.s));
+    TRY(gemm(c, g, 0, "dq"));
     g.A = r.qkvd;  // dk[p,j] = sum_i Mq[i,j] q[p,i] + ck[j] k[p,j]
     g.B = Mq; g.sbk = Ch; g.sbn = 1;
     g.C = dqkvd + C;
     g.R = r.qkvd + C;
     g.rs = ck;
-    LAUNCH(tr::launch_tgemm(g, 0, c.s));
+    TRY(gemm(c, g, 0, "dk"));
   }
   float* dqkv = c.alloc(P * C3);
   LAUNCH(tr::launch_dw_fwd(dqkvd, C3, c.W(p + ".attn.qkv_dwconv.weight"), nullptr, 1, C3, Bn, r.H, r.W, dqkv, C3, c.s));
@@ -552,6 +598,7 @@ int net_fwd(Ctx& c, const float* img, const float* rate, float* hq, float* sr) {
   const long long P1 = (long long)B * H * W, P2 = P1 / 4, P3 = P1 / 16, P4 = P1 / 64;
   const int H2 = H / 2, W2 = W / 2, H3 = H / 4, W3 = W / 4, H4 = H / 8, W4 = W / 8;
 
+  c.tag = "net";
   s.img_h = c.alloc(P1 * ic);
   LAUNCH(tr::launch_nchw_to_nhwc(img, ic, B, (long long)H * W, s.img_h, ic, 0, c.s));
   s.pe = c.alloc(P1 * d);
@@ -637,6 +684,7 @@ int net_bwd(Ctx& c, const float* dhq, const float* dsr, bool has_dsr) {
   const long long P1 = (long long)B * H * W, P2 = P1 / 4, P3 = P1 / 16, P4 = P1 / 64;
   const int H2 = H / 2, W2 = W / 2, H3 = H / 4, W3 = W / 4, H4 = H / 8, W4 = W / 8;
 
+  c.tag = "net";
   float* dhq_h = c.alloc(P1 * oc);
   if (dhq) LAUNCH(tr::launch_nchw_to_nhwc(dhq, oc, B, (long long)H * W, dhq_h, oc, 0, c.s));
   else LAUNCH(hipMemsetAsync(dhq_h, 0, P1 * oc * sizeof(float), c.s));
@@ -740,6 +788,24 @@ void ctx_init(Ctx& c, const kdlae_tt_handle* h, void* ws, size_t ws_bytes, bool 
   c.red = c.alloc(kRedCap);
 }
 
+// KDLAE_DEBUG=train_trace: wait for the call's launches and append "phase,layer,kernel,ms" rows to
+// the KDLAE_PROBE_DUMP file (diagnostics; the launches are the same, each bracketed by two events)
+void trace_dump(kdlae_tt_handle* h, hipStream_t s, const char* phase) {
+  if (h->trace.empty()) return;
+  (void)hipStreamSynchronize(s);
+  const char* path = getenv("KDLAE_PROBE_DUMP");
+  FILE* f = path ? fopen(path, "a") : nullptr;
+  for (auto& t : h->trace) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, t.a, t.b);
+    if (f) fprintf(f, "%s,%s,%.5f\n", phase, t.tag.c_str(), ms);
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  if (f) fclose(f);
+  h->trace.clear();
+}
+
 }  // namespace
 
 extern "C" {
@@ -815,9 +881,11 @@ int kdlae_tt_forward(kdlae_tt_handle* h, const float* theta, const float* img, c
   Ctx c;
   ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
   c.th = theta;
+  if (kdlae::debug_flag("train_trace")) c.trace = &h->trace;
   h->sv = Saved{};
   h->sv.B = B; h->sv.H = H; h->sv.W = W;
   rc = net_fwd(c, img, rate, hq, sr);
+  trace_dump(h, c.s, "fwd");
   if (rc) return rc;
   h->sv.ws = ws;
   h->sv.fwd_end = c.off;
@@ -845,9 +913,12 @@ int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, 
   c.th = theta;
   c.gr = grad;
   c.off = h->sv.fwd_end;
+  if (kdlae::debug_flag("train_trace")) c.trace = &h->trace;
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
-  return net_bwd(c, dhq, dsr, has_dsr);
+  const int rc = net_bwd(c, dhq, dsr, has_dsr);
+  trace_dump(h, c.s, "bwd");
+  return rc;
 }
 
 int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float* dhq, const float* dsr, float* grad,
@@ -917,9 +988,11 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
   c.record_marks = true;
   std::map<int64_t, std::pair<int, int>> written;  // what the real run writes, checked against the marks
   c.touch = &written;
+  if (kdlae::debug_flag("train_trace")) c.trace = &h->trace;
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
   int rc = net_bwd(c, dhq, dsr, has_dsr);
+  trace_dump(h, c.s, "bwd");
   if (rc) return rc;
   // every gradient the launches wrote must have been seen by the dry run the marks came from (a
   // write it missed could be all-reduced before it lands)

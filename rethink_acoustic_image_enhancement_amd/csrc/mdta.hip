@@ -210,10 +210,9 @@ __host__ __device__ constexpr int gram_waves(int ct) {
 #ifndef KDLAE_RING6_WAVES
 #define KDLAE_RING6_WAVES 10
 #endif
-// A/B: the ring kernel's stencil window rolls in registers across rows (1 new ring row per row)
-#ifndef KDLAE_GRAM_ROLL
-#define KDLAE_GRAM_ROLL 0
-#endif
+// r03 A/B (profiles/r03_gram_ab_probe.txt, retired): a stencil window rolled in registers across rows
+// (6 LDS reads per job and row instead of 18) and q / k staged transposed with a quad swizzle
+// (ds_read_b128 operands) were both no faster; neither LDS traffic nor issue is this kernel's limit
 // waves per block for the LDS-DMA ring kernel (one block per CU at CT = 6)
 #ifndef KDLAE_RING3_WAVES
 #define KDLAE_RING3_WAVES 9
@@ -387,7 +386,8 @@ struct GramRing {
   static constexpr int RowF4 = Pieces * 64;
   static constexpr int NSlot = 6;
   static constexpr int S = (Ch % 32 == 16) ? Ch : Ch + 16;
-  static constexpr size_t lds_bytes = (size_t)NSlot * RowF4 * 16 + 4 * 16 * S * 4 + 2 * Ch * 4;
+  static constexpr int Stage = 16 * S;  // floats per staging buffer
+  static constexpr size_t lds_bytes = (size_t)NSlot * RowF4 * 16 + 4 * Stage * 4 + 2 * Ch * 4;
   // DMA waves: the leading waves none of whose jobs (w, w + NW, ...) is a v job (job >= 2 CT)
   static constexpr int dma_waves() {
     int n = 0;
@@ -409,9 +409,10 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
   static_assert(NDW >= 1 && 3 * PPD < 64, "ring DMA accounting");
   extern __shared__ __attribute__((aligned(16))) dma::f32x4 gring[];
   float* ringf = reinterpret_cast<float*>(gring);
-  float* qs = ringf + R::NSlot * R::RowF4 * 4;  // [2][16 * S]
-  float* ks = qs + 2 * 16 * S;                  // [2][16 * S]
-  float* nred = ks + 2 * 16 * S;                // [2 Ch]
+  constexpr int ST = R::Stage;
+  float* qs = ringf + R::NSlot * R::RowF4 * 4;  // [2][ST]
+  float* ks = qs + 2 * ST;                      // [2][ST]
+  float* nred = ks + 2 * ST;                    // [2 Ch]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, lq = lane >> 4;
@@ -501,23 +502,6 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
         }
       }
     };
-#if KDLAE_GRAM_ROLL
-    // rows r-1 and r of the window of stencil(r) are rows r-1, r of stencil(r-1)'s window already in
-    // registers: shift, and read only ring row r+1 (6 LDS reads per job instead of 18)
-    auto roll_win = [&](int r) {
-      const float* rp = ringf + ((r + 1) % R::NSlot) * R::RowF4 * 4 + 4 * lq * PS + li;
-#pragma unroll
-      for (int j = 0; j < JPW; ++j) {
-        const int co = part[j] * Ch + ctj[j] * 16;
-#pragma unroll
-        for (int c6 = 0; c6 < 6; ++c6) {
-          win[j][0][c6] = win[j][1][c6];
-          win[j][1][c6] = win[j][2][c6];
-          win[j][2][c6] = rp[c6 * PS + co];
-        }
-      }
-    };
-#endif
     auto stencil = [&](int r, int sb, int s) {
 #pragma unroll
       for (int j = 0; j < JPW; ++j) {
@@ -568,11 +552,7 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
           kv[k][s] = ks[buf * 16 * S + lp * S + 16 * jj + li];
         }
       }
-#if KDLAE_GRAM_ROLL
-      if (st) roll_win(y + 1);
-#else
       if (st) load_win(y + 1);
-#endif
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
 #pragma unroll
