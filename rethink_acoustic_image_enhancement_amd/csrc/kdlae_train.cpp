@@ -294,8 +294,9 @@ struct V {
 };
 
 // wp (optional): the weight as [Cout][ldw] rows (a padded copy), else the flat buffer's [Cout][Cin]
+// pad_ok: `out` is a private ld-rounded buffer whose row pad may be overwritten (TGemm::c_pad_ok)
 int conv1(Ctx& c, const std::string& n, V x, int Cin, int Cout, long long P, V out, const float* R = nullptr,
-          int ldr = 0, V wp = {nullptr, 0}) {
+          int ldr = 0, V wp = {nullptr, 0}, bool pad_ok = false) {
   tr::TGemm g;
   g.A = x.p; g.sam = x.ld; g.sak = 1;
   g.B = wp.p ? wp.p : c.W(n + ".weight"); g.sbk = 1; g.sbn = wp.p ? wp.ld : Cin;
@@ -303,6 +304,7 @@ int conv1(Ctx& c, const std::string& n, V x, int Cin, int Cout, long long P, V o
   g.bias = c.W(n + ".bias");
   g.R = R; g.srm = ldr; g.srn = 1;
   g.M = (int)P; g.N = Cout; g.K = Cin;
+  g.c_pad_ok = pad_ok;
   TRY(gemm(c, g, 0, n + " fwd"));
   return KDLAE_OK;
 }
@@ -317,7 +319,7 @@ int bias_grad(Ctx& c, V dy, int N, long long P, float* out) {
 
 // dW = dY^T X, db = colsum dY, dX = dY W (+R)
 int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long long P, V dx, const float* R = nullptr,
-              int ldr = 0, V wp = {nullptr, 0}) {
+              int ldr = 0, V wp = {nullptr, 0}, bool pad_ok = false) {
   tr::TGemm g;
   g.A = dy.p; g.sam = 1; g.sak = dy.ld;
   g.B = x.p; g.sbk = x.ld; g.sbn = 1;
@@ -333,6 +335,7 @@ int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long l
     d.C = dx.p; d.scm = dx.ld; d.scn = 1;
     d.R = R; d.srm = ldr; d.srn = 1;
     d.M = (int)P; d.N = Cin; d.K = Cout;
+    d.c_pad_ok = pad_ok;
     TRY(gemm(c, d, 0, n + " dX"));
   }
   return KDLAE_OK;
@@ -433,7 +436,7 @@ int block_fwd(Ctx& c, BlockRec& r) {
   // hidden-width buffers get a pixel stride rounded up to 4 floats so GEMM rows stay float4-aligned
   const int L2 = ld4(2 * hid), L1 = ld4(hid);
   r.y = c.alloc(P * L2);
-  TRY(conv1(c, p + ".ffn.project_in", {r.xn2, C}, C, 2 * hid, P, {r.y, L2}));
+  TRY(conv1(c, p + ".ffn.project_in", {r.xn2, C}, C, 2 * hid, P, {r.y, L2}, nullptr, 0, {nullptr, 0}, true));
   r.yd = c.alloc(P * L2);
   LAUNCH(tr::launch_dw_fwd(r.y, L2, c.W(p + ".ffn.dwconv.weight"), c.W(p + ".ffn.dwconv.bias"), 0, 2 * hid, Bn,
                            r.H, r.W, r.yd, L2, c.s));
@@ -496,7 +499,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   // ffn (KDLAE_model.py:101-106)
   const int L2 = ld4(2 * hid), L1 = ld4(hid);
   float* dg = c.alloc(P * L1);
-  TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, L1}, {d, C}, hid, C, P, {dg, L1}, nullptr, 0, {r.wpo, L1}));
+  TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, L1}, {d, C}, hid, C, P, {dg, L1}, nullptr, 0, {r.wpo, L1}, true));
   float* dyd = c.alloc(P * L2);
   LAUNCH(tr::launch_gate_bwd(dg, L1, r.yd, L2, hid, P, dyd, L2, c.s));
   float* dy = c.alloc(P * L2);

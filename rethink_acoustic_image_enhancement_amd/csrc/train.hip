@@ -507,8 +507,23 @@ static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 #ifndef KDLAE_SPLITK_MIN
 #define KDLAE_SPLITK_MIN 256
 #endif
+#ifndef KDLAE_TRAIN_ROWS
+#define KDLAE_TRAIN_ROWS 1
+#endif
+#ifndef KDLAE_TRAIN_COLS
+#define KDLAE_TRAIN_COLS 1
+#endif
+hipError_t launch_tgemm_reduce(const TGemm& g, hipStream_t s) {
+  const long long MN = (long long)g.M * g.N;
+  hipLaunchKernelGGL(tgemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64), (unsigned)(g.nz1 * g.nz2)), dim3(1024), 0,
+                     s, g);
+  return hipGetLastError();
+}
+
 hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  if (KDLAE_TRAIN_ROWS && !g.partial && tgemm_rows_eligible(g)) return launch_tgemm_rows(g, s);
+  if (KDLAE_TRAIN_COLS && g.partial && partial_cap > 0 && tgemm_cols_eligible(g)) return launch_tgemm_cols(g, partial_cap, s);
   const long long batch = (long long)g.nz1 * g.nz2;
   // 128-row tiles when the grid still holds >= 2 blocks per CU with them (tall activation GEMMs)
   const int rm = ((long long)((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * batch >= 512) ? 2 : 1;
@@ -568,10 +583,7 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, flags, rm, grid, s);
   else return hipErrorInvalidValue;
-  if (splits > 1) {
-    const long long MN = (long long)g.M * g.N;
-    hipLaunchKernelGGL(tgemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64), (unsigned)batch), dim3(1024), 0, s, g);
-  }
+  if (splits > 1) return launch_tgemm_reduce(g, s);
   return hipGetLastError();
 }
 

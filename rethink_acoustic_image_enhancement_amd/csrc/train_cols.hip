@@ -1,0 +1,201 @@
+// Pixel-reduction MFMA GEMM of the training step (gfx950): C(m, n) = sum_p A(m, p) B(p, n) where the
+// contraction runs over pixels — the 1x1 conv weight gradient dW = dY^T X
+// (Train/basicsr/models/image_restoration_model.py:213 l_pix.backward() through KDLAE_model.py:99-106,
+// :127, :143) and the MDTA Gram G = q^T k / dA = dout^T v per (image, head) (KDLAE_model.py:137-138).
+// Both operands are NHWC rows (channels contiguous): A(m, p) = A[p * lda + m], B(p, n) = B[p * ldb + n].
+//
+// v_mfma_f32_16x16x4_f32 takes its k (= pixel) index from lane >> 4 for both operands, so lane
+// (li, lq) supplies A[pixel 4j + lq][16i + li] and B[pixel 4j + lq][16t + li]: one dword per
+// operand tile per k-step, straight from HBM into VGPRs (16 lanes read 64 contiguous bytes of one
+// pixel row; the tiles of a wave cover whole lines).  A wave owns TM x TN accumulator tiles over a
+// pixel chunk; each loaded A value feeds TN MFMAs and each B value TM, so the wave moves
+// (TM + TN) x 256 B per TM x TN MFMAs.  The four waves of a block take neighbouring wave tiles of
+// the same pixel chunk (their rows meet in L1/L2).  Pixel chunks are split-K partials
+// [batch][chunk][M][N], summed in fixed order by tgemm_reduce_kernel: deterministic.
+// Loads are unconditional buffer ops (rows past P / channels past M, N read 0 through the
+// descriptor range), so the prefetch of the next k-steps is never drained by a dynamic vmcnt.
+#include <stdint.h>
+
+#include "train_kernels.h"
+
+namespace kdlae {
+namespace train {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kU = 4;          // k-steps (4 pixels each) per pipeline stage
+
+struct ColsArgs {
+  TGemm g;
+  int kchunk;     // pixels per chunk (multiple of 4 kU)
+  int splits;     // chunks
+  int mt, nt;     // 16-wide tiles along M and N
+  int wtm, wtn;   // wave tiles along M and N
+};
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, long long bytes) {
+  const long long cap = 0x7fffff00LL;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)(bytes < cap ? bytes : cap), 0x00020000);
+}
+constexpr unsigned kOOB = 0x80000000u;
+
+template <int TM, int TN>
+__global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
+  const TGemm& g = a.g;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int wt = blockIdx.y * 4 + wave;
+  if (wt >= a.wtm * a.wtn) return;  // wave-uniform; no block barrier below
+  const int wm = wt / a.wtn, wn = wt - wm * a.wtn;
+  const int z = blockIdx.z, z1 = z / g.nz2, z2 = z - z1 * g.nz2;
+  const int ks = blockIdx.x;
+  const int p0 = ks * a.kchunk, p1 = min(g.K, p0 + a.kchunk);
+  // operands: A(m, p) = A[p * sak + m] (sam == 1), B(p, n) = B[p * sbk + n] (sbn == 1)
+  const float* A = g.A + z1 * g.bA1 + z2 * g.bA2;
+  const float* B = g.B + z1 * g.bB1 + z2 * g.bB2;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(A, (long long)(p1 - 1) * g.sak * 4 + 4LL * g.M);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(B, (long long)(p1 - 1) * g.sbk * 4 + 4LL * g.N);
+  // this lane's byte offset of pixel lq, column 16 tile + li, per tile (kOOB past M / N); a k-step
+  // adds a wave-uniform pixel offset.  Pixels >= p1 fall past the descriptor range by themselves
+  // (row stride >= M, N), so no load carries a per-lane condition.
+  const unsigned sa = (unsigned)g.sak * 4u, sb = (unsigned)g.sbk * 4u;
+  unsigned am[TM], bn[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = (wm * TM + i) * 16 + li;
+    am[i] = m < g.M ? (unsigned)lq * sa + 4u * (unsigned)m : kOOB;
+  }
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int n = (wn * TN + t) * 16 + li;
+    bn[t] = n < g.N ? (unsigned)lq * sb + 4u * (unsigned)n : kOOB;
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int t = 0; t < TN; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // stage = kU k-steps = 4 kU pixels: lane reads pixel q + 4u + lq for u < kU
+  auto load = [&](int q, float (&av)[kU][TM], float (&bv)[kU][TN]) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const unsigned pa = (unsigned)(q + 4 * u) * sa, pb = (unsigned)(q + 4 * u) * sb;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        av[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, (int)(am[i] + pa), 0, 0));
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        bv[u][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (int)(bn[t] + pb), 0, 0));
+    }
+  };
+  auto compute = [&](const float (&av)[kU][TM], const float (&bv)[kU][TN]) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int t = 0; t < TN; ++t) acc[i][t] = mfma4(av[u][i], bv[u][t], acc[i][t]);
+  };
+
+  constexpr int kStage = 4 * kU;
+  float a0[kU][TM], b0[kU][TN], a1[kU][TM], b1[kU][TN];
+  if (p0 < p1) {
+    load(p0, a0, b0);
+    for (int q = p0; q < p1; q += 2 * kStage) {
+      if (q + kStage < p1) load(q + kStage, a1, b1);
+      compute(a0, b0);
+      if (q + kStage >= p1) break;
+      if (q + 2 * kStage < p1) load(q + 2 * kStage, a0, b0);
+      compute(a1, b1);
+    }
+  }
+  // partial [z][ks][M][N]: lane (li, lq) of (i, t) holds rows 16(wm TM + i) + 4lq + r, column 16(wn TN + t) + li
+  float* part = g.partial + ((long long)z * a.splits + ks) * g.M * g.N;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const int n = (wn * TN + t) * 16 + li;
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = (wm * TM + i) * 16 + 4 * lq + r;
+        if (m < g.M) part[(long long)m * g.N + n] = acc[i][t][r];
+      }
+    }
+}
+
+template <int TM, int TN>
+hipError_t launch_tt(const ColsArgs& a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((tgemm_cols_kernel<TM, TN>), grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+#ifndef KDLAE_COLS_WAVES
+#define KDLAE_COLS_WAVES 4096
+#endif
+
+bool tgemm_cols_eligible(const TGemm& g) {
+  if (g.amode != 0 || g.bmode != 0 || g.alpha != 1.f || !g.partial) return false;
+  if (g.sam != 1 || g.sbn != 1 || g.M <= 0 || g.N <= 0 || g.K <= 0) return false;
+  if ((long long)g.K * g.sak * 4 >= (1LL << 31) - 64 || (long long)g.K * g.sbk * 4 >= (1LL << 31) - 64) return false;
+  return true;
+}
+
+hipError_t launch_tgemm_cols(TGemm g, size_t partial_cap, hipStream_t s) {
+  if (!tgemm_cols_eligible(g)) return hipErrorInvalidValue;
+  ColsArgs a;
+  a.mt = (g.M + 15) / 16;
+  a.nt = (g.N + 15) / 16;
+  // wave tile: TM, TN in {2, 3, 4}, the least padded
+  auto pick = [](int tiles) {
+    int best = 4, pad = 1 << 30;
+    for (int c = 4; c >= 2; --c) {
+      const int p = (tiles + c - 1) / c * c;
+      if (p < pad) best = c, pad = p;
+    }
+    return best;
+  };
+  const int TM = pick(a.mt), TN = (TM == 4 && pick(a.nt) == 4) ? 2 : pick(a.nt);  // 4 x 4 spills
+  a.wtm = (a.mt + TM - 1) / TM;
+  a.wtn = (a.nt + TN - 1) / TN;
+  const int wtiles = a.wtm * a.wtn;
+  const int gy = (wtiles + 3) / 4;
+  const long long batch = (long long)g.nz1 * g.nz2;
+  // pixel chunks: ~KDLAE_COLS_WAVES waves in all, chunks of >= 256 pixels, partials within capacity
+  long long splits = (KDLAE_COLS_WAVES + (long long)wtiles * batch - 1) / ((long long)wtiles * batch);
+  const long long maxs = (g.K + 255) / 256;
+  if (splits > maxs) splits = maxs;
+  const long long cap = (long long)(partial_cap / ((size_t)g.M * g.N * batch));
+  if (splits > cap) splits = cap;
+  if (splits < 1) return hipErrorInvalidValue;
+  int kchunk = (int)((g.K + splits - 1) / splits);
+  kchunk = (kchunk + 4 * kU - 1) / (4 * kU) * (4 * kU);
+  splits = (g.K + kchunk - 1) / kchunk;
+  a.kchunk = kchunk;
+  a.splits = (int)splits;
+  g.splits = (int)splits;
+  a.g = g;
+  const dim3 grid((unsigned)splits, (unsigned)gy, (unsigned)batch);
+  hipError_t e;
+#define TT(m, n) \
+  if (TM == m && TN == n) e = launch_tt<m, n>(a, grid, s); else
+  TT(2, 2) TT(2, 3) TT(2, 4) TT(3, 2) TT(3, 3) TT(3, 4) TT(4, 2) TT(4, 3) e = hipErrorInvalidValue;
+#undef TT
+  if (e != hipSuccess) return e;
+  return launch_tgemm_reduce(g, s);
+}
+
+}  // namespace train
+}  // namespace kdlae

@@ -36,9 +36,23 @@ struct TGemm {
   // im2col geometry (amode 1 / bmode 1..3)
   int Bn = 0, H = 0, W = 0, Cg = 0, dil = 1; long long lda = 0, ldb = 0;
   int splits = 1; float* partial = nullptr;
+  // the C view's row pad [N, ld4(N)) belongs to nobody else (a ld-rounded private buffer): a
+  // kernel may store whole float4 quads there (zeros: the weights past N are zero)
+  bool c_pad_ok = false;
 };
 // Launch; picks split-K itself when `partial` (capacity `partial_cap` floats) is given.
 hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s);
+// Row-streaming kernel (train_rows.hip) for plain contractions with k-contiguous A rows and no
+// split-K: weights staged in LDS in MFMA fragment order, A streamed to VGPRs.  launch_tgemm routes
+// every eligible call there.
+bool tgemm_rows_eligible(const TGemm& g);
+hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s);
+// Pixel-reduction kernel (train_cols.hip) for split-K contractions over pixels with channel-
+// contiguous operands (1x1 dW, MDTA Gram / dA): split-K partials + launch_tgemm_reduce.
+bool tgemm_cols_eligible(const TGemm& g);
+hipError_t launch_tgemm_cols(TGemm g, size_t partial_cap, hipStream_t s);
+// fixed-order sum of g.splits partials ([batch][splits][M][N] at g.partial) + the epilogue into C
+hipError_t launch_tgemm_reduce(const TGemm& g, hipStream_t s);
 
 // LayerNorm over channels per pixel (KDLAE_model.py:50-52 BiasFree, :67-70 WithBias), eps 1e-5.
 // forward: y = LN(x) * w (+ b); stats[p] = (mean, rstd)
