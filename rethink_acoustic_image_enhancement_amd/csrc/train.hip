@@ -522,8 +522,15 @@ hipError_t launch_tgemm_reduce(const TGemm& g, hipStream_t s) {
 
 hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
-  if (KDLAE_TRAIN_ROWS && !g.partial && tgemm_rows_eligible(g)) return launch_tgemm_rows(g, s);
-  if (KDLAE_TRAIN_COLS && g.partial && partial_cap > 0 && tgemm_cols_eligible(g)) return launch_tgemm_cols(g, partial_cap, s);
+  // r03 per-shape sweep (tools/micro/rows_bench.cpp, profiles/r03_train_gemm_bench.txt): the row-
+  // streaming and pixel-reduction kernels win 25-55% on the tall contractions; on the 64^2 / 32^2
+  // levels (a few thousand rows, K or N up to 2042) the tiled kernel's finer grid is faster
+  const long long rows = (long long)g.M * g.nz1 * g.nz2;
+  if (KDLAE_TRAIN_ROWS && !g.partial && (rows >= 65536 || (rows >= 24576 && g.K <= 256)) && tgemm_rows_eligible(g))
+    return launch_tgemm_rows(g, s);
+  if (KDLAE_TRAIN_COLS && g.partial && partial_cap > 0 && (long long)g.K * g.nz1 * g.nz2 >= 16384 &&
+      tgemm_cols_eligible(g))
+    return launch_tgemm_cols(g, partial_cap, s);
   const long long batch = (long long)g.nz1 * g.nz2;
   // 128-row tiles when the grid still holds >= 2 blocks per CU with them (tall activation GEMMs)
   const int rm = ((long long)((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * batch >= 512) ? 2 : 1;

@@ -134,17 +134,52 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
     }
 }
 
+// blocks of this variant resident on the whole chip (hipOccupancy..., cached)
 template <int TM, int TN>
-hipError_t launch_tt(const ColsArgs& a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((tgemm_cols_kernel<TM, TN>), grid, dim3(kThreads), 0, s, a);
-  return hipGetLastError();
+int slots() {
+  static int n = 0;
+  if (!n) {
+    int b = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&tgemm_cols_kernel<TM, TN>),
+                                                     kThreads, 0) != hipSuccess || b < 1)
+      b = 1;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus < 1)
+      cus = 256;
+    n = b * cus;
+  }
+  return n;
+}
+
+// split count: whole rounds of resident blocks (r03 sweep: a fixed wave target was up to 40% off
+// either way depending on the shape), chunks of at least KDLAE_COLS_MIN pixels, within the
+// partial-buffer capacity
+#ifndef KDLAE_COLS_MIN
+#define KDLAE_COLS_MIN 256
+#endif
+template <int TM, int TN>
+hipError_t launch_tt(TGemm g, ColsArgs a, int gy, long long batch, size_t partial_cap, hipStream_t s) {
+  long long splits = ((long long)slots<TM, TN>() + gy * batch - 1) / (gy * batch);
+  const long long maxs = (g.K + KDLAE_COLS_MIN - 1) / KDLAE_COLS_MIN;
+  if (splits > maxs) splits = maxs;
+  const long long cap = (long long)(partial_cap / ((size_t)g.M * g.N * batch));
+  if (splits > cap) splits = cap;
+  if (splits < 1) return hipErrorInvalidValue;
+  int kchunk = (int)((g.K + splits - 1) / splits);
+  kchunk = (kchunk + 4 * kU - 1) / (4 * kU) * (4 * kU);
+  splits = (g.K + kchunk - 1) / kchunk;
+  a.kchunk = kchunk;
+  a.splits = (int)splits;
+  g.splits = (int)splits;
+  a.g = g;
+  hipLaunchKernelGGL((tgemm_cols_kernel<TM, TN>), dim3((unsigned)splits, (unsigned)gy, (unsigned)batch), dim3(kThreads),
+                     0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_tgemm_reduce(g, s);
 }
 
 }  // namespace
-
-#ifndef KDLAE_COLS_WAVES
-#define KDLAE_COLS_WAVES 4096
-#endif
 
 bool tgemm_cols_eligible(const TGemm& g) {
   if (g.amode != 0 || g.bmode != 0 || g.alpha != 1.f || !g.partial) return false;
@@ -173,28 +208,11 @@ hipError_t launch_tgemm_cols(TGemm g, size_t partial_cap, hipStream_t s) {
   const int wtiles = a.wtm * a.wtn;
   const int gy = (wtiles + 3) / 4;
   const long long batch = (long long)g.nz1 * g.nz2;
-  // pixel chunks: ~KDLAE_COLS_WAVES waves in all, chunks of >= 256 pixels, partials within capacity
-  long long splits = (KDLAE_COLS_WAVES + (long long)wtiles * batch - 1) / ((long long)wtiles * batch);
-  const long long maxs = (g.K + 255) / 256;
-  if (splits > maxs) splits = maxs;
-  const long long cap = (long long)(partial_cap / ((size_t)g.M * g.N * batch));
-  if (splits > cap) splits = cap;
-  if (splits < 1) return hipErrorInvalidValue;
-  int kchunk = (int)((g.K + splits - 1) / splits);
-  kchunk = (kchunk + 4 * kU - 1) / (4 * kU) * (4 * kU);
-  splits = (g.K + kchunk - 1) / kchunk;
-  a.kchunk = kchunk;
-  a.splits = (int)splits;
-  g.splits = (int)splits;
-  a.g = g;
-  const dim3 grid((unsigned)splits, (unsigned)gy, (unsigned)batch);
-  hipError_t e;
 #define TT(m, n) \
-  if (TM == m && TN == n) e = launch_tt<m, n>(a, grid, s); else
-  TT(2, 2) TT(2, 3) TT(2, 4) TT(3, 2) TT(3, 3) TT(3, 4) TT(4, 2) TT(4, 3) e = hipErrorInvalidValue;
+  if (TM == m && TN == n) return launch_tt<m, n>(g, a, gy, batch, partial_cap, s);
+  TT(2, 2) TT(2, 3) TT(2, 4) TT(3, 2) TT(3, 3) TT(3, 4) TT(4, 2) TT(4, 3)
 #undef TT
-  if (e != hipSuccess) return e;
-  return launch_tgemm_reduce(g, s);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace train

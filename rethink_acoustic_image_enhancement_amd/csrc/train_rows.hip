@@ -58,7 +58,7 @@ constexpr unsigned kOOB = 0x80000000u;  // past every descriptor's range: loads 
 #define KDLAE_ROWS_LB2 1
 #endif
 #ifndef KDLAE_ROWS_EPI_ALWAYS
-#define KDLAE_ROWS_EPI_ALWAYS 1
+#define KDLAE_ROWS_EPI_ALWAYS 0
 #endif
 template <int NT, bool HASR, bool VECC>
 #if KDLAE_ROWS_LB2
@@ -260,8 +260,35 @@ __global__ __launch_bounds__(kThreads) void tgemm_rows_kernel(RowsArgs a) {
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static inline bool m4(long long v) { return (v & 3) == 0; }
 
+// resident blocks per CU for this variant at this LDS size (hipOccupancy..., cached per variant and
+// LDS KiB) times the CU count: the grid is one full round of them, each block walking its row
+// tiles (r03 sweep, tools/micro/rows_bench.cpp: a fixed 1024-block grid was 10-45% slower on the
+// shapes whose LDS or VGPRs allow one or two blocks per CU — the second partial round ran alone)
+static int g_cus = 0;
 template <int NT, bool HASR, bool VECC>
-hipError_t launch_nt(const RowsArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+int slots(size_t lds) {
+  static int cache[161] = {};
+  const int kb = (int)((lds + 1023) / 1024);
+  if (kb > 160) return 0;
+  if (!cache[kb]) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&tgemm_rows_kernel<NT, HASR, VECC>),
+                                                     kThreads, lds) != hipSuccess || n < 1)
+      n = 1;
+    cache[kb] = n;
+  }
+  if (!g_cus) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus < 1)
+      cus = 256;
+    g_cus = cus;
+  }
+  return cache[kb] * g_cus;
+}
+
+template <int NT, bool HASR, bool VECC>
+hipError_t launch_nt(RowsArgs a, int nz, size_t lds, hipStream_t s) {
   static size_t attr[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
@@ -271,21 +298,23 @@ hipError_t launch_nt(const RowsArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr[dev] = lds;
   }
+  const long long units = (long long)a.ncb * nz;
+  long long gx = (slots<NT, HASR, VECC>(lds) + units - 1) / units;
+  if (gx > a.row_tiles) gx = a.row_tiles;
+  if (gx < 1) gx = 1;
+  a.gx = (int)gx;
+  const dim3 grid((unsigned)((a.ncb * gx + 7) / 8 * 8), 1, (unsigned)nz);
   hipLaunchKernelGGL((tgemm_rows_kernel<NT, HASR, VECC>), grid, dim3(kThreads), lds, s, a);
   return hipGetLastError();
 }
 
 template <int NT>
-hipError_t launch_nt(const RowsArgs& a, bool hasr, bool vecc, dim3 grid, size_t lds, hipStream_t s) {
-  if (hasr) return vecc ? launch_nt<NT, true, true>(a, grid, lds, s) : launch_nt<NT, true, false>(a, grid, lds, s);
-  return vecc ? launch_nt<NT, false, true>(a, grid, lds, s) : launch_nt<NT, false, false>(a, grid, lds, s);
+hipError_t launch_nt(const RowsArgs& a, bool hasr, bool vecc, int nz, size_t lds, hipStream_t s) {
+  if (hasr) return vecc ? launch_nt<NT, true, true>(a, nz, lds, s) : launch_nt<NT, true, false>(a, nz, lds, s);
+  return vecc ? launch_nt<NT, false, true>(a, nz, lds, s) : launch_nt<NT, false, false>(a, nz, lds, s);
 }
 
 }  // namespace
-
-#ifndef KDLAE_ROWS_BLOCKS
-#define KDLAE_ROWS_BLOCKS 1024
-#endif
 
 bool tgemm_rows_eligible(const TGemm& g) {
   if (g.amode != 0 || g.bmode != 0 || g.alpha != 1.f || g.sak != 1) return false;
@@ -338,15 +367,11 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   const int ncb = (ntiles + NT - 1) / NT;
   const int nz = g.nz1 * g.nz2;
   const size_t lds = (size_t)NT * a.kg * 1024 + (size_t)NT * 128;
-  long long gx = (KDLAE_ROWS_BLOCKS + (long long)ncb * nz - 1) / ((long long)ncb * nz);
-  if (gx > a.row_tiles) gx = a.row_tiles;
-  if (gx < 1) gx = 1;
   a.ncb = ncb;
-  a.gx = (int)gx;
-  const dim3 grid((unsigned)((ncb * gx + 7) / 8 * 8), 1, (unsigned)nz);
+  a.gx = 1;
 #define NTCASE(n)                                                            \
   case n:                                                                    \
-    return launch_nt<n>(a, g.R != nullptr, vecc, grid, lds, s);
+    return launch_nt<n>(a, g.R != nullptr, vecc, nz, lds, s);
   switch (NT) {
     NTCASE(1)
     NTCASE(2)
