@@ -351,7 +351,10 @@ int conv3(Ctx& c, const std::string& n, V x, int Cin, int Cout, int Bn, int H, i
   g.R = R; g.srm = ldr; g.srn = 1;
   g.M = Bn * H * W; g.N = Cout; g.K = 9 * Cin;
   g.Bn = Bn; g.H = H; g.W = W; g.dil = dil;
-  TRY(gemm(c, g, 0, n + " fwd3"));
+  // split-K when the pixel tiles alone leave the chip idle (the 16^2 / 32^2 Upsample convs: 72-144
+  // tiles, K up to 3456); launch_tgemm only splits where that fills it
+  g.partial = c.splitk;
+  TRY(gemm(c, g, kSplitCap, n + " fwd3"));
   return KDLAE_OK;
 }
 
@@ -376,7 +379,8 @@ int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn
     d.R = R; d.srm = ldr; d.srn = 1;
     d.M = (int)P; d.N = Cin; d.K = 9 * Cout;
     d.Bn = Bn; d.H = H; d.W = W; d.dil = dil;
-    TRY(gemm(c, d, 0, n + " dX3"));
+    d.partial = c.splitk;
+    TRY(gemm(c, d, kSplitCap, n + " dX3"));
   }
   return KDLAE_OK;
 }

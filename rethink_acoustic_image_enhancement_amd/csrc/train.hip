@@ -727,9 +727,181 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     else hipLaunchKernelGGL((KERNEL<8>), grid, dim3(256), 0, s, __VA_ARGS__);                       \
   } while (0)
 
+// Lane-group variant (r03) for float4-aligned views: G lanes share a pixel (G = 16 / 32 / 64 for
+// C <= 64 / 128 / 256, and 64 lanes x 2 quads up to 512), each lane NV float4 quads, 64 / G pixels
+// per wave, shuffle sums over log2(G) steps instead of a 6-step full-wave reduction per pixel and
+// statistic.  The one-wave-per-pixel kernels above left 25-40 of 64 lanes idle at C = 48 / 96
+// (1.9 TB/s on the 393216-pixel sr-branch LayerNorm).
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <int G, int NV>
+__global__ __launch_bounds__(256) void ln2_fwd_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ w,
+                                                      const float* __restrict__ b, int C, long long P, int biasfree,
+                                                      float* __restrict__ y, int ldy, float* __restrict__ stats) {
+  constexpr int PPW = 64 / G;  // pixels per wave
+  const int lane = threadIdx.x & 63, gl = lane % G, gp = lane / G;
+  const int Cq = C >> 2;
+  f32x4 wv[NV], bv[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int q = gl + G * j;
+    wv[j] = q < Cq ? *reinterpret_cast<const f32x4*>(w + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bv[j] = (q < Cq && b) ? *reinterpret_cast<const f32x4*>(b + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const long long nwave = (long long)gridDim.x * 4;
+  const float invC = 1.f / C;
+  for (long long p0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * PPW; p0 < P; p0 += nwave * PPW) {
+    const long long p = p0 + gp;
+    const bool live = p < P;
+    f32x4 v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int q = gl + G * j;
+      v[j] = (live && q < Cq) ? *reinterpret_cast<const f32x4*>(x + p * ldx + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    const float mu = group_sum<G>(s) * invC;
+    float qq = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      if (gl + G * j < Cq)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qq += (v[j][e] - mu) * (v[j][e] - mu);
+    const float var = group_sum<G>(qq) * invC;
+    const float sd = sqrtf(var + 1e-5f);
+    if (!live) continue;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int q = gl + G * j;
+      if (q >= Cq) continue;
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = biasfree ? v[j][e] / sd * wv[j][e] : (v[j][e] - mu) / sd * wv[j][e] + bv[j][e];
+      *reinterpret_cast<f32x4*>(y + p * ldy + 4 * q) = o;
+    }
+    if (gl == 0) {
+      stats[2 * p] = mu;
+      stats[2 * p + 1] = 1.f / sd;
+    }
+  }
+}
+
+template <int G, int NV>
+__global__ __launch_bounds__(256) void ln2_bwd_kernel(const float* __restrict__ dy, int ldd, const float* __restrict__ x,
+                                                      int ldx, const float* __restrict__ w,
+                                                      const float* __restrict__ stats, int C, long long P, int biasfree,
+                                                      const float* R, int ldr, float* dx, int lddx,
+                                                      float* __restrict__ part) {
+  constexpr int PPW = 64 / G;
+  __shared__ f32x4 red[4][2][G * NV];
+  const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6, gl = lane % G, gp = lane / G;
+  const int Cq = C >> 2;
+  f32x4 wr[NV], aw[NV], ab[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int q = gl + G * j;
+    wr[j] = q < Cq ? *reinterpret_cast<const f32x4*>(w + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    aw[j] = ab[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const long long nwave = (long long)gridDim.x * 4;
+  const float invC = 1.f / C;
+  for (long long p0 = ((long long)blockIdx.x * 4 + wv_) * PPW; p0 < P; p0 += nwave * PPW) {
+    const long long p = p0 + gp;
+    const bool live = p < P;
+    const float mu = live ? stats[2 * p] : 0.f, r = live ? stats[2 * p + 1] : 0.f;
+    f32x4 dv[NV], xv[NV], rv[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int q = gl + G * j;
+      const bool ok = live && q < Cq;
+      dv[j] = ok ? *reinterpret_cast<const f32x4*>(dy + p * ldd + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+      xv[j] = ok ? *reinterpret_cast<const f32x4*>(x + p * ldx + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+      rv[j] = (ok && R) ? *reinterpret_cast<const f32x4*>(R + p * ldr + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float s1 = 0.f, s2 = 0.f;
+    f32x4 gv[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = biasfree ? xv[j][e] * r : (xv[j][e] - mu) * r;
+        aw[j][e] += dv[j][e] * xh;
+        ab[j][e] += dv[j][e];
+        gv[j][e] = dv[j][e] * wr[j][e];
+        s1 += gv[j][e] * (biasfree ? xv[j][e] : xh);
+        s2 += gv[j][e];
+      }
+    s1 = group_sum<G>(s1) * invC;
+    s2 = group_sum<G>(s2) * invC;
+    if (!live) continue;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int q = gl + G * j;
+      if (q >= Cq) continue;
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = biasfree ? r * gv[j][e] - r * r * r * (xv[j][e] - mu) * s1
+                                 : r * (gv[j][e] - s2 - (xv[j][e] - mu) * r * s1);
+        o[e] = d + rv[j][e];
+      }
+      *reinterpret_cast<f32x4*>(dx + p * lddx + 4 * q) = o;
+    }
+  }
+  // per-channel partials: the PPW pixel groups of a wave (lanes gl, gl + G, ...) in fixed order,
+  // then the 4 waves in fixed order
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = G; o < 64; o <<= 1) {
+        aw[j][e] += __shfl_xor(aw[j][e], o);
+        ab[j][e] += __shfl_xor(ab[j][e], o);
+      }
+  if (gp == 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      red[wv_][0][gl + G * j] = aw[j];
+      red[wv_][1][gl + G * j] = ab[j];
+    }
+  __syncthreads();
+  const int ncol = biasfree ? C : 2 * C;
+  for (int c = threadIdx.x; c < ncol; c += blockDim.x) {
+    const int which = c < C ? 0 : 1, cc = c < C ? c : c - C;
+    const int q = cc >> 2, e = cc & 3;
+    part[(long long)blockIdx.x * ncol + c] =
+        ((red[0][which][q][e] + red[1][which][q][e]) + red[2][which][q][e]) + red[3][which][q][e];
+  }
+}
+
+static inline bool ln2_ok(const void* a, int lda, const void* b, int ldb, int C) {
+  return C % 4 == 0 && C <= 512 && ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0 && lda % 4 == 0 && ldb % 4 == 0;
+}
+
+#define LN2_DISPATCH(KERNEL, grid, ...)                                                              \
+  do {                                                                                               \
+    if (C <= 64) hipLaunchKernelGGL((KERNEL<16, 1>), grid, dim3(256), 0, s, __VA_ARGS__);              \
+    else if (C <= 128) hipLaunchKernelGGL((KERNEL<32, 1>), grid, dim3(256), 0, s, __VA_ARGS__);        \
+    else if (C <= 256) hipLaunchKernelGGL((KERNEL<64, 1>), grid, dim3(256), 0, s, __VA_ARGS__);        \
+    else hipLaunchKernelGGL((KERNEL<64, 2>), grid, dim3(256), 0, s, __VA_ARGS__);                      \
+  } while (0)
+
 hipError_t launch_ln_fwd(const float* x, int ldx, const float* w, const float* b, int C, long long P, int biasfree,
                          float* y, int ldy, float* stats, hipStream_t s) {
   if (C > 512) return hipErrorInvalidValue;
+  if (ln2_ok(x, ldx, y, ldy, C) && ((uintptr_t)w & 15) == 0 && (!b || ((uintptr_t)b & 15) == 0)) {
+    const int ppw = C <= 64 ? 4 : C <= 128 ? 2 : 1;
+    LN2_DISPATCH(ln2_fwd_kernel, dim3(grid_for(P, 4 * ppw * 2, 16384)), x, ldx, w, b, C, P, biasfree, y, ldy, stats);
+    return hipGetLastError();
+  }
   LN_DISPATCH(ln_fwd_kernel, dim3(grid_for(P, 4 * LN_NP, 16384)), x, ldx, w, b, C, P, biasfree, y, ldy, stats);
   return hipGetLastError();
 }
@@ -738,6 +910,10 @@ hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, cons
                          long long P, int biasfree, const float* R, int ldr, float* dx, int lddx, float* part, int nblk,
                          hipStream_t s) {
   if (C > 512) return hipErrorInvalidValue;
+  if (ln2_ok(dy, ldd, x, ldx, C) && ln2_ok(dx, lddx, w, 4, C) && (!R || ln2_ok(R, ldr, R, ldr, C))) {
+    LN2_DISPATCH(ln2_bwd_kernel, dim3(nblk), dy, ldd, x, ldx, w, stats, C, P, biasfree, R, ldr, dx, lddx, part);
+    return hipGetLastError();
+  }
   LN_DISPATCH(ln_bwd_kernel, dim3(nblk), dy, ldd, x, ldx, w, stats, C, P, biasfree, R, ldr, dx, lddx, part);
   return hipGetLastError();
 }
