@@ -442,10 +442,10 @@ int block_fwd(Ctx& c, BlockRec& r) {
   r.y = c.alloc(P * L2);
   TRY(conv1(c, p + ".ffn.project_in", {r.xn2, C}, C, 2 * hid, P, {r.y, L2}, nullptr, 0, {nullptr, 0}, true));
   r.yd = c.alloc(P * L2);
-  LAUNCH(tr::launch_dw_fwd(r.y, L2, c.W(p + ".ffn.dwconv.weight"), c.W(p + ".ffn.dwconv.bias"), 0, 2 * hid, Bn,
-                           r.H, r.W, r.yd, L2, c.s));
   r.g = c.alloc(P * L1);
-  LAUNCH(tr::launch_gate_fwd(r.yd, L2, hid, P, r.g, L1, c.s));
+  // dwconv + GELU gate in one pass (train_dwg.hip): yd for the backward, g for project_out
+  LAUNCH(tr::launch_dwgate_fwd(r.y, L2, c.W(p + ".ffn.dwconv.weight"), c.W(p + ".ffn.dwconv.bias"), hid, Bn, r.H,
+                               r.W, r.yd, L2, r.g, L1, c.s));
   r.out = c.alloc(P * C);
   if (hid % 4) {
     // row stride hid is not a multiple of 4 floats: a zero-padded [C][ld4(hid)] copy lets the forward
@@ -458,10 +458,20 @@ int block_fwd(Ctx& c, BlockRec& r) {
   return KDLAE_OK;
 }
 
+// sum the nb partial rows [9 C weights | C bias] of a depthwise conv's gradient into its keys
+int dw_reduce(Ctx& c, int nb, int C, const std::string& n);
+
 int dw_wgrad(Ctx& c, const float* dy, const float* x, int ld, int C, int Bn, int H, int W, const std::string& n) {
   const long long P = (long long)Bn * H * W;
   const int nb = tr::dw_wgrad_blocks(C, Bn, H, W, nblk_for(P, 10LL * C, 256));
   LAUNCH(tr::launch_dw_wgrad(dy, ld, x, ld, C, Bn, H, W, c.red, nb, c.s));
+  return dw_reduce(c, nb, C, n);
+}
+
+// fused depthwise backward (train_dwg.hip) when its partial rows fit the reduction buffer
+bool dwg_fits(int C, int Bn, int H, int W) { return (size_t)tr::dwg_blocks(Bn, H, W) * 10 * C <= kRedCap; }
+
+int dw_reduce(Ctx& c, int nb, int C, const std::string& n) {
   // partial columns: [9 C weights | C bias]; one reduce when the bias key directly follows the
   // weight key in the flat buffer (keys are 16-byte aligned, so only when 9 C % 4 == 0)
   float* gw = c.G(n + ".weight");
@@ -504,11 +514,18 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   const int L2 = ld4(2 * hid), L1 = ld4(hid);
   float* dg = c.alloc(P * L1);
   TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, L1}, {d, C}, hid, C, P, {dg, L1}, nullptr, 0, {r.wpo, L1}, true));
-  float* dyd = c.alloc(P * L2);
-  LAUNCH(tr::launch_gate_bwd(dg, L1, r.yd, L2, hid, P, dyd, L2, c.s));
   float* dy = c.alloc(P * L2);
-  LAUNCH(tr::launch_dw_fwd(dyd, L2, c.W(p + ".ffn.dwconv.weight"), nullptr, 1, 2 * hid, Bn, r.H, r.W, dy, L2, c.s));
-  TRY(dw_wgrad(c, dyd, r.y, L2, 2 * hid, Bn, r.H, r.W, p + ".ffn.dwconv"));
+  if (dwg_fits(2 * hid, Bn, r.H, r.W)) {
+    // gate backward + transposed dwconv + dwconv weight gradient in one pass (train_dwg.hip)
+    LAUNCH(tr::launch_dwgate_bwd(dg, L1, r.yd, L2, r.y, L2, c.W(p + ".ffn.dwconv.weight"), hid, Bn, r.H, r.W, dy, L2,
+                                 c.red, c.s));
+    TRY(dw_reduce(c, tr::dwg_blocks(Bn, r.H, r.W), 2 * hid, p + ".ffn.dwconv"));
+  } else {
+    float* dyd = c.alloc(P * L2);
+    LAUNCH(tr::launch_gate_bwd(dg, L1, r.yd, L2, hid, P, dyd, L2, c.s));
+    LAUNCH(tr::launch_dw_fwd(dyd, L2, c.W(p + ".ffn.dwconv.weight"), nullptr, 1, 2 * hid, Bn, r.H, r.W, dy, L2, c.s));
+    TRY(dw_wgrad(c, dyd, r.y, L2, 2 * hid, Bn, r.H, r.W, p + ".ffn.dwconv"));
+  }
   float* dxn2 = c.alloc(P * C);
   TRY(conv1_bwd(c, p + ".ffn.project_in", {r.xn2, C}, {dy, L2}, C, 2 * hid, P, {dxn2, C}));
   float* dx1 = c.alloc(P * C);
@@ -560,8 +577,15 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
     TRY(gemm(c, g, 0, "dk"));
   }
   float* dqkv = c.alloc(P * C3);
-  LAUNCH(tr::launch_dw_fwd(dqkvd, C3, c.W(p + ".attn.qkv_dwconv.weight"), nullptr, 1, C3, Bn, r.H, r.W, dqkv, C3, c.s));
-  TRY(dw_wgrad(c, dqkvd, r.qkv, C3, C3, Bn, r.H, r.W, p + ".attn.qkv_dwconv"));
+  if (dwg_fits(C3, Bn, r.H, r.W)) {
+    LAUNCH(tr::launch_dw_bwd(dqkvd, C3, r.qkv, C3, c.W(p + ".attn.qkv_dwconv.weight"), C3, Bn, r.H, r.W, dqkv, C3,
+                             c.red, c.s));
+    TRY(dw_reduce(c, tr::dwg_blocks(Bn, r.H, r.W), C3, p + ".attn.qkv_dwconv"));
+  } else {
+    LAUNCH(tr::launch_dw_fwd(dqkvd, C3, c.W(p + ".attn.qkv_dwconv.weight"), nullptr, 1, C3, Bn, r.H, r.W, dqkv, C3,
+                             c.s));
+    TRY(dw_wgrad(c, dqkvd, r.qkv, C3, C3, Bn, r.H, r.W, p + ".attn.qkv_dwconv"));
+  }
   float* dxn1 = c.alloc(P * C);
   TRY(conv1_bwd(c, p + ".attn.qkv", {r.xn1, C}, {dqkv, C3}, C, C3, P, {dxn1, C}));
   TRY(ln_bwd(c, dxn1, r.x, r.st1, C, P, p + ".norm1.body", dx1, d));

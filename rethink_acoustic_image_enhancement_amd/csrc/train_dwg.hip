@@ -1,0 +1,248 @@
+// Fused depthwise-3x3 kernels of the training step (gfx950): the GDFN middle
+// (KDLAE_model.py:101-105: x1, x2 = dwconv(project_in(x)).chunk(2); gelu(x1) * x2) and the MDTA qkv
+// dwconv (:127), forward and backward, each in one pass over HBM.
+//
+//   dwgate_fwd : yd = dw(y) (+ bias) for both halves, g = gelu_erf(yd1) * yd2 — y read once, yd
+//                (the backward's gate input) and g written; the separate dwconv + gate kernels read
+//                yd a second time.
+//   dw_bwd     : from dyd (GATE: dyd = gate_bwd(dg, yd) computed on the fly), dy = dw^T(dyd) (the
+//                flipped-tap conv) and the weight / bias gradient partials sum dyd * y_in(shifted),
+//                sum dyd — dyd is never written; the unfused chain wrote it and read it twice.
+//
+// Layout: NHWC views, channels contiguous; the GDFN's y / yd hold x1 at [0, hid), x2 at
+// [hid, 2 hid) (hid odd for the released widths, so the halves are not float4-aligned: one channel
+// per lane, 64 consecutive channels = 256 B per load).  A block is 4 waves = 4 column groups of 4
+// columns (16 columns) x TY rows of one image x 64 channels; a thread walks its 4 columns down the
+// rows with a 3-row x 6-column register window per tensor (each input row is loaded once per walk;
+// the 2 halo columns are the neighbouring wave's, L1 hits).  Accumulation order per output: bias,
+// then taps row-major (as dw_tile_fwd_kernel).  Weight gradient partials: the block's 4 waves in
+// fixed order -> part[spatial block][c * 9 + t] and part[..][9 C + c] (C = all channels), summed
+// over spatial blocks in fixed order by part_reduce: deterministic.
+#include <math.h>
+
+#include "train_kernels.h"
+
+namespace kdlae {
+namespace train {
+
+namespace {
+
+constexpr int kU = 4;         // columns per thread
+constexpr int kTX = 4 * kU;   // columns per block
+constexpr int kTY = 16;       // rows per block
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+struct Geo {
+  int b, x0, y0, y1, c;
+  long long img0;
+  bool live;
+};
+
+__device__ __forceinline__ Geo geo(int C, int H, int W, int tiles_x) {
+  Geo o;
+  const int t = blockIdx.x;
+  o.b = blockIdx.z;
+  o.x0 = (t % tiles_x) * kTX + (threadIdx.x >> 6) * kU;
+  o.y0 = (t / tiles_x) * kTY;
+  o.y1 = min(H, o.y0 + kTY);
+  o.c = blockIdx.y * 64 + (threadIdx.x & 63);
+  o.live = o.c < C;
+  o.img0 = (long long)o.b * H * W;
+  return o;
+}
+
+// row yy, columns x0 - 1 .. x0 + kU of channel off (zero outside the image / past the channels)
+__device__ __forceinline__ void load_row(const float* __restrict__ p, int ld, const Geo& o, int H, int W, int yy,
+                                         int off, float (&r)[kU + 2]) {
+  const bool oky = o.live && yy >= 0 && yy < H;
+#pragma unroll
+  for (int j = 0; j < kU + 2; ++j) {
+    const int xx = o.x0 - 1 + j;
+    r[j] = (oky && xx >= 0 && xx < W) ? p[(o.img0 + (long long)yy * W + xx) * ld + off] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void dwgate_fwd_kernel(const float* __restrict__ y, int ldi,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         int hid, int H, int W, int tiles_x, float* __restrict__ yd,
+                                                         int ldyd, float* __restrict__ g, int ldg) {
+  const Geo o = geo(hid, H, W, tiles_x);
+  const int c = o.c;
+  float w1[9], w2[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    w1[t] = o.live ? w[c * 9 + t] : 0.f;
+    w2[t] = o.live ? w[(hid + c) * 9 + t] : 0.f;
+  }
+  const float b1 = (o.live && bias) ? bias[c] : 0.f, b2 = (o.live && bias) ? bias[hid + c] : 0.f;
+  float a[3][kU + 2], v[3][kU + 2];  // rows y-1, y, y+1 of halves 1 and 2
+  load_row(y, ldi, o, H, W, o.y0 - 1, c, a[0]);
+  load_row(y, ldi, o, H, W, o.y0, c, a[1]);
+  load_row(y, ldi, o, H, W, o.y0 - 1, hid + c, v[0]);
+  load_row(y, ldi, o, H, W, o.y0, hid + c, v[1]);
+  for (int yy = o.y0; yy < o.y1; ++yy) {
+    load_row(y, ldi, o, H, W, yy + 1, c, a[2]);
+    load_row(y, ldi, o, H, W, yy + 1, hid + c, v[2]);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      float s1 = b1, s2 = b2;
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) {
+          s1 += w1[ty * 3 + tx] * a[ty][u + tx];
+          s2 += w2[ty * 3 + tx] * v[ty][u + tx];
+        }
+      const int xx = o.x0 + u;
+      if (o.live && xx < W) {
+        const long long p = o.img0 + (long long)yy * W + xx;
+        yd[p * ldyd + c] = s1;
+        yd[p * ldyd + hid + c] = s2;
+        g[p * ldg + c] = gelu_erf(s1) * s2;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kU + 2; ++j) {
+      a[0][j] = a[1][j];
+      a[1][j] = a[2][j];
+      v[0][j] = v[1][j];
+      v[1][j] = v[2][j];
+    }
+  }
+}
+
+// GATE: two halves, dyd from (dg, yd); else one tensor of C = `hid` channels, dyd read as given.
+template <bool GATE>
+__global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ dg, int ldg,
+                                                     const float* __restrict__ yd, int ldyd,
+                                                     const float* __restrict__ yin, int ldi,
+                                                     const float* __restrict__ w, int hid, int H, int W, int tiles_x,
+                                                     float* __restrict__ dy, int lddy, float* __restrict__ part) {
+  constexpr int NH = GATE ? 2 : 1;
+  __shared__ float red[4][64][10 * NH];
+  const Geo o = geo(hid, H, W, tiles_x);
+  const int c = o.c;
+  float wf[NH][9];  // flipped taps (the transposed conv)
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wf[h][t] = o.live ? w[(h * hid + c) * 9 + 8 - t] : 0.f;
+  float acc[NH][10];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int t = 0; t < 10; ++t) acc[h][t] = 0.f;
+  float d[NH][3][kU + 2], x[NH][3][kU + 2];
+  // dyd of row yy for both halves: gate backward of (dg, yd1, yd2), or the given gradient
+  auto row_d = [&](int yy, float (&d0)[kU + 2], float (&d1)[kU + 2]) {
+    if constexpr (GATE) {
+      float gg[kU + 2], y1[kU + 2], y2[kU + 2];
+      load_row(dg, ldg, o, H, W, yy, c, gg);
+      load_row(yd, ldyd, o, H, W, yy, c, y1);
+      load_row(yd, ldyd, o, H, W, yy, hid + c, y2);
+#pragma unroll
+      for (int j = 0; j < kU + 2; ++j) {
+        const float cdf = 0.5f * (1.f + erff(y1[j] * 0.70710678118654752f));
+        const float pdf = 0.39894228040143268f * expf(-0.5f * y1[j] * y1[j]);
+        d0[j] = gg[j] * y2[j] * (cdf + y1[j] * pdf);
+        d1[j] = gg[j] * y1[j] * cdf;
+      }
+    } else {
+      load_row(yd, ldyd, o, H, W, yy, c, d0);
+      (void)d1;
+    }
+  };
+  row_d(o.y0 - 1, d[0][0], d[NH - 1][0]);
+  row_d(o.y0, d[0][1], d[NH - 1][1]);
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    load_row(yin, ldi, o, H, W, o.y0 - 1, h * hid + c, x[h][0]);
+    load_row(yin, ldi, o, H, W, o.y0, h * hid + c, x[h][1]);
+  }
+  for (int yy = o.y0; yy < o.y1; ++yy) {
+    row_d(yy + 1, d[0][2], d[NH - 1][2]);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) load_row(yin, ldi, o, H, W, yy + 1, h * hid + c, x[h][2]);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int xx = o.x0 + u;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        float s = 0.f;
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) s += wf[h][ty * 3 + tx] * d[h][ty][u + tx];
+        if (o.live && xx < W) dy[(o.img0 + (long long)yy * W + xx) * lddy + h * hid + c] = s;
+        // weight / bias gradient: centre dyd times the input at each tap (zero past the image)
+        const float dc = d[h][1][u + 1];
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) acc[h][ty * 3 + tx] += dc * x[h][ty][u + tx];
+        acc[h][9] += dc;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int j = 0; j < kU + 2; ++j) {
+        d[h][0][j] = d[h][1][j];
+        d[h][1][j] = d[h][2][j];
+        x[h][0][j] = x[h][1][j];
+        x[h][1][j] = x[h][2][j];
+      }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int t = 0; t < 10; ++t) red[wv][lane][h * 10 + t] = acc[h][t];
+  __syncthreads();
+  if (wv != 0 || !o.live) return;
+  const int Ctot = NH * hid;
+  float* pr = part + ((long long)o.b * gridDim.x + blockIdx.x) * 10 * Ctot;
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      const float s = ((red[0][lane][h * 10 + t] + red[1][lane][h * 10 + t]) + red[2][lane][h * 10 + t]) +
+                      red[3][lane][h * 10 + t];
+      const int ch = h * hid + c;
+      if (t < 9) pr[ch * 9 + t] = s;
+      else pr[9 * Ctot + ch] = s;
+    }
+}
+
+}  // namespace
+
+int dwg_blocks(int Bn, int H, int W) { return Bn * ((W + kTX - 1) / kTX) * ((H + kTY - 1) / kTY); }
+
+hipError_t launch_dwgate_fwd(const float* y, int ldi, const float* w, const float* b, int hid, int Bn, int H, int W,
+                             float* yd, int ldyd, float* g, int ldg, hipStream_t s) {
+  const int tx = (W + kTX - 1) / kTX, ty = (H + kTY - 1) / kTY;
+  hipLaunchKernelGGL(dwgate_fwd_kernel, dim3(tx * ty, (hid + 63) / 64, Bn), dim3(256), 0, s, y, ldi, w, b, hid, H, W,
+                     tx, yd, ldyd, g, ldg);
+  return hipGetLastError();
+}
+
+hipError_t launch_dwgate_bwd(const float* dg, int ldg, const float* yd, int ldyd, const float* yin, int ldi,
+                             const float* w, int hid, int Bn, int H, int W, float* dy, int lddy, float* part,
+                             hipStream_t s) {
+  const int tx = (W + kTX - 1) / kTX, ty = (H + kTY - 1) / kTY;
+  hipLaunchKernelGGL(dw_bwd_kernel<true>, dim3(tx * ty, (hid + 63) / 64, Bn), dim3(256), 0, s, dg, ldg, yd, ldyd, yin,
+                     ldi, w, hid, H, W, tx, dy, lddy, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_dw_bwd(const float* dyd, int ldd, const float* yin, int ldi, const float* w, int C, int Bn, int H,
+                         int W, float* dy, int lddy, float* part, hipStream_t s) {
+  const int tx = (W + kTX - 1) / kTX, ty = (H + kTY - 1) / kTY;
+  hipLaunchKernelGGL(dw_bwd_kernel<false>, dim3(tx * ty, (C + 63) / 64, Bn), dim3(256), 0, s, nullptr, 0, dyd, ldd,
+                     yin, ldi, w, C, H, W, tx, dy, lddy, part);
+  return hipGetLastError();
+}
+
+}  // namespace train
+}  // namespace kdlae

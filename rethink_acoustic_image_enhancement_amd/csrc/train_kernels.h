@@ -74,6 +74,19 @@ int dw_wgrad_blocks(int C, int Bn, int H, int W, int max_blocks);
 hipError_t launch_dw_wgrad(const float* dy, int ldd, const float* in, int ldi, int C, int Bn, int H, int W,
                            float* part, int nblk, hipStream_t s);
 
+// Fused depthwise kernels (train_dwg.hip).  GDFN forward: yd = dw(y) (+b) over both halves
+// (x1 at [0, hid), x2 at [hid, 2 hid)) and g = gelu_erf(yd1) * yd2.  Backward: dy = dw^T(dyd) and the
+// weight / bias gradient partials part[dwg_blocks][10 C] (C = 2 hid, layout of launch_dw_wgrad),
+// with dyd = gate_bwd(dg, yd) computed on the fly (dwgate) or given (dw_bwd, C channels).
+int dwg_blocks(int Bn, int H, int W);
+hipError_t launch_dwgate_fwd(const float* y, int ldi, const float* w, const float* b, int hid, int Bn, int H, int W,
+                             float* yd, int ldyd, float* g, int ldg, hipStream_t s);
+hipError_t launch_dwgate_bwd(const float* dg, int ldg, const float* yd, int ldyd, const float* yin, int ldi,
+                             const float* w, int hid, int Bn, int H, int W, float* dy, int lddy, float* part,
+                             hipStream_t s);
+hipError_t launch_dw_bwd(const float* dyd, int ldd, const float* yin, int ldi, const float* w, int C, int Bn, int H,
+                         int W, float* dy, int lddy, float* part, hipStream_t s);
+
 // column reductions: out[seg][c] = sum over rows of segment seg of f(x[r][c]); f = x or x^2.
 // Two passes (partials then a fixed-order reduce), deterministic.
 hipError_t launch_colsum(const float* x, int ldx, int ncols, long long rows_per_seg, int nseg, int square,

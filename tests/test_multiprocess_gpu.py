@@ -76,7 +76,9 @@ def _worker(rank, world, port, q):
         tr2.optimize_parameters(lq, {k: v[s:e].cuda() for k, v in gt.items()})
         res["theta_bucketed"] = tr2.theta.detach().cpu()
         res["nbuckets"] = len(tr2.buckets)
-        q.put((rank, res))
+        # numpy copies travel by value: a torch CPU tensor is passed as a file descriptor the parent
+        # fetches from this process's resource sharer, which is gone once the rank has exited
+        q.put((rank, {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in res.items()}))
         dist.destroy_process_group()
     except Exception as ex:  # surface the failure in the parent instead of hanging on the queue
         q.put((rank, repr(ex)))
@@ -104,6 +106,8 @@ def test_two_processes_share_the_gpu():
     res = dict(q.get(timeout=240) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
+    res = {r: ({k: (torch.from_numpy(v) if isinstance(v, np.ndarray) else v) for k, v in d.items()}
+               if isinstance(d, dict) else d) for r, d in res.items()}
     for r in range(2):
         assert isinstance(res[r], dict), res[r]
         assert torch.equal(res[r]["hq"], ref["hq"]) and torch.equal(res[r]["sr"], ref["sr"])
