@@ -29,7 +29,14 @@ namespace {
 
 constexpr int kU = 4;         // columns per thread
 constexpr int kTX = 4 * kU;   // columns per block
-constexpr int kTY = 16;       // rows per block
+// rows per block: 16, or 8 / 4 on the small levels so the grid still has >= 256 spatial blocks (the
+// 16^2 latent: 6 blocks per channel group at 16 rows, 0.7-1.0 TB/s)
+int rows_per_block(int Bn, int H, int W) {
+  const int tx = (W + kTX - 1) / kTX;
+  int ty = 16;
+  while (ty > 4 && (long long)Bn * tx * ((H + ty - 1) / ty) < 256) ty >>= 1;
+  return ty;
+}
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
@@ -39,13 +46,13 @@ struct Geo {
   bool live;
 };
 
-__device__ __forceinline__ Geo geo(int C, int H, int W, int tiles_x) {
+__device__ __forceinline__ Geo geo(int C, int H, int W, int tiles_x, int ty) {
   Geo o;
   const int t = blockIdx.x;
   o.b = blockIdx.z;
   o.x0 = (t % tiles_x) * kTX + (threadIdx.x >> 6) * kU;
-  o.y0 = (t / tiles_x) * kTY;
-  o.y1 = min(H, o.y0 + kTY);
+  o.y0 = (t / tiles_x) * ty;
+  o.y1 = min(H, o.y0 + ty);
   o.c = blockIdx.y * 64 + (threadIdx.x & 63);
   o.live = o.c < C;
   o.img0 = (long long)o.b * H * W;
@@ -65,9 +72,10 @@ __device__ __forceinline__ void load_row(const float* __restrict__ p, int ld, co
 
 __global__ __launch_bounds__(256) void dwgate_fwd_kernel(const float* __restrict__ y, int ldi,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
-                                                         int hid, int H, int W, int tiles_x, float* __restrict__ yd,
-                                                         int ldyd, float* __restrict__ g, int ldg) {
-  const Geo o = geo(hid, H, W, tiles_x);
+                                                         int hid, int H, int W, int tiles_x, int ty,
+                                                         float* __restrict__ yd, int ldyd, float* __restrict__ g,
+                                                         int ldg) {
+  const Geo o = geo(hid, H, W, tiles_x, ty);
   const int c = o.c;
   float w1[9], w2[9];
 #pragma unroll
@@ -118,10 +126,11 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
                                                      const float* __restrict__ yd, int ldyd,
                                                      const float* __restrict__ yin, int ldi,
                                                      const float* __restrict__ w, int hid, int H, int W, int tiles_x,
-                                                     float* __restrict__ dy, int lddy, float* __restrict__ part) {
+                                                     int ty, float* __restrict__ dy, int lddy,
+                                                     float* __restrict__ part) {
   constexpr int NH = GATE ? 2 : 1;
   __shared__ float red[4][64][10 * NH];
-  const Geo o = geo(hid, H, W, tiles_x);
+  const Geo o = geo(hid, H, W, tiles_x, ty);
   const int c = o.c;
   float wf[NH][9];  // flipped taps (the transposed conv)
 #pragma unroll
@@ -217,30 +226,33 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
 
 }  // namespace
 
-int dwg_blocks(int Bn, int H, int W) { return Bn * ((W + kTX - 1) / kTX) * ((H + kTY - 1) / kTY); }
+int dwg_blocks(int Bn, int H, int W) {
+  const int ty = rows_per_block(Bn, H, W);
+  return Bn * ((W + kTX - 1) / kTX) * ((H + ty - 1) / ty);
+}
 
 hipError_t launch_dwgate_fwd(const float* y, int ldi, const float* w, const float* b, int hid, int Bn, int H, int W,
                              float* yd, int ldyd, float* g, int ldg, hipStream_t s) {
-  const int tx = (W + kTX - 1) / kTX, ty = (H + kTY - 1) / kTY;
-  hipLaunchKernelGGL(dwgate_fwd_kernel, dim3(tx * ty, (hid + 63) / 64, Bn), dim3(256), 0, s, y, ldi, w, b, hid, H, W,
-                     tx, yd, ldyd, g, ldg);
+  const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
+  hipLaunchKernelGGL(dwgate_fwd_kernel, dim3(tx * nty, (hid + 63) / 64, Bn), dim3(256), 0, s, y, ldi, w, b, hid, H, W,
+                     tx, ty, yd, ldyd, g, ldg);
   return hipGetLastError();
 }
 
 hipError_t launch_dwgate_bwd(const float* dg, int ldg, const float* yd, int ldyd, const float* yin, int ldi,
                              const float* w, int hid, int Bn, int H, int W, float* dy, int lddy, float* part,
                              hipStream_t s) {
-  const int tx = (W + kTX - 1) / kTX, ty = (H + kTY - 1) / kTY;
-  hipLaunchKernelGGL(dw_bwd_kernel<true>, dim3(tx * ty, (hid + 63) / 64, Bn), dim3(256), 0, s, dg, ldg, yd, ldyd, yin,
-                     ldi, w, hid, H, W, tx, dy, lddy, part);
+  const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
+  hipLaunchKernelGGL(dw_bwd_kernel<true>, dim3(tx * nty, (hid + 63) / 64, Bn), dim3(256), 0, s, dg, ldg, yd, ldyd,
+                     yin, ldi, w, hid, H, W, tx, ty, dy, lddy, part);
   return hipGetLastError();
 }
 
 hipError_t launch_dw_bwd(const float* dyd, int ldd, const float* yin, int ldi, const float* w, int C, int Bn, int H,
                          int W, float* dy, int lddy, float* part, hipStream_t s) {
-  const int tx = (W + kTX - 1) / kTX, ty = (H + kTY - 1) / kTY;
-  hipLaunchKernelGGL(dw_bwd_kernel<false>, dim3(tx * ty, (C + 63) / 64, Bn), dim3(256), 0, s, nullptr, 0, dyd, ldd,
-                     yin, ldi, w, C, H, W, tx, dy, lddy, part);
+  const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
+  hipLaunchKernelGGL(dw_bwd_kernel<false>, dim3(tx * nty, (C + 63) / 64, Bn), dim3(256), 0, s, nullptr, 0, dyd, ldd,
+                     yin, ldi, w, C, H, W, tx, ty, dy, lddy, part);
   return hipGetLastError();
 }
 
