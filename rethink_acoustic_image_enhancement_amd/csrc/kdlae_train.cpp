@@ -192,6 +192,10 @@ struct Ctx {
   // launch trace (diagnostics only: KDLAE_DEBUG=train_trace); tag = the layer being sequenced
   std::vector<kdlae_tt_handle::TraceRec>* trace = nullptr;
   std::string tag;
+  // queued partial reductions of the backward (one batched launch at the next flush: a mark, the
+  // end of a TransformerBlock, or a full queue); red_off = floats of `red` their partials occupy
+  std::vector<tr::RedDesc> pend;
+  size_t red_off = 0;
 
   float* alloc(size_t n) {
     off = (off + 255) / 256 * 256;
@@ -216,10 +220,25 @@ struct Ctx {
   }
 };
 
+int flush_reduce(Ctx& c);
+
+// a region of the reduction buffer for a queued reduction's partials (flushes when full)
+float* red_take(Ctx& c, size_t n) {
+  n = (n + 63) / 64 * 64;
+  if (c.red_off + n > kRedCap) {
+    if (flush_reduce(c) != KDLAE_OK) return nullptr;
+  }
+  float* p = c.red + c.red_off;
+  c.red_off += n;
+  return p;
+}
+
 // A point in the backward after which some parameters' gradients are final (one TransformerBlock,
 // one head conv, ...).  kdlae_tt_backward_marked records an event at the marks that close a suffix
 // of the flat buffer, so the caller can all-reduce that suffix while the backward continues.
 int mark(Ctx& c) {
+  int rc = flush_reduce(c);  // the gradients this mark declares final
+  if (rc) return rc;
   if (c.record_marks && !c.dry && c.cur_mark < (int)c.h->mark_slot.size()) {
     const int j = c.h->mark_slot[c.cur_mark];
     if (j >= 0) {
@@ -264,6 +283,27 @@ void trace_end(Ctx& c, hipEvent_t a, const char* what) {
   } while (0)
 
 inline int ld4(int n) { return (n + 3) / 4 * 4; }
+
+int flush_reduce(Ctx& c) {
+  if (!c.pend.empty()) LAUNCH(tr::launch_part_reduce_multi(c.pend.data(), (int)c.pend.size(), c.s));
+  c.pend.clear();
+  c.red_off = 0;
+  return KDLAE_OK;
+}
+
+// queue out[0, ncols) = sum over nblk rows (stride pstride) of part; flushed in one batched launch
+int queue_reduce(Ctx& c, const float* part, int nblk, int ncols, int pstride, float* out) {
+  if (!out || ncols <= 0) return KDLAE_OK;
+  tr::RedDesc d;
+  d.part = part;
+  d.out = out;
+  d.nblk = nblk;
+  d.ncols = ncols;
+  d.pstride = pstride;
+  c.pend.push_back(d);
+  if ((int)c.pend.size() == tr::kRedBatch) return flush_reduce(c);
+  return KDLAE_OK;
+}
 
 // one tgemm launch; `what` (+ the shape) labels it in the launch trace
 int gemm(Ctx& c, const tr::TGemm& g, size_t cap, const std::string& what) {
@@ -312,8 +352,10 @@ int conv1(Ctx& c, const std::string& n, V x, int Cin, int Cout, long long P, V o
 int bias_grad(Ctx& c, V dy, int N, long long P, float* out) {
   if (!out) return KDLAE_OK;
   const int nb = nblk_for(P, N);
-  LAUNCH(tr::launch_colsum(dy.p, dy.ld, N, P, 1, 0, c.red, nb, c.s));
-  LAUNCH(tr::launch_part_reduce(c.red, nb, N, 1, out, 0, 1.f, c.s));
+  float* part = red_take(c, (size_t)nb * N);
+  if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+  LAUNCH(tr::launch_colsum(dy.p, dy.ld, N, P, 1, 0, part, nb, c.s));
+  return queue_reduce(c, part, nb, N, N, out);
   return KDLAE_OK;
 }
 
@@ -459,30 +501,28 @@ int block_fwd(Ctx& c, BlockRec& r) {
 }
 
 // sum the nb partial rows [9 C weights | C bias] of a depthwise conv's gradient into its keys
-int dw_reduce(Ctx& c, int nb, int C, const std::string& n);
+int dw_reduce(Ctx& c, const float* part, int nb, int C, const std::string& n);
 
 int dw_wgrad(Ctx& c, const float* dy, const float* x, int ld, int C, int Bn, int H, int W, const std::string& n) {
   const long long P = (long long)Bn * H * W;
   const int nb = tr::dw_wgrad_blocks(C, Bn, H, W, nblk_for(P, 10LL * C, 256));
-  LAUNCH(tr::launch_dw_wgrad(dy, ld, x, ld, C, Bn, H, W, c.red, nb, c.s));
-  return dw_reduce(c, nb, C, n);
+  float* part = red_take(c, (size_t)nb * 10 * C);
+  if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+  LAUNCH(tr::launch_dw_wgrad(dy, ld, x, ld, C, Bn, H, W, part, nb, c.s));
+  return dw_reduce(c, part, nb, C, n);
 }
 
 // fused depthwise backward (train_dwg.hip) when its partial rows fit the reduction buffer
 bool dwg_fits(int C, int Bn, int H, int W) { return (size_t)tr::dwg_blocks(Bn, H, W) * 10 * C <= kRedCap; }
 
-int dw_reduce(Ctx& c, int nb, int C, const std::string& n) {
+int dw_reduce(Ctx& c, const float* part, int nb, int C, const std::string& n) {
   // partial columns: [9 C weights | C bias]; one reduce when the bias key directly follows the
   // weight key in the flat buffer (keys are 16-byte aligned, so only when 9 C % 4 == 0)
   float* gw = c.G(n + ".weight");
   float* gb = c.G(n + ".bias");
-  if (!gb || gb == gw + 9LL * C) {
-    LAUNCH(tr::launch_part_reduce(c.red, nb, gb ? 10 * C : 9 * C, 1, gw, 0, 1.f, c.s, 10 * C));
-  } else {
-    LAUNCH(tr::launch_part_reduce(c.red, nb, 9 * C, 1, gw, 0, 1.f, c.s, 10 * C));
-    LAUNCH(tr::launch_part_reduce(c.red + 9LL * C, nb, C, 1, gb, 0, 1.f, c.s, 10 * C));
-  }
-  return KDLAE_OK;
+  if (!gb || gb == gw + 9LL * C) return queue_reduce(c, part, nb, gb ? 10 * C : 9 * C, 10 * C, gw);
+  TRY(queue_reduce(c, part, nb, 9 * C, 10 * C, gw));
+  return queue_reduce(c, part + 9LL * C, nb, C, 10 * C, gb);
 }
 
 int ln_bwd(Ctx& c, const float* dy, const float* x, const float* st, int C, long long P, const std::string& n,
@@ -490,17 +530,15 @@ int ln_bwd(Ctx& c, const float* dy, const float* x, const float* st, int C, long
   const int bf = c.h->cfg.layernorm_biasfree;
   const int ncol = bf ? C : 2 * C;
   const int nb = nblk_for(P, ncol);
-  LAUNCH(tr::launch_ln_bwd(dy, C, x, C, c.W(n + ".weight"), st, C, P, bf, R, C, dx, C, c.red, nb, c.s));
+  float* part = red_take(c, (size_t)nb * ncol);
+  if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+  LAUNCH(tr::launch_ln_bwd(dy, C, x, C, c.W(n + ".weight"), st, C, P, bf, R, C, dx, C, part, nb, c.s));
   // partial columns: [C weight | C bias (WithBias)], split when the keys are not adjacent
   float* gw = c.G(n + ".weight");
   float* gb = bf ? nullptr : c.G(n + ".bias");
-  if (!gb || gb == gw + C) {
-    LAUNCH(tr::launch_part_reduce(c.red, nb, ncol, 1, gw, 0, 1.f, c.s));
-  } else {
-    LAUNCH(tr::launch_part_reduce(c.red, nb, C, 1, gw, 0, 1.f, c.s, ncol));
-    LAUNCH(tr::launch_part_reduce(c.red + C, nb, C, 1, gb, 0, 1.f, c.s, ncol));
-  }
-  return KDLAE_OK;
+  if (!gb || gb == gw + C) return queue_reduce(c, part, nb, ncol, ncol, gw);
+  TRY(queue_reduce(c, part, nb, C, ncol, gw));
+  return queue_reduce(c, part + C, nb, C, ncol, gb);
 }
 
 // d: [P][C] gradient of the block output on entry, of the block input on exit
@@ -517,9 +555,12 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   float* dy = c.alloc(P * L2);
   if (dwg_fits(2 * hid, Bn, r.H, r.W)) {
     // gate backward + transposed dwconv + dwconv weight gradient in one pass (train_dwg.hip)
+    const int nb = tr::dwg_blocks(Bn, r.H, r.W);
+    float* part = red_take(c, (size_t)nb * 10 * 2 * hid);
+    if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
     LAUNCH(tr::launch_dwgate_bwd(dg, L1, r.yd, L2, r.y, L2, c.W(p + ".ffn.dwconv.weight"), hid, Bn, r.H, r.W, dy, L2,
-                                 c.red, c.s));
-    TRY(dw_reduce(c, tr::dwg_blocks(Bn, r.H, r.W), 2 * hid, p + ".ffn.dwconv"));
+                                 part, c.s));
+    TRY(dw_reduce(c, part, nb, 2 * hid, p + ".ffn.dwconv"));
   } else {
     float* dyd = c.alloc(P * L2);
     LAUNCH(tr::launch_gate_bwd(dg, L1, r.yd, L2, hid, P, dyd, L2, c.s));
@@ -559,7 +600,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   float* dtp = c.alloc((size_t)Bn * heads);
   LAUNCH(tr::launch_attn_bwd(r.G, r.sumsq, c.W(p + ".attn.temperature"), r.A, dA, Bn, C, heads, Mq, cq, ck, dtp, c.s));
   float* gtemp = c.G(p + ".attn.temperature");  // outside LAUNCH: the dry run must record the write
-  LAUNCH(tr::launch_part_reduce(dtp, Bn, heads, 1, gtemp, 0, 1.f, c.s));
+  TRY(queue_reduce(c, dtp, Bn, heads, heads, gtemp));
   {
     tr::TGemm g;  // dq[p,i] = sum_j Mq[i,j] k[p,j] + cq[i] q[p,i]
     g.A = r.qkvd + C; g.sam = C3; g.sak = 1; g.bA1 = HW * C3; g.bA2 = Ch;
@@ -578,9 +619,12 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   }
   float* dqkv = c.alloc(P * C3);
   if (dwg_fits(C3, Bn, r.H, r.W)) {
+    const int nb = tr::dwg_blocks(Bn, r.H, r.W);
+    float* part = red_take(c, (size_t)nb * 10 * C3);
+    if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
     LAUNCH(tr::launch_dw_bwd(dqkvd, C3, r.qkv, C3, c.W(p + ".attn.qkv_dwconv.weight"), C3, Bn, r.H, r.W, dqkv, C3,
-                             c.red, c.s));
-    TRY(dw_reduce(c, tr::dwg_blocks(Bn, r.H, r.W), C3, p + ".attn.qkv_dwconv"));
+                             part, c.s));
+    TRY(dw_reduce(c, part, nb, C3, p + ".attn.qkv_dwconv"));
   } else {
     LAUNCH(tr::launch_dw_fwd(dqkvd, C3, c.W(p + ".attn.qkv_dwconv.weight"), nullptr, 1, C3, Bn, r.H, r.W, dqkv, C3,
                              c.s));
@@ -589,6 +633,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   float* dxn1 = c.alloc(P * C);
   TRY(conv1_bwd(c, p + ".attn.qkv", {r.xn1, C}, {dqkv, C3}, C, C3, P, {dxn1, C}));
   TRY(ln_bwd(c, dxn1, r.x, r.st1, C, P, p + ".norm1.body", dx1, d));
+  TRY(flush_reduce(c));  // before the block's scratch (dtp) is released
   c.off = mark;
   return KDLAE_OK;
 }
@@ -947,7 +992,8 @@ int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, 
   if (kdlae::debug_flag("train_trace")) c.trace = &h->trace;
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
-  const int rc = net_bwd(c, dhq, dsr, has_dsr);
+  int rc = net_bwd(c, dhq, dsr, has_dsr);
+  if (rc == KDLAE_OK) rc = flush_reduce(c);
   trace_dump(h, c.s, "bwd");
   return rc;
 }
@@ -1023,6 +1069,7 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
   int rc = net_bwd(c, dhq, dsr, has_dsr);
+  if (rc == KDLAE_OK) rc = flush_reduce(c);
   trace_dump(h, c.s, "bwd");
   if (rc) return rc;
   // every gradient the launches wrote must have been seen by the dry run the marks came from (a

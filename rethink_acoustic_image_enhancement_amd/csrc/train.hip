@@ -536,7 +536,11 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   const int rm = ((long long)((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * batch >= 512) ? 2 : 1;
   const int tiles = ((g.M + 64 * rm - 1) / (64 * rm)) * ((g.N + BN - 1) / BN);
   int splits = 1;
-  if (g.partial && partial_cap > 0) {
+  // implicit-GEMM convolutions (amode 1) split only when their tiles leave the chip mostly idle:
+  // r03 trace, splitting the 384-768-tile shapes as well was 20-110% slower (the partial round trip
+  // outweighs the fuller grid), the 72-144-tile Upsample convs 18-71% faster
+  const bool split_ok = g.amode != 1 || (long long)tiles * batch < 256;
+  if (g.partial && partial_cap > 0 && split_ok) {
     // fill ~KDLAE_SPLITK_BLOCKS blocks, each split at least KDLAE_SPLITK_MIN deep
     const long long blocks = tiles * batch;
     long long want = (KDLAE_SPLITK_BLOCKS + blocks - 1) / blocks;
@@ -1216,6 +1220,55 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(const float* __restri
     const long long o = (long long)seg * ncols + c;
     out[o] = accumulate ? out[o] + s : s;
   }
+}
+
+// Several independent partial reductions in one launch (r03): a TransformerBlock's backward ends
+// with ~5 small ones (two LayerNorm weight gradients, two depthwise weight + bias gradients, the
+// temperature); one launch each cost ~6.5 us of mostly fixed overhead.  Block x serves column group
+// x of the descriptor whose prefix range holds it; same fixed-order sums as part_reduce_kernel.
+__global__ __launch_bounds__(1024) void part_reduce_multi_kernel(RedBatch rb) {
+  __shared__ float red[16][64];
+  int j = 0;
+  while (j + 1 < rb.n && (int)blockIdx.x >= rb.cg_prefix[j + 1]) ++j;
+  const RedDesc& d = rb.d[j];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = ((int)blockIdx.x - rb.cg_prefix[j]) * 64 + lane;
+  float a = 0.f;
+  if (c < d.ncols) {
+    const float* p = d.part + c;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int b = wv;
+    for (; b + 48 < d.nblk; b += 64) {
+      a0 += p[(long long)b * d.pstride];
+      a1 += p[(long long)(b + 16) * d.pstride];
+      a2 += p[(long long)(b + 32) * d.pstride];
+      a3 += p[(long long)(b + 48) * d.pstride];
+    }
+    for (; b < d.nblk; b += 16) a0 += p[(long long)b * d.pstride];
+    a = (a0 + a1) + (a2 + a3);
+  }
+  red[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0 && c < d.ncols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][lane];
+    d.out[c] = s * d.scale;
+  }
+}
+
+hipError_t launch_part_reduce_multi(const RedDesc* d, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n > kRedBatch) return hipErrorInvalidValue;
+  RedBatch rb;
+  rb.n = n;
+  rb.cg_prefix[0] = 0;
+  for (int j = 0; j < n; ++j) {
+    rb.d[j] = d[j];
+    rb.cg_prefix[j + 1] = rb.cg_prefix[j] + (d[j].ncols + 63) / 64;
+  }
+  hipLaunchKernelGGL(part_reduce_multi_kernel, dim3(rb.cg_prefix[n]), dim3(1024), 0, s, rb);
+  return hipGetLastError();
 }
 
 hipError_t launch_colsum(const float* x, int ldx, int ncols, long long rows_per_seg, int nseg, int square, float* part,

@@ -95,6 +95,21 @@ hipError_t launch_colsum(const float* x, int ldx, int ncols, long long rows_per_
 hipError_t launch_part_reduce(const float* part, int nblk, int ncols, int nseg, float* out, int accumulate,
                               float scale, hipStream_t s, int pstride = 0);
 
+// out[c] = scale * sum_b part[b * pstride + c] for up to kRedBatch independent reductions, one launch
+struct RedDesc {
+  const float* part = nullptr;
+  float* out = nullptr;
+  int nblk = 0, ncols = 0, pstride = 0;
+  float scale = 1.f;
+};
+constexpr int kRedBatch = 8;
+struct RedBatch {
+  RedDesc d[kRedBatch];
+  int n;
+  int cg_prefix[kRedBatch + 1];
+};
+hipError_t launch_part_reduce_multi(const RedDesc* d, int n, hipStream_t s);
+
 // GELU gate (KDLAE_model.py:104-105): g = gelu_erf(y[:, :h]) * y[:, h:]
 hipError_t launch_gate_fwd(const float* y, int ldy, int hid, long long P, float* g, int ldg, hipStream_t s);
 hipError_t launch_gate_bwd(const float* dg, int ldg, const float* y, int ldy, int hid, long long P, float* dy,
