@@ -11,6 +11,7 @@
 // The same code runs in a dry mode (no launches) to size it, so the size is exact.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -197,6 +198,7 @@ struct Ctx {
   std::vector<tr::RedDesc> pend;
   size_t red_off = 0;
 
+  size_t red_cap = 0;  // floats of `red` (red_floats(): the largest single reduction's partials)
   float* alloc(size_t n) {
     off = (off + 255) / 256 * 256;
     float* p = reinterpret_cast<float*>(base + off);
@@ -225,9 +227,10 @@ int flush_reduce(Ctx& c);
 // a region of the reduction buffer for a queued reduction's partials (flushes when full)
 float* red_take(Ctx& c, size_t n) {
   n = (n + 63) / 64 * 64;
-  if (c.red_off + n > kRedCap) {
+  if (c.red_off + n > c.red_cap) {
     if (flush_reduce(c) != KDLAE_OK) return nullptr;
   }
+  if (n > c.red_cap) return nullptr;  // red_floats() covers every reduction of the step
   float* p = c.red + c.red_off;
   c.red_off += n;
   return p;
@@ -501,20 +504,6 @@ int block_fwd(Ctx& c, BlockRec& r) {
 }
 
 // sum the nb partial rows [9 C weights | C bias] of a depthwise conv's gradient into its keys
-int dw_reduce(Ctx& c, const float* part, int nb, int C, const std::string& n);
-
-int dw_wgrad(Ctx& c, const float* dy, const float* x, int ld, int C, int Bn, int H, int W, const std::string& n) {
-  const long long P = (long long)Bn * H * W;
-  const int nb = tr::dw_wgrad_blocks(C, Bn, H, W, nblk_for(P, 10LL * C, 256));
-  float* part = red_take(c, (size_t)nb * 10 * C);
-  if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
-  LAUNCH(tr::launch_dw_wgrad(dy, ld, x, ld, C, Bn, H, W, part, nb, c.s));
-  return dw_reduce(c, part, nb, C, n);
-}
-
-// fused depthwise backward (train_dwg.hip) when its partial rows fit the reduction buffer
-bool dwg_fits(int C, int Bn, int H, int W) { return (size_t)tr::dwg_blocks(Bn, H, W) * 10 * C <= kRedCap; }
-
 int dw_reduce(Ctx& c, const float* part, int nb, int C, const std::string& n) {
   // partial columns: [9 C weights | C bias]; one reduce when the bias key directly follows the
   // weight key in the flat buffer (keys are 16-byte aligned, so only when 9 C % 4 == 0)
@@ -553,7 +542,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   float* dg = c.alloc(P * L1);
   TRY(conv1_bwd(c, p + ".ffn.project_out", {r.g, L1}, {d, C}, hid, C, P, {dg, L1}, nullptr, 0, {r.wpo, L1}, true));
   float* dy = c.alloc(P * L2);
-  if (dwg_fits(2 * hid, Bn, r.H, r.W)) {
+  {
     // gate backward + transposed dwconv + dwconv weight gradient in one pass (train_dwg.hip)
     const int nb = tr::dwg_blocks(Bn, r.H, r.W);
     float* part = red_take(c, (size_t)nb * 10 * 2 * hid);
@@ -561,11 +550,6 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
     LAUNCH(tr::launch_dwgate_bwd(dg, L1, r.yd, L2, r.y, L2, c.W(p + ".ffn.dwconv.weight"), hid, Bn, r.H, r.W, dy, L2,
                                  part, c.s));
     TRY(dw_reduce(c, part, nb, 2 * hid, p + ".ffn.dwconv"));
-  } else {
-    float* dyd = c.alloc(P * L2);
-    LAUNCH(tr::launch_gate_bwd(dg, L1, r.yd, L2, hid, P, dyd, L2, c.s));
-    LAUNCH(tr::launch_dw_fwd(dyd, L2, c.W(p + ".ffn.dwconv.weight"), nullptr, 1, 2 * hid, Bn, r.H, r.W, dy, L2, c.s));
-    TRY(dw_wgrad(c, dyd, r.y, L2, 2 * hid, Bn, r.H, r.W, p + ".ffn.dwconv"));
   }
   float* dxn2 = c.alloc(P * C);
   TRY(conv1_bwd(c, p + ".ffn.project_in", {r.xn2, C}, {dy, L2}, C, 2 * hid, P, {dxn2, C}));
@@ -618,17 +602,13 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
     TRY(gemm(c, g, 0, "dk"));
   }
   float* dqkv = c.alloc(P * C3);
-  if (dwg_fits(C3, Bn, r.H, r.W)) {
+  {
     const int nb = tr::dwg_blocks(Bn, r.H, r.W);
     float* part = red_take(c, (size_t)nb * 10 * C3);
     if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
     LAUNCH(tr::launch_dw_bwd(dqkvd, C3, r.qkv, C3, c.W(p + ".attn.qkv_dwconv.weight"), C3, Bn, r.H, r.W, dqkv, C3,
                              part, c.s));
     TRY(dw_reduce(c, part, nb, C3, p + ".attn.qkv_dwconv"));
-  } else {
-    LAUNCH(tr::launch_dw_fwd(dqkvd, C3, c.W(p + ".attn.qkv_dwconv.weight"), nullptr, 1, C3, Bn, r.H, r.W, dqkv, C3,
-                             c.s));
-    TRY(dw_wgrad(c, dqkvd, r.qkv, C3, C3, Bn, r.H, r.W, p + ".attn.qkv_dwconv"));
   }
   float* dxn1 = c.alloc(P * C);
   TRY(conv1_bwd(c, p + ".attn.qkv", {r.xn1, C}, {dqkv, C3}, C, C3, P, {dxn1, C}));
@@ -853,7 +833,27 @@ int net_bwd(Ctx& c, const float* dhq, const float* dsr, bool has_dsr) {
   return KDLAE_OK;
 }
 
-void ctx_init(Ctx& c, const kdlae_tt_handle* h, void* ws, size_t ws_bytes, bool dry, hipStream_t s) {
+// floats the reduction buffer needs: kRedCap, or the largest fused depthwise backward's partials
+// ([dwg_blocks][10 C] at each level's resolution, C = 2 hid or 3 dim) when that is larger
+size_t red_floats(const kdlae_t_config& cf, int B, int H, int W) {
+  size_t need = kRedCap;
+  auto level = [&](int C, int h, int w) {
+    const size_t nb = (size_t)tr::dwg_blocks(B, h, w);
+    const int hid = hid_of(cf, C);
+    need = std::max(need, nb * 10 * (size_t)std::max(2 * hid, 3 * C) + 64);
+  };
+  const int d = cf.dim;
+  level(d, H, W);
+  level(2 * d, H, W);  // decoder_level1 / refinement / refinement_out
+  level(2 * d, H / 2, W / 2);
+  level(4 * d, H / 4, W / 4);
+  level(8 * d, H / 8, W / 8);
+  if (cf.static_train) level(d, 2 * H, 2 * W);  // enhance
+  return need;
+}
+
+void ctx_init(Ctx& c, const kdlae_tt_handle* h, void* ws, size_t ws_bytes, bool dry, hipStream_t s, int B, int H,
+              int W) {
   c.h = h;
   c.dry = dry;
   c.s = s;
@@ -861,7 +861,8 @@ void ctx_init(Ctx& c, const kdlae_tt_handle* h, void* ws, size_t ws_bytes, bool 
   c.cap = ws_bytes;
   c.off = 0;
   c.splitk = c.alloc(kSplitCap);
-  c.red = c.alloc(kRedCap);
+  c.red_cap = red_floats(h->cfg, B, H, W);
+  c.red = c.alloc(c.red_cap);
 }
 
 // KDLAE_DEBUG=train_trace: wait for the call's launches and append "phase,layer,kernel,ms" rows to
@@ -930,7 +931,7 @@ int64_t kdlae_tt_workspace_bytes(kdlae_tt_handle* h, int B, int H, int W) {
   if (h->ws_B == B && h->ws_H == H && h->ws_W == W) return h->ws_bytes;
   Saved keep = h->sv;
   Ctx c;
-  ctx_init(c, h, nullptr, 0, true, nullptr);
+  ctx_init(c, h, nullptr, 0, true, nullptr, B, H, W);
   h->sv = Saved{};
   h->sv.B = B; h->sv.H = H; h->sv.W = W;
   int rc = net_fwd(c, nullptr, nullptr, nullptr, nullptr);
@@ -955,7 +956,7 @@ int kdlae_tt_forward(kdlae_tt_handle* h, const float* theta, const float* img, c
   if (need < 0 || (size_t)need > ws_bytes) return fail(KDLAE_ESTATE, "training workspace too small");
   kdlae::DeviceGuard dg(h->device);
   Ctx c;
-  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
+  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream, B, H, W);
   c.th = theta;
   if (kdlae::debug_flag("train_trace")) c.trace = &h->trace;
   h->sv = Saved{};
@@ -977,7 +978,7 @@ int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, 
   const bool has_dsr = h->cfg.static_train && dsr;
   {  // size the backward before launching anything
     Ctx d;
-    ctx_init(d, h, nullptr, 0, true, nullptr);
+    ctx_init(d, h, nullptr, 0, true, nullptr, h->sv.B, h->sv.H, h->sv.W);
     d.off = h->sv.fwd_end;
     int rc = net_bwd(d, dhq, dsr, has_dsr);
     if (rc) return rc;
@@ -985,7 +986,7 @@ int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, 
   }
   kdlae::DeviceGuard dg(h->device);
   Ctx c;
-  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
+  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream, h->sv.B, h->sv.H, h->sv.W);
   c.th = theta;
   c.gr = grad;
   c.off = h->sv.fwd_end;
@@ -1011,7 +1012,7 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
     int nmarks = 0;
     {  // size the backward and find, per mark, which suffix of the flat buffer is final there
       Ctx d;
-      ctx_init(d, h, nullptr, 0, true, nullptr);
+      ctx_init(d, h, nullptr, 0, true, nullptr, h->sv.B, h->sv.H, h->sv.W);
       d.off = h->sv.fwd_end;
       d.gr = grad;
       d.touch = &touch;
@@ -1058,7 +1059,7 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
     h->mark_ev.push_back(e);
   }
   Ctx c;
-  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream);
+  ctx_init(c, h, ws, ws_bytes, false, (hipStream_t)stream, h->sv.B, h->sv.H, h->sv.W);
   c.th = theta;
   c.gr = grad;
   c.off = h->sv.fwd_end;

@@ -1,6 +1,7 @@
 // KDLAE-T training kernels for gfx950 (MI355X): generic MFMA GEMM with im2col / shifted-B modes and a
 // deterministic split-K, LayerNorm forward/backward with wavefront-shuffle channel reductions,
-// depthwise 3x3 forward / dX / dW, the MDTA softmax and its backward, the GELU gate, PixelShuffle,
+// depthwise 3x3 forward (the GDFN's fused depthwise + gate and both backward passes are in
+// train_dwg.hip), the MDTA softmax and its backward, PixelShuffle,
 // L1LossSr, grad-norm clip and AdamW.  Every reduction over pixels is two-pass (per-block partials,
 // then a fixed-order sum), so a training step is bit-reproducible run to run.
 //
@@ -979,65 +980,6 @@ __global__ __launch_bounds__(256) void dw_row_fwd_kernel(const float* __restrict
   }
 }
 
-// dW partials: block (chunk, channel group) sums dy[p,c] * in[p + off_t, c] (t < 9) and dy[p,c] (bias)
-// over its row segments; 4 waves combined in fixed order -> part[chunk][c*9 + t], part[chunk][9C + c].
-__global__ __launch_bounds__(256) void dw_row_wgrad_kernel(const float* __restrict__ dy, int ldd,
-                                                           const float* __restrict__ in, int ldi, int C, int Bn,
-                                                           int H, int W, int nrs, int per,
-                                                           float* __restrict__ part) {
-  __shared__ float red[4][10][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c = blockIdx.y * 64 + lane;
-  const bool live = c < C;
-  const int nsx = (W + DW_SEG - 1) / DW_SEG;
-  float acc[10];
-#pragma unroll
-  for (int k = 0; k < 10; ++k) acc[k] = 0.f;
-  const int r0 = blockIdx.x * per, r1 = min(nrs, r0 + per);
-  for (int r = r0 + wv; r < r1; r += 4) {
-    const int xs = r % nsx, row = r / nsx;
-    const int y = row % H, bi = row / H;
-    const long long img0 = (long long)bi * H * W;
-    const int x0 = xs * DW_SEG, x1 = min(W, x0 + DW_SEG);
-    float col[DW_U + 2][3];
-    dw_load_col(in, ldi, img0, y, x0 - 1, H, W, c, live, col[0]);
-    dw_load_col(in, ldi, img0, y, x0, H, W, c, live, col[1]);
-    for (int x = x0; x < x1; x += DW_U) {
-      float d[DW_U];
-#pragma unroll
-      for (int u = 0; u < DW_U; ++u) {
-        dw_load_col(in, ldi, img0, y, x + 1 + u, H, W, c, live, col[2 + u]);
-        d[u] = (live && x + u < x1) ? dy[(img0 + (long long)y * W + x + u) * ldd + c] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < DW_U; ++u) {
-#pragma unroll
-        for (int ty = 0; ty < 3; ++ty)
-#pragma unroll
-          for (int tx = 0; tx < 3; ++tx) acc[ty * 3 + tx] += d[u] * col[u + tx][ty];
-        acc[9] += d[u];
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        col[0][k] = col[DW_U][k];
-        col[1][k] = col[DW_U + 1][k];
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 10; ++k) red[wv][k][lane] = acc[k];
-  __syncthreads();
-  if (wv == 0 && live) {
-    float* o = part + (long long)blockIdx.x * 10 * C;
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const float s = ((red[0][k][lane] + red[1][k][lane]) + red[2][k][lane]) + red[3][k][lane];
-      if (k < 9) o[c * 9 + k] = s;
-      else o[9 * C + c] = s;
-    }
-  }
-}
-
 static int dw_rowsegs(int Bn, int H, int W) { return Bn * H * ((W + DW_SEG - 1) / DW_SEG); }
 
 // LDS-tiled version for views with ldi, ldo % 4 == 0: a block owns TY = 8 rows x TX pixel columns x
@@ -1139,25 +1081,6 @@ hipError_t launch_dw_fwd(const float* in, int ldi, const float* w, const float* 
   const int nrs = dw_rowsegs(Bn, H, W);
   hipLaunchKernelGGL(dw_row_fwd_kernel, dim3((nrs + 3) / 4, (C + 63) / 64), dim3(256), 0, s, in, ldi, w, b, flip, C,
                      Bn, H, W, nrs, out, ldo);
-  return hipGetLastError();
-}
-
-int dw_wgrad_blocks(int C, int Bn, int H, int W, int max_blocks) {
-  const int nrs = dw_rowsegs(Bn, H, W);
-  int nb = (nrs + 3) / 4;  // at least 4 row segments (one per wave) per block
-  if (nb > max_blocks) nb = max_blocks;
-  if (nb < 1) nb = 1;
-  const int per = (nrs + nb - 1) / nb;
-  return (nrs + per - 1) / per;
-}
-
-hipError_t launch_dw_wgrad(const float* dy, int ldd, const float* in, int ldi, int C, int Bn, int H, int W,
-                           float* part, int nblk, hipStream_t s) {
-  const int nrs = dw_rowsegs(Bn, H, W);
-  const int per = (nrs + nblk - 1) / nblk;
-  if ((nrs + per - 1) / per != nblk) return hipErrorInvalidValue;  // nblk must come from dw_wgrad_blocks
-  hipLaunchKernelGGL(dw_row_wgrad_kernel, dim3(nblk, (C + 63) / 64), dim3(256), 0, s, dy, ldd, in, ldi, C, Bn, H, W,
-                     nrs, per, part);
   return hipGetLastError();
 }
 
@@ -1285,46 +1208,6 @@ hipError_t launch_part_reduce(const float* part, int nblk, int ncols, int nseg, 
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------------------------- GELU gate
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-
-__global__ void gate_fwd_kernel(const float* __restrict__ y, int ldy, int hid, long long P, float* __restrict__ g,
-                                int ldg) {
-  const long long total = P * hid;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const long long p = idx / hid;
-    const int c = (int)(idx - p * hid);
-    g[p * ldg + c] = gelu_erf(y[p * ldy + c]) * y[p * ldy + hid + c];
-  }
-}
-
-__global__ void gate_bwd_kernel(const float* __restrict__ dg, int ldg, const float* __restrict__ y, int ldy, int hid,
-                                long long P, float* __restrict__ dy, int lddy) {
-  const long long total = P * hid;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const long long p = idx / hid;
-    const int c = (int)(idx - p * hid);
-    const float x1 = y[p * ldy + c], x2 = y[p * ldy + hid + c], d = dg[p * ldg + c];
-    const float cdf = 0.5f * (1.f + erff(x1 * 0.70710678118654752f));
-    const float pdf = 0.39894228040143268f * expf(-0.5f * x1 * x1);
-    dy[p * lddy + c] = d * x2 * (cdf + x1 * pdf);
-    dy[p * lddy + hid + c] = d * x1 * cdf;
-  }
-}
-
-hipError_t launch_gate_fwd(const float* y, int ldy, int hid, long long P, float* g, int ldg, hipStream_t s) {
-  hipLaunchKernelGGL(gate_fwd_kernel, dim3(grid_for(P * hid, 256, 65536)), dim3(256), 0, s, y, ldy, hid, P, g, ldg);
-  return hipGetLastError();
-}
-
-hipError_t launch_gate_bwd(const float* dg, int ldg, const float* y, int ldy, int hid, long long P, float* dy, int lddy,
-                           hipStream_t s) {
-  hipLaunchKernelGGL(gate_bwd_kernel, dim3(grid_for(P * hid, 256, 65536)), dim3(256), 0, s, dg, ldg, y, ldy, hid, P,
-                     dy, lddy);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------------------------- MDTA core
 constexpr float kNormEps = 1e-12f;  // F.normalize eps (KDLAE_model.py:135-136)

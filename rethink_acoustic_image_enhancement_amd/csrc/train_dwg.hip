@@ -27,13 +27,19 @@ namespace train {
 
 namespace {
 
-constexpr int kU = 4;         // columns per thread
+#ifndef KDLAE_DWG_U
+#define KDLAE_DWG_U 4
+#endif
+#ifndef KDLAE_DWG_TY
+#define KDLAE_DWG_TY 16
+#endif
+constexpr int kU = KDLAE_DWG_U;  // columns per thread
 constexpr int kTX = 4 * kU;   // columns per block
 // rows per block: 16, or 8 / 4 on the small levels so the grid still has >= 256 spatial blocks (the
 // 16^2 latent: 6 blocks per channel group at 16 rows, 0.7-1.0 TB/s)
 int rows_per_block(int Bn, int H, int W) {
   const int tx = (W + kTX - 1) / kTX;
-  int ty = 16;
+  int ty = KDLAE_DWG_TY;
   while (ty > 4 && (long long)Bn * tx * ((H + ty - 1) / ty) < 256) ty >>= 1;
   return ty;
 }

@@ -68,15 +68,9 @@ hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, cons
 // w[c][8-t] (dX of the same conv).
 hipError_t launch_dw_fwd(const float* in, int ldi, const float* w, const float* b, int flip, int C, int Bn, int H,
                          int W, float* out, int ldo, hipStream_t s);
-// dW partials over nblk = dw_wgrad_blocks(...) row chunks: part[blk][c*9 + t] = sum dy[p,c] in[p+off_t,c],
-// part[blk][9C + c] = sum dy[p,c]
-int dw_wgrad_blocks(int C, int Bn, int H, int W, int max_blocks);
-hipError_t launch_dw_wgrad(const float* dy, int ldd, const float* in, int ldi, int C, int Bn, int H, int W,
-                           float* part, int nblk, hipStream_t s);
-
 // Fused depthwise kernels (train_dwg.hip).  GDFN forward: yd = dw(y) (+b) over both halves
 // (x1 at [0, hid), x2 at [hid, 2 hid)) and g = gelu_erf(yd1) * yd2.  Backward: dy = dw^T(dyd) and the
-// weight / bias gradient partials part[dwg_blocks][10 C] (C = 2 hid, layout of launch_dw_wgrad),
+// weight / bias gradient partials part[dwg_blocks][10 C] (C = 2 hid; columns [9 C weights | C biases]),
 // with dyd = gate_bwd(dg, yd) computed on the fly (dwgate) or given (dw_bwd, C channels).
 int dwg_blocks(int Bn, int H, int W);
 hipError_t launch_dwgate_fwd(const float* y, int ldi, const float* w, const float* b, int hid, int Bn, int H, int W,
@@ -109,11 +103,6 @@ struct RedBatch {
   int cg_prefix[kRedBatch + 1];
 };
 hipError_t launch_part_reduce_multi(const RedDesc* d, int n, hipStream_t s);
-
-// GELU gate (KDLAE_model.py:104-105): g = gelu_erf(y[:, :h]) * y[:, h:]
-hipError_t launch_gate_fwd(const float* y, int ldy, int hid, long long P, float* g, int ldg, hipStream_t s);
-hipError_t launch_gate_bwd(const float* dg, int ldg, const float* y, int ldy, int hid, long long P, float* dy,
-                           int lddy, hipStream_t s);
 
 // MDTA core (KDLAE_model.py:130-140), per (image, head) with Ch x Ch matrices:
 // A = softmax(t[h] * G / (max(nq,eps) max(nk,eps)^T)), nq/nk from sumsq [B][2C] (q at [0,C), k at [C,2C)).

@@ -54,18 +54,9 @@ constexpr unsigned kOOB = 0x80000000u;  // past every descriptor's range: loads 
 // columns / k-groups take the kOOB offset), so each iteration issues the same number of vector
 // memory ops and the compiler's vmcnt waits for the current chunk's A registers stay exact instead
 // of draining the next chunk's prefetch (and the previous tile's stores).
-#ifndef KDLAE_ROWS_LB2
-#define KDLAE_ROWS_LB2 1
-#endif
-#ifndef KDLAE_ROWS_EPI_ALWAYS
-#define KDLAE_ROWS_EPI_ALWAYS 0
-#endif
+// (2 waves per SIMD: the r03 sweep measured a 1-wave-per-SIMD register budget slower)
 template <int NT, bool HASR, bool VECC>
-#if KDLAE_ROWS_LB2
 __global__ __launch_bounds__(kThreads, 2) void tgemm_rows_kernel(RowsArgs a) {
-#else
-__global__ __launch_bounds__(kThreads) void tgemm_rows_kernel(RowsArgs a) {
-#endif
   // [NT][kg][64] fragments, then [NT][4] bias and [NT][4] residual scale
   extern __shared__ __attribute__((aligned(16))) f32x4 wl[];
   const TGemm& g = a.g;
@@ -210,12 +201,11 @@ __global__ __launch_bounds__(kThreads) void tgemm_rows_kernel(RowsArgs a) {
         }
       }
     }
-    // epilogue, issued by every item (stores of a tile's earlier chunks go to kOOB): lane (li, lq)
-    // of (t, r) holds channels n0 + 16t + 4lq .. +3 of row 16r + li
+    // epilogue of a tile's last chunk (an unconditional epilogue with the earlier chunks' stores
+    // sent to kOOB measured up to 25% slower): lane (li, lq) of (t, r) holds channels
+    // n0 + 16t + 4lq .. +3 of row 16r + li
     const bool closes = ch == a.nchunk - 1;
-#if !KDLAE_ROWS_EPI_ALWAYS
     if (!closes) return;
-#endif
     const int row0 = tile * kTileRows + wave * (kRT * 16);
 #pragma unroll
     for (int r = 0; r < kRT; ++r) {

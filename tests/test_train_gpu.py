@@ -214,6 +214,26 @@ def test_full_config_small_image_matches_oracle():
     _check_grads(keys, tr.engine.keys, tr.grad.cpu(), grads_ref)
 
 
+def test_odd_width_config_matches_oracle():
+    """dim 10 (C = 10 / 20 / 40 / 80, 3C = 30, hid = 26, 2 hid = 52): widths that are not multiples of
+    4 take the scalar fallbacks — one-wave LayerNorm, the row-sweep depthwise forward, the tiled GEMM
+    with scalar operand loads and the row-streaming GEMM's element stores — on a ragged 2 x 32 x 48
+    batch with the sr branch (enhance at 64 x 96), WithBias."""
+    cfg = dict(dim=10, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, LayerNorm_type="WithBias")
+    m = _model(cfg)
+    keys = [k for k, _ in m.named_parameters()]
+    img = torch.from_numpy(hash_images("img:odd", (2, 3, 32, 48)))
+    rate = torch.full((2, 1, 32, 48), 0.4)
+    gt = {"hq": torch.from_numpy(hash_images("gt:odd", (2, 3, 32, 48))),
+          "sr": torch.from_numpy(hash_images("gtsr:odd", (2, 3, 64, 96)))}
+    tr = KDLAETrainer(m)
+    loss = tr.forward_backward({"img": img.to(DEV), "denoise_rate": rate.to(DEV)}, _dev(gt))
+    torch.cuda.synchronize()
+    loss_ref, grads_ref = _oracle(cfg, keys, img, rate, gt)
+    assert abs(float(loss) - float(loss_ref)) <= 1e-5 * abs(float(loss_ref))
+    _check_grads(keys, tr.engine.keys, tr.grad.cpu(), grads_ref)
+
+
 @pytest.mark.parametrize("cfg", [dict(LayerNorm_type="BiasFree"),
                                  dict(LayerNorm_type="WithBias", params="plus", static="no")])
 def test_marked_backward_equals_backward_and_marks_close_suffixes(cfg):
@@ -273,7 +293,7 @@ def test_mark_events_fire_after_their_suffix_is_final():
     done = torch.cuda.Event()
     tr.grad.fill_(float("nan"))  # a snapshot of a not-yet-zeroed or unwritten range shows up as NaN
     torch.cuda.synchronize()
-    torch.cuda._sleep(200_000_000)  # hold the GPU while the host enqueues the step and the snapshots
+    torch.cuda._sleep(1_000_000_000)  # hold the GPU while the host enqueues the step and the snapshots (a tracer slows the host)
     tr.forward_backward(inp, gt, marked=True)
     done.record()
     for j, lo in enumerate(los):

@@ -52,7 +52,10 @@ def launched_kernels(prof_dir):
     import sqlite3
     ks = {}
     for f in glob.glob(os.path.join(prof_dir, "**", "*.db"), recursive=True):
-        for (name, n) in sqlite3.connect(f).execute("select name, count(*) from kernels group by name"):
+        con = sqlite3.connect(f)
+        if not con.execute("select name from sqlite_master where type in ('table', 'view') and name = 'kernels'").fetchall():
+            continue  # a CSV run leaves an empty database beside its CSV files
+        for (name, n) in con.execute("select name, count(*) from kernels group by name"):
             k = norm(name)
             ks[k] = ks.get(k, 0) + int(n)
     for f in glob.glob(os.path.join(prof_dir, "**", "*kernel_stats.csv"), recursive=True):
