@@ -144,13 +144,18 @@ def timed_steps(step, steps: int, distributed: bool, dev):
 
 def cpu_timed(fn, runs: int = 3):
     """BASELINE.md CPU-baseline procedure: one untimed warm-up call, then the median of `runs`
-    timed calls.  Returns (warm-up output, median seconds, sorted timings)."""
+    timed calls.  Returns (warm-up output, median seconds, sorted timings).  A progress line per
+    call goes to stderr (the T16 sample is ~40 s a call: a silent 3-minute stretch reads as a hang
+    to a watchdog)."""
+    t0 = time.perf_counter()
     out = fn()
+    print(f"[bench] cpu baseline warm-up: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     ts = []
-    for _ in range(runs):
+    for i in range(runs):
         t0 = time.perf_counter()
         fn()
         ts.append(time.perf_counter() - t0)
+        print(f"[bench] cpu baseline run {i + 1}/{runs}: {ts[-1]:.1f} s", file=sys.stderr, flush=True)
     ts.sort()
     return out, ts[len(ts) // 2], ts
 

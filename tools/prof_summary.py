@@ -10,7 +10,8 @@ import sqlite3
 
 
 def short(name):
-    n = re.sub(r"\(.*", "", name)
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", n)
     n = n.replace("void ", "").replace("kdlae::", "")
     return n
 
