@@ -293,6 +293,31 @@ int kdlae_train_mixup(const float* in, float* out, int B, int64_t per_sample, co
 /* replaces BaseModel.model_ema(decay) (Train/basicsr/models/base_model.py:54-62) over the flat buffers. */
 int kdlae_train_ema(float* ema, const float* theta, int64_t n, float decay, void* stream);
 
+/* ---- Kernel self-test entry points (tests/test_kernel_variants_gpu.py; not part of the drop-in
+ * boundary).  One launch of the training GEMM family on caller device buffers:
+ *   C(m, n) = sum_k A(m, k) B(k, n) [+ bias[n]] [+ rs[n] R(m, n)], batch z = z1 * nz2 + z2, every
+ *   operand offset by z1 * b?1 + z2 * b?2 (floats); amode 1 = implicit 3x3 im2col of the NHWC view A
+ *   (pixel stride lda, k = tap * Cg + c, dilation dil, zero padding), bmode 1 = the NHWC view B shifted
+ *   by tap z2 (conv weight gradient), bmode 2 / 3 = a 3x3 OIHW weight as the forward / transposed
+ *   conv operand (see train_kernels.h TGemm).  route: 0 = the engine's own dispatch, 1 = the
+ *   row-streaming kernel, 2 = the pixel-reduction kernel (needs partial), 3 = the tiled kernels. */
+typedef struct kdlae_debug_tgemm_desc {
+  const float* A; int64_t sam, sak; int amode;
+  const float* B; int64_t sbk, sbn; int bmode;
+  float* C; int64_t scm, scn;
+  const float* bias;
+  const float* R; int64_t srm, srn;
+  const float* rs;
+  int M, N, K, nz1, nz2;
+  int64_t bA1, bA2, bB1, bB2, bC1, bC2, bR1, bR2, brs1, brs2;
+  int Bn, H, W, Cg, dil;
+  int64_t lda, ldb;
+  float* partial; int64_t partial_floats;
+  int route;
+  int c_pad_ok;
+} kdlae_debug_tgemm_desc;
+int kdlae_debug_tgemm(const kdlae_debug_tgemm_desc* d, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,6 +37,7 @@ EXPORTS = (
     "kdlae_tt_mark_count", "kdlae_tt_mark_lo", "kdlae_tt_mark_wait", "kdlae_tt_mark_sync",
     "kdlae_train_l1sr_scratch_floats", "kdlae_train_l1sr", "kdlae_train_adamw_scratch_floats",
     "kdlae_train_clip_adamw", "kdlae_train_mixup", "kdlae_train_ema",
+    "kdlae_debug_tgemm",
 )
 
 
@@ -158,6 +159,7 @@ def lib() -> ctypes.CDLL:
                                          c_void_p]
     L.kdlae_train_mixup.argtypes = [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_float, c_void_p]
     L.kdlae_train_ema.argtypes = [c_void_p, c_void_p, c_int64, c_float, c_void_p]
+    L.kdlae_debug_tgemm.argtypes = [c_void_p, c_void_p]
     for name in EXPORTS:
         if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes", "_padded_size", "_num_floats",
                               "_scratch_floats", "_params_numel", "_mark_lo")):

@@ -532,9 +532,14 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   if (KDLAE_TRAIN_COLS && g.partial && partial_cap > 0 && (long long)g.K * g.nz1 * g.nz2 >= 16384 &&
       tgemm_cols_eligible(g))
     return launch_tgemm_cols(g, partial_cap, s);
+  return launch_tgemm_tiled(g, partial_cap, s);
+}
+
+hipError_t launch_tgemm_tiled(TGemm g, size_t partial_cap, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
   const long long batch = (long long)g.nz1 * g.nz2;
   // 128-row tiles when the grid still holds >= 2 blocks per CU with them (tall activation GEMMs)
-  const int rm = ((long long)((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * batch >= 512) ? 2 : 1;
+  const int rm = (g.bmode != 1 && (long long)((g.M + 127) / 128) * ((g.N + BN - 1) / BN) * batch >= 512) ? 2 : 1;
   const int tiles = ((g.M + 64 * rm - 1) / (64 * rm)) * ((g.N + BN - 1) / BN);
   int splits = 1;
   // implicit-GEMM convolutions (amode 1) split only when their tiles leave the chip mostly idle:
@@ -591,7 +596,8 @@ hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s) {
   } else if (g.amode == 0 && g.bmode == 0) {
     launch_t<0, 0>(g, kchunk, flags, rm, grid, s);
   }
-  else if (g.amode == 0 && g.bmode == 1) launch_t<0, 1>(g, kchunk, flags, rm, grid, s);
+  // (the conv weight gradient's M = C_out never reaches 512 tiles of 128 rows: 64-row tiles only)
+  else if (g.amode == 0 && g.bmode == 1) hipLaunchKernelGGL((tgemm_kernel<0, 1, 1>), grid, dim3(256), 0, s, g, kchunk, flags);
   else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, flags, rm, grid, s);
   else return hipErrorInvalidValue;

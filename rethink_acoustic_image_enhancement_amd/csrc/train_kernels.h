@@ -42,6 +42,8 @@ struct TGemm {
 };
 // Launch; picks split-K itself when `partial` (capacity `partial_cap` floats) is given.
 hipError_t launch_tgemm(TGemm g, size_t partial_cap, hipStream_t s);
+// the tiled 64 x 64 / 128 x 64 kernels only (launch_tgemm's fallback: small grids, im2col modes)
+hipError_t launch_tgemm_tiled(TGemm g, size_t partial_cap, hipStream_t s);
 // Row-streaming kernel (train_rows.hip) for plain contractions with k-contiguous A rows and no
 // split-K: weights staged in LDS in MFMA fragment order, A streamed to VGPRs.  launch_tgemm routes
 // every eligible call there.

@@ -300,7 +300,11 @@ hipError_t launch_nt(RowsArgs a, int nz, size_t lds, hipStream_t s) {
 
 template <int NT>
 hipError_t launch_nt(const RowsArgs& a, bool hasr, bool vecc, int nz, size_t lds, hipStream_t s) {
-  if (hasr) return vecc ? launch_nt<NT, true, true>(a, nz, lds, s) : launch_nt<NT, true, false>(a, nz, lds, s);
+  if constexpr (NT <= 4) {  // residual variants only up to NT = 4 (wider ones spill)
+    if (hasr) return vecc ? launch_nt<NT, true, true>(a, nz, lds, s) : launch_nt<NT, true, false>(a, nz, lds, s);
+  } else {
+    if (hasr) return hipErrorInvalidValue;
+  }
   return vecc ? launch_nt<NT, false, true>(a, nz, lds, s) : launch_nt<NT, false, false>(a, nz, lds, s);
 }
 
