@@ -318,6 +318,85 @@ typedef struct kdlae_debug_tgemm_desc {
 } kdlae_debug_tgemm_desc;
 int kdlae_debug_tgemm(const kdlae_debug_tgemm_desc* d, void* stream);
 
+/* One launch of the inference implicit-GEMM family (gemm.hip) with the tile shape forced:
+ *   out[b][p][n] = relu?( sum_k A'[b][p][k] Wp(n, k) + bias[n] (+ R) ), A' = A or LN(A) over ln_C
+ *   (ln 1 BiasFree, 2 WithBias, unit weight); ksize 3: implicit 3x3 (kt 3: 3x3x3 over F frames),
+ *   k = tap * 16 cg_per_tap + c, zero padding = dil; out_mode 1 / 2 stores through PixelUnshuffle(2)
+ *   / PixelShuffle(2) (R then in the output geometry).  Wp: fragment-packed [ntiles][kgroups][64][4],
+ *   element (l, e) of (t, g) = W(16 t + l % 16, 16 g + 4 (l / 16) + e); + b * w_img_stride per image.
+ *   Wm != 0: fused attention output, x1 = R + Wm v (+ bias_m) stored to out1, then out = LN(x1) W.
+ *   stats: [pixels][2] scratch when LN meets a chunked K.  group_tiles > 0: resident schedule.
+ *   tiles_per_block 0: the engine's grid rule.  route 0: production dispatch; 1: the r01
+ *   conv_gemm_kernel of (NT, KG) (the fallback for ld % 4 != 0 views). */
+typedef struct kdlae_debug_gemm_desc {
+  const float* A; int lda;
+  int Bn, F, H, W;
+  int ksize, kt, dil, cg_per_tap, kgroups;
+  const float* Wp; int64_t w_img_stride; int ntiles, N;
+  const float* bias;
+  float* out; int ldo;
+  const float* R; int ldr;
+  int ln, ln_C, relu, out_mode;
+  float* stats;
+  const float* Wm; int64_t wm_img_stride; const float* bias_m; float* out1; int ldo1;
+  int NT, KG, wpe, group_tiles, tiles_per_block;
+  int route;
+} kdlae_debug_gemm_desc;
+int kdlae_debug_gemm(const kdlae_debug_gemm_desc* d, void* stream);
+/* Entry i of a compiled variant table: family 0 conv_gemm_kernel (NT, KG, CONV3, OUT, PF, WPE, RES),
+ * 1 gemm_res_kernel (NT, KG, NCH, PF), 2 gemm_chunk_kernel (NT, KG, CONV3, OUT), 3 gemm_attn_in_kernel
+ * (NT, KG, NCH).  Fills v[0..6]; returns 1, or 0 past the end. */
+int kdlae_debug_gemm_variant(int family, int i, int* v);
+
+/* MDTA pass 1 + 2 (mdta.hip): depthwise 3x3 of qkv ([P][ld], wdw [9][3C] tap-major, bdw [3C]), v
+ * stored to v_out, per (image, head) the Gram q k^T and the squared norms summed into
+ * reduced[Bn * heads][Ch^2 + 2 Ch] (Gram in accumulator order: element (i * CT + j) * 256 + 4 l + e =
+ * G[16 i + 4 (l / 16) + e][16 j + l % 16], CT = Ch / 16; then |q_c|^2, |k_c|^2).  partial: scratch of
+ * partial_floats.  route 0: production (ring kernel where it applies), 1: without the ring kernel
+ * (zeros ignored), 2: the generic 64-pixel-step kernel. */
+typedef struct kdlae_debug_gram_desc {
+  const float* qkv; int ld;
+  const float* wdw; const float* bdw;
+  float* v_out; int ldv;
+  float* partial; int64_t partial_floats;
+  float* reduced;
+  const float* zeros;
+  int C, heads, Bn, H, W;
+  int route;
+} kdlae_debug_gram_desc;
+int kdlae_debug_gram(const kdlae_debug_gram_desc* d, void* stream);
+
+/* Training LayerNorm (train.hip) over P pixels of C channels: dir 0 forward y = LN(x) w (+ b),
+ * stats[P][2]; dir 1 backward dx = R + dLN(dy), part[nblk][C | 2 C] the per-block weight (and bias)
+ * gradient partials.  route 0: production dispatch, 1: the one-wave-per-pixel kernels. */
+typedef struct kdlae_debug_ln_desc {
+  int dir;
+  const float* x; int ldx;
+  const float* w; const float* b;
+  int C; int64_t P; int biasfree;
+  float* y; int ldy;
+  float* stats;
+  const float* dy; int ldd;
+  const float* R; int ldr;
+  float* dx; int lddx;
+  float* part; int nblk;
+  int route;
+} kdlae_debug_ln_desc;
+int kdlae_debug_ln(const kdlae_debug_ln_desc* d, void* stream);
+
+/* Small-input 3x3 / 3x3x3 conv (conv_small.hip), Cin * 9 * kt <= 36, Cout % 16 == 0: input element
+ * (b, frame t, y, x, c) at in[b sb + t st + y sy + x sx + c sc] (minus in_sub at the same offset),
+ * w [Cout][Cin][kt][3][3], NHWC output [Bn * F * H * W][ldo]; valid input extent vh x vw (0 = H, W). */
+typedef struct kdlae_debug_small_in_desc {
+  const float* in; int64_t sb, sc, sy, sx, st;
+  const float* in_sub;
+  int Cin, Cout, dil, kt, F;
+  const float* w; const float* bias;
+  float* out; int ldo;
+  int Bn, H, W, vh, vw, relu;
+} kdlae_debug_small_in_desc;
+int kdlae_debug_small_in(const kdlae_debug_small_in_desc* d, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,11 @@ EXPORTS = (
     "kdlae_train_l1sr_scratch_floats", "kdlae_train_l1sr", "kdlae_train_adamw_scratch_floats",
     "kdlae_train_clip_adamw", "kdlae_train_mixup", "kdlae_train_ema",
     "kdlae_debug_tgemm",
+    "kdlae_debug_gemm",
+    "kdlae_debug_gemm_variant",
+    "kdlae_debug_gram",
+    "kdlae_debug_ln",
+    "kdlae_debug_small_in",
 )
 
 
@@ -160,6 +165,9 @@ def lib() -> ctypes.CDLL:
     L.kdlae_train_mixup.argtypes = [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_float, c_void_p]
     L.kdlae_train_ema.argtypes = [c_void_p, c_void_p, c_int64, c_float, c_void_p]
     L.kdlae_debug_tgemm.argtypes = [c_void_p, c_void_p]
+    for f in ("kdlae_debug_gemm", "kdlae_debug_gram", "kdlae_debug_ln", "kdlae_debug_small_in"):
+        getattr(L, f).argtypes = [c_void_p, c_void_p]
+    L.kdlae_debug_gemm_variant.argtypes = [c_int, c_int, ctypes.POINTER(c_int)]
     for name in EXPORTS:
         if not name.endswith(("_last_error", "_abi_version", "_workspace_bytes", "_padded_size", "_num_floats",
                               "_scratch_floats", "_params_numel", "_mark_lo")):

@@ -53,7 +53,12 @@ __global__ __launch_bounds__(256) void conv_small_in_kernel(SmallInParams p) {
     const int co = 16 * t + li;
     const bool cok = co < p.Cout;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) wf[t][s] = (cok && kok[s]) ? p.w[co * K + 4 * s + lq] : 0.f;
+    for (int s = 0; s < KS; ++s) {
+      const int k = 4 * s + lq;
+      // wt: transposed conv's weight [Cin][wt][3][3], flipped taps (kt 1: k = ci * 9 + tap)
+      const int wi = p.wt ? ((k / 9) * p.wt + co) * 9 + 8 - k % 9 : co * K + k;
+      wf[t][s] = (cok && kok[s]) ? p.w[wi] : 0.f;
+    }
     const int cb = 16 * t + 4 * lq;
     bq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (p.bias && cb < p.Cout) bq[t] = f32x4{p.bias[cb], p.bias[cb + 1], p.bias[cb + 2], p.bias[cb + 3]};
@@ -122,14 +127,15 @@ static void launch_small_in_nt(const SmallInParams& p, unsigned blocks, hipStrea
 }
 
 hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s) {
-  if (p.Cin * 9 * p.kt > 36 || p.Cout % 16 || (p.kt != 1 && p.kt != 3)) return hipErrorInvalidValue;
+  if (p.Cin * 9 * p.kt > 36 || p.Cout % 16 || (p.kt != 1 && p.kt != 3) || (p.wt && (p.kt != 1 || p.wt < p.Cout)))
+    return hipErrorInvalidValue;
   const long long chunks = ((long long)p.Bn * p.F * p.H * p.W + 63) / 64;
   long long blocks = (chunks + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   const int K = p.Cin * 9 * p.kt;
   for (int co0 = 0; co0 < p.Cout; co0 += 128) {  // up to 8 output tiles per pass
     SmallInParams q = p;
-    q.w = p.w + (size_t)co0 * K;
+    q.w = p.w + (p.wt ? (size_t)co0 * 9 : (size_t)co0 * K);
     q.bias = p.bias ? p.bias + co0 : nullptr;
     q.out = p.out + co0;
     q.Cout = p.Cout - co0 < 128 ? p.Cout - co0 : 128;
@@ -148,7 +154,7 @@ __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
   const int nw = taps * p.Cin * 4;
   for (int i = threadIdx.x; i < nw; i += 256) {
     const int o = i & 3, ci = (i >> 2) % p.Cin, t = (i >> 2) / p.Cin;
-    wso[i] = o < p.Cout ? p.w[(o * p.Cin + ci) * taps + t] : 0.f;
+    wso[i] = o < p.Cout ? p.w[p.wt ? (ci * p.Cout + o) * taps + taps - 1 - t : (o * p.Cin + ci) * taps + t] : 0.f;
   }
   __syncthreads();
   const int fhw = p.H * p.W;
@@ -193,6 +199,7 @@ __global__ __launch_bounds__(256) void conv_small_out_kernel(SmallOutParams p) {
         if (p.res) v += p.res[oi];
         p.out[oi] = v;
       } else {
+        if (p.res_nhwc) v += p.res_nhwc[pix * p.ldr + o];
         p.out[pix * p.ldo + o] = v;
       }
     }
@@ -217,7 +224,7 @@ __global__ __launch_bounds__(256) void conv_small_out_tiled_kernel(SmallOutParam
     const int t = i / p.Cin, ci = i - t * p.Cin;
     f32x4 w4;
 #pragma unroll
-    for (int o = 0; o < 4; ++o) w4[o] = o < p.Cout ? p.w[(o * p.Cin + ci) * 9 + t] : 0.f;
+    for (int o = 0; o < 4; ++o) w4[o] = o < p.Cout ? p.w[p.wt ? (ci * p.Cout + o) * 9 + 8 - t : (o * p.Cin + ci) * 9 + t] : 0.f;
     wq[i] = w4;
   }
   const int tx_n = (p.W + kSoTW - 1) / kSoTW, ty_n = (p.H + kSoTH - 1) / kSoTH;
@@ -294,6 +301,7 @@ __global__ __launch_bounds__(256) void conv_small_out_tiled_kernel(SmallOutParam
         if (p.res) v += p.res[oi];
         p.out[oi] = v;
       } else {
+        if (p.res_nhwc) v += p.res_nhwc[pix * p.ldr + o];
         p.out[pix * p.ldo + o] = v;
       }
     }
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(256) void conv_small_out_tiled_kernel(SmallOutParam
 }
 
 hipError_t launch_conv_small_out(const SmallOutParams& p, hipStream_t s) {
-  if (p.Cin % 16 || (p.ks != 1 && p.ks != 3)) return hipErrorInvalidValue;
+  if (p.Cin % 16 || (p.ks != 1 && p.ks != 3) || (p.wt && p.ks != 3)) return hipErrorInvalidValue;
   if (p.ks == 3 && p.F == 1 && p.ld % 4 == 0 && p.Cin <= 256) {
     const long long blocks = (long long)p.Bn * ((p.H + kSoTH - 1) / kSoTH) * ((p.W + kSoTW - 1) / kSoTW);
     const size_t lds = (size_t)9 * p.Cin * sizeof(f32x4);

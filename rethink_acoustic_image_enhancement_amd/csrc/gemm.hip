@@ -975,25 +975,38 @@ static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, si
   X(6, 3, 1, true) X(6, 3, 2, true) X(9, 6, 1, true) X(9, 6, 2, true) X(8, 6, 1, true) X(8, 6, 2, true) \
   X(6, 6, 1, true) X(6, 6, 2, true) X(6, 6, 3, true) X(3, 6, 1, true) X(3, 6, 2, true) X(3, 8, 1, true) X(3, 8, 2, true) \
   X(6, 8, 1, true) X(6, 8, 2, true) X(6, 12, 1, false) X(6, 12, 2, false) X(8, 12, 1, false) \
-  X(8, 12, 2, false) X(3, 12, 1, false) X(3, 12, 2, false) X(6, 16, 1, false) X(3, 16, 1, false)
+  X(3, 12, 1, false) X(3, 12, 2, false) X(6, 16, 1, false) X(3, 16, 1, false)
+// (every entry's NT x NCH x KG KiB of weights fits the 160 KiB LDS; choose_variant keeps it <= 158)
+
+// residual (HASR) instance only where launch_gemm's no-spill rule (res_ok) can admit a residual
+template <int NT, int KG, int NCH>
+constexpr bool res2_hasr_ok() { return NT * NCH <= 12 && NT * NCH * KG <= 72 && KG <= 8; }
 
 template <int NT, int KG, int NCH, bool PF>
 static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
+  constexpr bool RK = res2_hasr_ok<NT, KG, NCH>();
   static size_t attr_lds[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   if (lds > attr_lds[dev]) {
-    for (const void* f : {reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, 2, true, PF>),
-                          reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, 2, false, PF>)}) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, 2, false, PF>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if constexpr (RK) {
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, 2, true, PF>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
     attr_lds[dev] = lds;
   }
-  if (p.R)
-    hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, true, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
-  else
-    hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, false, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+  if constexpr (RK) {
+    if (p.R) {
+      hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, true, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+      return hipGetLastError();
+    }
+  }
+  if (p.R) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, false, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
   return hipGetLastError();
 }
 
@@ -1052,7 +1065,10 @@ static hipError_t launch_chunk2(const GemmParams& p, int grid_x, int grid_y, hip
   return hipGetLastError();
 }
 
-hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s) {
+// route 0: the production dispatch; route 1 (self-test only): skip the r02 straight-line resident
+// and chunked kernels so the r01 conv_gemm_kernel instance of (NT, KG) runs — the fallback the
+// production dispatch takes for views those kernels cannot address (ld % 4 != 0, > 2 GiB images)
+hipError_t launch_gemm_route(const GemmParams& p, int NT, int KG, int wpe, int grid_x, int route, hipStream_t s) {
   const bool c3 = p.ksize == 3;
   const bool res = p.group_tiles > 0;
   if (p.ln && !p.stats && (p.kchunks > 1 || p.kgroups > KG)) return hipErrorInvalidValue;  // LN needs whole rows
@@ -1083,7 +1099,7 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
 #undef X
     return hipErrorInvalidValue;
   }
-  if (res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && !p.relu) {
+  if (route == 0 && res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && !p.relu) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;
     const int nch = (p.group_tiles + NT - 1) / NT;
@@ -1092,6 +1108,7 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
     // residual variants keep NT x 2 residual float4 live across the chunk's MFMAs: only where that
     // fits the 256-VGPR budget without spills (hipcc -Rpass-analysis), else the r01 kernel
     const bool res_ok = !p.R || (NT * nch <= 12 && NT * nch * KG <= 72 && KG <= 8 && p.ldr % 4 == 0);  // no VGPR spills
+    // (res2_hasr_ok is this rule at compile time: keep the two in step)
     if (mx < (1LL << 31) && lds <= 160 * 1024 && p.lda % 4 == 0 && p.ldo % 4 == 0 && res_ok) {
 #define X(a, b, c, f) \
       if (NT == a && KG == b && nch == c) return launch_res2<a, b, c, f>(p, grid_x, grid_y, lds, s);
@@ -1113,7 +1130,7 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
     lds = (size_t)NT * KG * 1024 + (size_t)NT * 64;
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (!res && gemm_has_variant2(NT, KG, c3, p.out_mode) && p.lda % 4 == 0) {
+  if (route == 0 && !res && gemm_has_variant2(NT, KG, c3, p.out_mode) && p.lda % 4 == 0) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long osz = p.out_mode == 2 ? 4 * HW : (p.out_mode == 1 ? HW / 4 : HW);
     const bool fits = HW * p.lda * 4 < (1LL << 31) && osz * p.ldo * 4 < (1LL << 31) &&
@@ -1131,6 +1148,45 @@ hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x,
   KDLAE_GEMM_VARIANTS(X)
 #undef X
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s) {
+  return launch_gemm_route(p, NT, KG, wpe, grid_x, 0, s);
+}
+
+// Entry i of a variant table (self-test enumeration): family 0 = conv_gemm_kernel (NT, KG, CONV3,
+// OUT, PF, WPE, RES), 1 = gemm_res_kernel (NT, KG, NCH, PF), 2 = gemm_chunk_kernel (NT, KG, CONV3,
+// OUT), 3 = gemm_attn_in_kernel (NT, KG, NCH).  Returns false past the end.
+bool gemm_variant_entry(int family, int i, int* v) {
+  int n = 0;
+  switch (family) {
+    case 0:
+#define X(a, b, c, o, f, w, r) \
+  if (n++ == i) { v[0] = a; v[1] = b; v[2] = c; v[3] = o; v[4] = f; v[5] = w; v[6] = r; return true; }
+      KDLAE_GEMM_VARIANTS(X)
+#undef X
+      return false;
+    case 1:
+#define X(a, b, c, f) \
+  if (n++ == i) { v[0] = a; v[1] = b; v[2] = c; v[3] = f; return true; }
+      KDLAE_GEMM_RES2_VARIANTS(X)
+#undef X
+      return false;
+    case 2:
+#define X(a, b, c, o) \
+  if (n++ == i) { v[0] = a; v[1] = b; v[2] = c; v[3] = o; return true; }
+      KDLAE_GEMM_CHUNK2_VARIANTS(X)
+#undef X
+      return false;
+    case 3:
+#define X(a, b, c) \
+  if (n++ == i) { v[0] = a; v[1] = b; v[2] = c; return true; }
+      KDLAE_GEMM_ATTN_IN_VARIANTS(X)
+#undef X
+      return false;
+    default:
+      return false;
+  }
 }
 
 }  // namespace kdlae

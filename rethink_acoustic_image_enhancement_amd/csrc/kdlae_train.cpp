@@ -386,8 +386,70 @@ int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long l
   return KDLAE_OK;
 }
 
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// A 3x3 conv with a narrow side (<= 4 channels: the image heads and the 3- / 4-channel inputs) is a
+// 64-wide GEMM tile that is mostly padding; those run on the inference path's small-channel kernels
+// (conv_small.hip): narrow input -> the MFMA small-input kernel (K = 9 Cin <= 36), narrow output ->
+// the LDS-tiled VALU head kernel.  `wt` selects the transposed-conv (dX) weight view of the same
+// OIHW weight.  Returns 1 when it launched, 0 when the shape is not one of theirs.
+int conv3_narrow(Ctx& c, const float* w, const float* bias, V in, int Cin, int Cout, int Bn, int H, int W, int dil,
+                 V out, const float* R, int ldr, bool transposed, int* done) {
+  *done = 0;
+  if (!R && Cin * 9 <= 36 && Cout % 16 == 0 && out.ld % 4 == 0 && al16(out.p)) {
+    kdlae::SmallInParams p{};
+    p.in = in.p;
+    p.sb = (long long)H * W * in.ld;
+    p.sc = 1;
+    p.sy = (long long)W * in.ld;
+    p.sx = in.ld;
+    p.Cin = Cin;
+    p.Cout = Cout;
+    p.dil = dil;
+    p.w = w;
+    p.wt = transposed ? Cout : 0;
+    p.bias = bias;
+    p.out = out.p;
+    p.ldo = out.ld;
+    p.Bn = Bn;
+    p.H = H;
+    p.W = W;
+    p.F = 1;
+    p.kt = 1;
+    LAUNCH(kdlae::launch_conv_small_in(p, c.s));
+    *done = 1;
+    return KDLAE_OK;
+  }
+  if (Cout <= 4 && Cin % 16 == 0 && Cin <= 256 && dil == 1 && in.ld % 4 == 0 && al16(in.p)) {
+    kdlae::SmallOutParams p{};
+    p.in = in.p;
+    p.ld = in.ld;
+    p.Cin = Cin;
+    p.Cout = Cout;
+    p.w = w;
+    p.wt = transposed ? 1 : 0;
+    p.bias = bias;
+    p.Bn = Bn;
+    p.H = H;
+    p.W = W;
+    p.F = 1;
+    p.ks = 3;
+    p.out = out.p;
+    p.out_nchw = 0;
+    p.ldo = out.ld;
+    p.res_nhwc = R;
+    p.ldr = ldr;
+    LAUNCH(kdlae::launch_conv_small_out(p, c.s));
+    *done = 1;
+  }
+  return KDLAE_OK;
+}
+
 int conv3(Ctx& c, const std::string& n, V x, int Cin, int Cout, int Bn, int H, int W, int dil, V out,
           const float* R = nullptr, int ldr = 0) {
+  int done = 0;
+  TRY(conv3_narrow(c, c.W(n + ".weight"), c.W(n + ".bias"), x, Cin, Cout, Bn, H, W, dil, out, R, ldr, false, &done));
+  if (done) return KDLAE_OK;
   tr::TGemm g;
   g.A = x.p; g.amode = 1; g.lda = x.ld; g.Cg = Cin;
   g.B = c.W(n + ".weight"); g.bmode = 2;
@@ -406,17 +468,32 @@ int conv3(Ctx& c, const std::string& n, V x, int Cin, int Cout, int Bn, int H, i
 int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn, int H, int W, int dil, V dx,
               const float* R = nullptr, int ldr = 0) {
   const long long P = (long long)Bn * H * W;
-  tr::TGemm g;  // dW[co][ci][t] = sum_p dY[p,co] X[p + off_t, ci]
-  g.A = dy.p; g.sam = 1; g.sak = dy.ld;
-  g.B = x.p; g.bmode = 1; g.ldb = x.ld;
-  g.C = c.G(n + ".weight"); g.scm = (long long)Cin * 9; g.scn = 9; g.bC2 = 1;
-  g.nz2 = 9;
-  g.M = Cout; g.N = Cin; g.K = (int)P;
-  g.Bn = Bn; g.H = H; g.W = W; g.dil = dil;
-  g.partial = c.splitk;
-  TRY(gemm(c, g, kSplitCap, n + " dW3"));
+  float* gw = c.G(n + ".weight");
+  if (tr::dw3_small_ok(Cin, Cout) && gw) {
+    // narrow side: per-block [Cout][Cin][9] partials on the VALU (train_small.hip)
+    const int ncols = Cin * Cout * 9;
+    const int nb = tr::dw3_small_blocks(P, Cin, Cout, c.red_cap);
+    float* part = red_take(c, (size_t)nb * ncols);
+    if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+    LAUNCH(tr::launch_dw3_small(dy.p, dy.ld, x.p, x.ld, Cin, Cout, Bn, H, W, dil, part, nb, c.s));
+    TRY(queue_reduce(c, part, nb, ncols, ncols, gw));
+  } else {
+    tr::TGemm g;  // dW[co][ci][t] = sum_p dY[p,co] X[p + off_t, ci]
+    g.A = dy.p; g.sam = 1; g.sak = dy.ld;
+    g.B = x.p; g.bmode = 1; g.ldb = x.ld;
+    g.C = gw; g.scm = (long long)Cin * 9; g.scn = 9; g.bC2 = 1;
+    g.nz2 = 9;
+    g.M = Cout; g.N = Cin; g.K = (int)P;
+    g.Bn = Bn; g.H = H; g.W = W; g.dil = dil;
+    g.partial = c.splitk;
+    TRY(gemm(c, g, kSplitCap, n + " dW3"));
+  }
   TRY(bias_grad(c, dy, Cout, P, c.G(n + ".bias")));
   if (dx.p) {
+    // the transposed conv: Cout -> Cin channels (flipped taps), narrow-side kernels where they apply
+    int done = 0;
+    TRY(conv3_narrow(c, c.W(n + ".weight"), nullptr, dy, Cout, Cin, Bn, H, W, dil, dx, R, ldr, true, &done));
+    if (done) return KDLAE_OK;
     tr::TGemm d;  // transposed conv: flipped taps, channels swapped
     d.A = dy.p; d.amode = 1; d.lda = dy.ld; d.Cg = Cout;
     d.B = c.W(n + ".weight"); d.bmode = 3;

@@ -79,6 +79,8 @@ struct SmallInParams {             // 3x3 (kt=1) or 3x3x3 (kt=3) conv, Cin * 9 *
   int relu;
   const float* in_sub;                 // if set, the conv input is (in - in_sub) (ASDQE diff extractor)
   int vh, vw;                          // valid input extent (zero pad bottom/right beyond it); 0 = H, W
+  int wt;                              // > 0 (kt 1): w is the weight of the conv this one transposes, [Cin][wt][3][3]
+                                       // with wt = this conv's total Cout, taps flipped (a training dX)
 };
 
 struct SmallOutParams {            // 3x3 (ks=3) or pointwise (ks=1) conv with Cout <= 4, Cin % 16 == 0
@@ -89,14 +91,20 @@ struct SmallOutParams {            // 3x3 (ks=3) or pointwise (ks=1) conv with C
   float* out; int out_nchw; int ldo;   // NCHW (ldo unused) or NHWC with pixel stride ldo
   const float* res;                    // NCHW residual (same shape as out) or null
   const float* extra;                  // NCHW [B,1,H,W] copied into channel Cout (NHWC mode) or null
+  int wt;                              // 1 (ks 3): w is the weight of the conv this one transposes,
+                                       // [Cin][Cout][3][3] with flipped taps (a training dX)
+  const float* res_nhwc; int ldr;      // NHWC residual added before the store (NHWC mode; may alias out)
 };
 
 bool gemm_attn_in_variant(int NT, int KG, int nch);
 hipError_t launch_gemm(const GemmParams& p, int NT, int KG, int wpe, int grid_x, hipStream_t s);
+hipError_t launch_gemm_route(const GemmParams& p, int NT, int KG, int wpe, int grid_x, int route, hipStream_t s);
+bool gemm_variant_entry(int family, int i, int* v);
 bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident, int out_mode);
 bool gemm_has_variant2(int NT, int KG, bool conv3, int out_mode);  // r02 chunked kernel
 hipError_t launch_ln_stats(const float* x, int ld, int C, long long P, float* stats, hipStream_t s);
 hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s);
+hipError_t launch_dwconv_gram_route(const GramParams& p, int route, hipStream_t s);  // 2: generic kernel
 hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int heads, int nslots,
                               int slot_floats, hipStream_t s);
 hipError_t launch_attn_fold(const float* reduced, int slot_floats, const float* proj, const float* temp,

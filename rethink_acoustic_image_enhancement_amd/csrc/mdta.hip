@@ -584,8 +584,14 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
   for (int idx = threadIdx.x; idx < 2 * Ch; idx += 64 * NW) out[CT * CT * 256 + idx] = nred[idx];
 }
 
+// generic: the 64-pixel-step kernel whatever the width (self-test route; production takes it only
+// for W % 16 != 0 or a slot count that does not tile the strips)
 template <int CT>
-static void launch_gram_ct(const GramParams& p, hipStream_t s) {
+static void launch_gram_ct(const GramParams& p, bool generic, hipStream_t s) {
+  if (generic) {
+    hipLaunchKernelGGL(dwconv_gram_kernel<CT>, dim3(p.nslots, p.heads, p.Bn), dim3(256), 0, s, p);
+    return;
+  }
   if constexpr (CT <= 6) {
     using R = GramRing<CT>;
     if (p.zeros && p.W % 16 == 0 && p.nslots % (p.W / 16) == 0 && p.ld % 4 == 0 && p.C % 4 == 0 &&
@@ -607,16 +613,19 @@ static void launch_gram_ct(const GramParams& p, hipStream_t s) {
   }
 }
 
-hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s) {
+hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s) { return launch_dwconv_gram_route(p, 0, s); }
+
+hipError_t launch_dwconv_gram_route(const GramParams& p, int route, hipStream_t s) {
+  const bool g = route == 2;
   switch (p.Ch / 16) {
-    case 1: launch_gram_ct<1>(p, s); break;
-    case 2: launch_gram_ct<2>(p, s); break;
-    case 3: launch_gram_ct<3>(p, s); break;
-    case 4: launch_gram_ct<4>(p, s); break;
-    case 5: launch_gram_ct<5>(p, s); break;
-    case 6: launch_gram_ct<6>(p, s); break;
-    case 7: launch_gram_ct<7>(p, s); break;
-    case 8: launch_gram_ct<8>(p, s); break;
+    case 1: launch_gram_ct<1>(p, g, s); break;
+    case 2: launch_gram_ct<2>(p, g, s); break;
+    case 3: launch_gram_ct<3>(p, g, s); break;
+    case 4: launch_gram_ct<4>(p, g, s); break;
+    case 5: launch_gram_ct<5>(p, g, s); break;
+    case 6: launch_gram_ct<6>(p, g, s); break;
+    case 7: launch_gram_ct<7>(p, g, s); break;
+    case 8: launch_gram_ct<8>(p, g, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

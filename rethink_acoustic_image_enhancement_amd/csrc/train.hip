@@ -906,9 +906,9 @@ static inline bool ln2_ok(const void* a, int lda, const void* b, int ldb, int C)
   } while (0)
 
 hipError_t launch_ln_fwd(const float* x, int ldx, const float* w, const float* b, int C, long long P, int biasfree,
-                         float* y, int ldy, float* stats, hipStream_t s) {
+                         float* y, int ldy, float* stats, hipStream_t s, bool generic) {
   if (C > 512) return hipErrorInvalidValue;
-  if (ln2_ok(x, ldx, y, ldy, C) && ((uintptr_t)w & 15) == 0 && (!b || ((uintptr_t)b & 15) == 0)) {
+  if (!generic && ln2_ok(x, ldx, y, ldy, C) && ((uintptr_t)w & 15) == 0 && (!b || ((uintptr_t)b & 15) == 0)) {
     const int ppw = C <= 64 ? 4 : C <= 128 ? 2 : 1;
     LN2_DISPATCH(ln2_fwd_kernel, dim3(grid_for(P, 4 * ppw * 2, 16384)), x, ldx, w, b, C, P, biasfree, y, ldy, stats);
     return hipGetLastError();
@@ -919,9 +919,9 @@ hipError_t launch_ln_fwd(const float* x, int ldx, const float* w, const float* b
 
 hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, const float* w, const float* stats, int C,
                          long long P, int biasfree, const float* R, int ldr, float* dx, int lddx, float* part, int nblk,
-                         hipStream_t s) {
+                         hipStream_t s, bool generic) {
   if (C > 512) return hipErrorInvalidValue;
-  if (ln2_ok(dy, ldd, x, ldx, C) && ln2_ok(dx, lddx, w, 4, C) && (!R || ln2_ok(R, ldr, R, ldr, C))) {
+  if (!generic && ln2_ok(dy, ldd, x, ldx, C) && ln2_ok(dx, lddx, w, 4, C) && (!R || ln2_ok(R, ldr, R, ldr, C))) {
     LN2_DISPATCH(ln2_bwd_kernel, dim3(nblk), dy, ldd, x, ldx, w, stats, C, P, biasfree, R, ldr, dx, lddx, part);
     return hipGetLastError();
   }

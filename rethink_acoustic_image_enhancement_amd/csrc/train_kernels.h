@@ -57,14 +57,15 @@ hipError_t launch_tgemm_cols(TGemm g, size_t partial_cap, hipStream_t s);
 hipError_t launch_tgemm_reduce(const TGemm& g, hipStream_t s);
 
 // LayerNorm over channels per pixel (KDLAE_model.py:50-52 BiasFree, :67-70 WithBias), eps 1e-5.
-// forward: y = LN(x) * w (+ b); stats[p] = (mean, rstd)
+// forward: y = LN(x) * w (+ b); stats[p] = (mean, rstd).  generic (self-test): the one-wave-per-pixel
+// kernels the lane-group ones fall back to for misaligned views / C % 4 != 0
 hipError_t launch_ln_fwd(const float* x, int ldx, const float* w, const float* b, int C, long long P, int biasfree,
-                         float* y, int ldy, float* stats, hipStream_t s);
+                         float* y, int ldy, float* stats, hipStream_t s, bool generic = false);
 // backward: dx = R + dLN(dy) (R may be null or alias dx); per-block partial dw [nblk][C], db [nblk][C]
 // reduced into gw / gb by the caller's column reduce.  Returns the number of blocks used in *nblk.
 hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, const float* w, const float* stats,
                          int C, long long P, int biasfree, const float* R, int ldr, float* dx, int lddx,
-                         float* part, int nblk, hipStream_t s);
+                         float* part, int nblk, hipStream_t s, bool generic = false);
 
 // depthwise 3x3 (padding 1) over NHWC: out[p,c] = sum_t w[c][t] in[p+off_t, c] (+ b[c]); flip=1 uses
 // w[c][8-t] (dX of the same conv).
@@ -82,6 +83,13 @@ hipError_t launch_dwgate_bwd(const float* dg, int ldg, const float* yd, int ldyd
                              hipStream_t s);
 hipError_t launch_dw_bwd(const float* dyd, int ldd, const float* yin, int ldi, const float* w, int C, int Bn, int H,
                          int W, float* dy, int lddy, float* part, hipStream_t s);
+
+// 3x3 conv weight gradient with a side of <= 4 channels (train_small.hip): part[nblk][Cout * Cin * 9]
+// (OIHW order) partials of dW = sum_p dY[p] (x) X[p + off_t], summed by the caller's column reduce
+bool dw3_small_ok(int Cin, int Cout);
+int dw3_small_blocks(long long P, int Cin, int Cout, size_t part_cap);
+hipError_t launch_dw3_small(const float* dy, int ldd, const float* x, int ldx, int Cin, int Cout, int Bn, int H, int W,
+                            int dil, float* part, int nblk, hipStream_t s);
 
 // column reductions: out[seg][c] = sum over rows of segment seg of f(x[r][c]); f = x or x^2.
 // Two passes (partials then a fixed-order reduce), deterministic.
