@@ -124,6 +124,8 @@ def _gemm_case(NT, KG, c3, out_mode, route, group_tiles=0, ntiles=None, with_r=F
         Cin = 16 * cg
     else:
         kgroups = KG if (group_tiles or attn_in) else KG * kchunks - 1   # ragged last k-chunk
+        if ln and not (group_tiles or attn_in):
+            kgroups = min(kgroups, 32)   # row statistics (ln_stats_kernel) cover C <= 512
         Cin = 16 * kgroups
     K = 16 * kgroups
     if ntiles is None:
