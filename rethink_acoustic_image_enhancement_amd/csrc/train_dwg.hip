@@ -33,7 +33,14 @@ namespace {
 #ifndef KDLAE_DWG_TY
 #define KDLAE_DWG_TY 16
 #endif
+#ifndef KDLAE_DWG_PF
+#define KDLAE_DWG_PF 1
+#endif
 constexpr int kU = KDLAE_DWG_U;  // columns per thread
+// rows are loaded one row ahead of their use, so the next row's loads overlap this row's arithmetic
+// (r03 A/B at 6 x 128^2: qkv dwconv backward 3.32 -> 2.41 ms per step, GDFN forward 3.95 -> 3.74,
+// the VALU-bound GDFN backward 5.06 -> 4.98; 99.5 -> 101.2 img/s)
+constexpr bool kPF = KDLAE_DWG_PF != 0;
 constexpr int kTX = 4 * kU;   // columns per block
 // rows per block: 16, or 8 / 4 on the small levels so the grid still has >= 256 spatial blocks (the
 // 16^2 latent: 6 blocks per channel group at 16 rows, 0.7-1.0 TB/s)
@@ -113,9 +120,24 @@ __global__ __launch_bounds__(256) void dwgate_fwd_kernel(const float* __restrict
   load_row(y, ldi, o, H, W, o.y0, c, a[1]);
   load_row(y, ldi, o, H, W, o.y0 - 1, hid + c, v[0]);
   load_row(y, ldi, o, H, W, o.y0, hid + c, v[1]);
+  [[maybe_unused]] float an[kU + 2], vn[kU + 2];  // kPF: the row after next, in flight during this row
+  if constexpr (kPF) {
+    load_row(y, ldi, o, H, W, o.y0 + 1, c, an);
+    load_row(y, ldi, o, H, W, o.y0 + 1, hid + c, vn);
+  }
   for (int yy = o.y0; yy < o.y1; ++yy) {
-    load_row(y, ldi, o, H, W, yy + 1, c, a[2]);
-    load_row(y, ldi, o, H, W, yy + 1, hid + c, v[2]);
+    if constexpr (kPF) {
+#pragma unroll
+      for (int j = 0; j < kU + 2; ++j) {
+        a[2][j] = an[j];
+        v[2][j] = vn[j];
+      }
+      load_row(y, ldi, o, H, W, yy + 2, c, an);
+      load_row(y, ldi, o, H, W, yy + 2, hid + c, vn);
+    } else {
+      load_row(y, ldi, o, H, W, yy + 1, c, a[2]);
+      load_row(y, ldi, o, H, W, yy + 1, hid + c, v[2]);
+    }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       float s1 = b1, s2 = b2;
@@ -167,37 +189,52 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
 #pragma unroll
     for (int t = 0; t < 10; ++t) acc[h][t] = 0.f;
   float d[NH][3][kU + 2], x[NH][3][kU + 2];
-  // dyd of row yy for both halves: gate backward of (dg, yd1, yd2), or the given gradient
-  auto row_d = [&](int yy, float (&d0)[kU + 2], float (&d1)[kU + 2]) {
+  // raw inputs of one row (GATE: dg, yd1, yd2; else dyd in r1) and the layer input rows
+  float rg[GATE ? kU + 2 : 1], r1[kU + 2], r2[GATE ? kU + 2 : 1], rx[NH][kU + 2];
+  auto load_raw = [&](int yy) {
     if constexpr (GATE) {
-      float gg[kU + 2], y1[kU + 2], y2[kU + 2];
-      load_row(dg, ldg, o, H, W, yy, c, gg);
-      load_row(yd, ldyd, o, H, W, yy, c, y1);
-      load_row(yd, ldyd, o, H, W, yy, hid + c, y2);
+      load_row(dg, ldg, o, H, W, yy, c, rg);
+      load_row(yd, ldyd, o, H, W, yy, hid + c, r2);
+    }
+    load_row(yd, ldyd, o, H, W, yy, c, r1);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) load_row(yin, ldi, o, H, W, yy, h * hid + c, rx[h]);
+  };
+  // dyd of the raw row for both halves: gate backward of (dg, yd1, yd2), or the given gradient
+  auto row_d = [&](float (&d0)[kU + 2], float (&d1)[kU + 2]) {
+    if constexpr (GATE) {
 #pragma unroll
       for (int j = 0; j < kU + 2; ++j) {
         float ex;
-        const float cdf = 0.5f * (1.f + erf_half(y1[j], ex));
+        const float cdf = 0.5f * (1.f + erf_half(r1[j], ex));
         const float pdf = 0.39894228040143268f * ex;
-        d0[j] = gg[j] * y2[j] * (cdf + y1[j] * pdf);
-        d1[j] = gg[j] * y1[j] * cdf;
+        d0[j] = rg[j] * r2[j] * (cdf + r1[j] * pdf);
+        d1[j] = rg[j] * r1[j] * cdf;
       }
     } else {
-      load_row(yd, ldyd, o, H, W, yy, c, d0);
+#pragma unroll
+      for (int j = 0; j < kU + 2; ++j) d0[j] = r1[j];
       (void)d1;
     }
   };
-  row_d(o.y0 - 1, d[0][0], d[NH - 1][0]);
-  row_d(o.y0, d[0][1], d[NH - 1][1]);
+  auto take_x = [&](int slot) {
 #pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    load_row(yin, ldi, o, H, W, o.y0 - 1, h * hid + c, x[h][0]);
-    load_row(yin, ldi, o, H, W, o.y0, h * hid + c, x[h][1]);
-  }
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int j = 0; j < kU + 2; ++j) x[h][slot][j] = rx[h][j];
+  };
+  load_raw(o.y0 - 1);
+  row_d(d[0][0], d[NH - 1][0]);
+  take_x(0);
+  load_raw(o.y0);
+  row_d(d[0][1], d[NH - 1][1]);
+  take_x(1);
+  if constexpr (kPF) load_raw(o.y0 + 1);  // kPF: row yy + 1's loads are in flight during row yy - 1
   for (int yy = o.y0; yy < o.y1; ++yy) {
-    row_d(yy + 1, d[0][2], d[NH - 1][2]);
-#pragma unroll
-    for (int h = 0; h < NH; ++h) load_row(yin, ldi, o, H, W, yy + 1, h * hid + c, x[h][2]);
+    if constexpr (!kPF) load_raw(yy + 1);
+    row_d(d[0][2], d[NH - 1][2]);
+    take_x(2);
+    if constexpr (kPF) load_raw(yy + 2);
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int xx = o.x0 + u;
