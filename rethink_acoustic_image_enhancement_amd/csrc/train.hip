@@ -544,8 +544,11 @@ hipError_t launch_tgemm_tiled(TGemm g, size_t partial_cap, hipStream_t s) {
   int splits = 1;
   // implicit-GEMM convolutions (amode 1) split only when their tiles leave the chip mostly idle:
   // r03 trace, splitting the 384-768-tile shapes as well was 20-110% slower (the partial round trip
-  // outweighs the fuller grid), the 72-144-tile Upsample convs 18-71% faster
-  const bool split_ok = g.amode != 1 || (long long)tiles * batch < 256;
+  // outweighs the fuller grid), the 72-144-tile Upsample convs 18-71% faster; of the 288-tile
+  // shapes, the K = 3456 ones gain (16^2 / 32^2 Upsample fwd / dX 427 -> 318, 330 -> 205 us) and the
+  // K = 864 ones lose 10-20% (r03 A/B, gpurun_out/ab_sp)
+  const long long ctiles = (long long)tiles * batch;
+  const bool split_ok = g.amode != 1 || ctiles < 256 || (ctiles < 512 && g.K >= 1728);
   if (g.partial && partial_cap > 0 && split_ok) {
     // fill ~KDLAE_SPLITK_BLOCKS blocks, each split at least KDLAE_SPLITK_MIN deep
     const long long blocks = tiles * batch;
