@@ -1139,6 +1139,47 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x
     part[((long long)seg * nblk + blockIdx.y) * ncols + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// float4 form (ncols, ldx % 4 == 0, 16-byte aligned x): lane = (row sub-index lane >> 4, channel quad
+// lane & 15), so a wave reads 4 rows x 64 channels per step; rows r0 + 16 i + 4 wv + (lane >> 4).
+// Fixed order: per lane in row order, then the 4 row sub-indices, then the 4 waves.
+__global__ __launch_bounds__(256) void colsum4_kernel(const float* __restrict__ x, int ldx, int ncols,
+                                                      long long rows_per_seg, int square, float* __restrict__ part) {
+  __shared__ f32x4 red[4][16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, rsub = lane >> 4;
+  const int c = blockIdx.x * 64 + 4 * (lane & 15), seg = blockIdx.z, nblk = gridDim.y;
+  const long long per = (rows_per_seg + nblk - 1) / nblk;
+  const long long r0 = blockIdx.y * per, r1 = min(rows_per_seg, r0 + per);
+  const float* xs = x + (long long)seg * rows_per_seg * ldx;
+  f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  if (c < ncols) {
+    long long r = r0 + 4 * wv + rsub;
+    for (; r + 16 < r1; r += 32) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(xs + r * ldx + c);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(xs + (r + 16) * ldx + c);
+      a0 += square ? v0 * v0 : v0;
+      a1 += square ? v1 * v1 : v1;
+    }
+    for (; r < r1; r += 16) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xs + r * ldx + c);
+      a0 += square ? v * v : v;
+    }
+  }
+  f32x4 a = a0 + a1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] += __shfl_xor(a[e], 16);
+    a[e] += __shfl_xor(a[e], 32);
+  }
+  if (rsub == 0) red[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0 && lane < 16 && c < ncols) {
+    const f32x4 t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    float* o = part + ((long long)seg * nblk + blockIdx.y) * ncols + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = t[e];
+  }
+}
+
 __global__ __launch_bounds__(1024) void part_reduce_kernel(const float* __restrict__ part, int nblk, int ncols,
                                                            int pstride, int nseg, float* out, int accumulate,
                                                            float scale) {
@@ -1222,6 +1263,14 @@ hipError_t launch_part_reduce_multi(const RedDesc* d, int n, hipStream_t s) {
 
 hipError_t launch_colsum(const float* x, int ldx, int ncols, long long rows_per_seg, int nseg, int square, float* part,
                          int nblk, hipStream_t s) {
+#ifndef KDLAE_COLSUM4
+#define KDLAE_COLSUM4 1
+#endif
+  if (KDLAE_COLSUM4 && ncols % 4 == 0 && ldx % 4 == 0 && al16(x)) {
+    hipLaunchKernelGGL(colsum4_kernel, dim3((ncols + 63) / 64, nblk, nseg), dim3(256), 0, s, x, ldx, ncols,
+                       rows_per_seg, square, part);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(colsum_kernel, dim3((ncols + 63) / 64, nblk, nseg), dim3(256), 0, s, x, ldx, ncols,
                      rows_per_seg, square, part);
   return hipGetLastError();
