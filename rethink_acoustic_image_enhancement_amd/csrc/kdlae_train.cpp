@@ -573,8 +573,7 @@ int block_fwd(Ctx& c, BlockRec& r) {
     // row stride hid is not a multiple of 4 floats: a zero-padded [C][ld4(hid)] copy lets the forward
     // and dX GEMMs use the vectorised kernel (kept until the backward: theta is unchanged in between)
     r.wpo = c.alloc((size_t)C * L1);
-    LAUNCH(hipMemsetAsync(r.wpo, 0, (size_t)C * L1 * sizeof(float), c.s));
-    LAUNCH(tr::launch_copy_cols(c.W(p + ".ffn.project_out.weight"), hid, r.wpo, L1, hid, C, 0, c.s));
+    LAUNCH(tr::launch_copy_cols(c.W(p + ".ffn.project_out.weight"), hid, r.wpo, L1, hid, C, 0, c.s, L1));
   }
   TRY(conv1(c, p + ".ffn.project_out", {r.g, L1}, hid, C, P, {r.out, C}, r.x1, C, {r.wpo, L1}));
   return KDLAE_OK;

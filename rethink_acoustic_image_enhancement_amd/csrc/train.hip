@@ -1417,15 +1417,30 @@ __global__ void shuffle_kernel(const float* __restrict__ in, int ldi, float* __r
   }
 }
 
-__global__ void copy_cols_kernel(const float* __restrict__ in, int ldi, float* out, int ldo, int C, long long P,
-                                 int accumulate) {
-  const long long total = P * C;
+// out[p, 0:C] (= or +=) in[p, 0:C], and out[p, C:Wd] = 0 (Wd > C: a zero-padded copy).  32-bit
+// index math when the element count allows it (a 64-bit division per element was most of the cost)
+__global__ void copy_cols_kernel(const float* __restrict__ in, int ldi, float* out, int ldo, int C, int Wd,
+                                 long long P, int accumulate) {
+  const long long total = P * Wd;
+  const bool narrow = total < (1LL << 32);
   for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
-    const long long p = idx / C;
-    const int c = (int)(idx - p * C);
-    const float v = in[p * ldi + c];
-    out[p * ldo + c] = accumulate ? out[p * ldo + c] + v : v;
+    long long p;
+    int c;
+    if (narrow) {
+      const unsigned u = (unsigned)idx, pu = u / (unsigned)Wd;
+      p = pu;
+      c = (int)(u - pu * (unsigned)Wd);
+    } else {
+      p = idx / Wd;
+      c = (int)(idx - p * Wd);
+    }
+    if (c < C) {
+      const float v = in[p * ldi + c];
+      out[p * ldo + c] = accumulate ? out[p * ldo + c] + v : v;
+    } else {
+      out[p * ldo + c] = 0.f;
+    }
   }
 }
 
@@ -1464,9 +1479,10 @@ hipError_t launch_shuffle(const float* in, int ldi, float* out, int ldo, int C, 
 }
 
 hipError_t launch_copy_cols(const float* in, int ldi, float* out, int ldo, int C, long long P, int accumulate,
-                            hipStream_t s) {
-  hipLaunchKernelGGL(copy_cols_kernel, dim3(grid_for(P * C, 256, 65536)), dim3(256), 0, s, in, ldi, out, ldo, C, P,
-                     accumulate);
+                            hipStream_t s, int zero_to) {
+  const int Wd = zero_to > C ? zero_to : C;
+  hipLaunchKernelGGL(copy_cols_kernel, dim3(grid_for(P * Wd, 256, 65536)), dim3(256), 0, s, in, ldi, out, ldo, C, Wd,
+                     P, accumulate);
   return hipGetLastError();
 }
 

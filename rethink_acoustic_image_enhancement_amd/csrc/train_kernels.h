@@ -128,9 +128,9 @@ hipError_t launch_attn_bwd(const float* G, const float* sumsq, const float* temp
 // h, w are the low-resolution sizes, C the low-channel count.
 hipError_t launch_shuffle(const float* in, int ldi, float* out, int ldo, int C, int Bn, int h, int w, int dir,
                           hipStream_t s);
-// out[p, 0:C] (= or +=) in[p, 0:C]
+// out[p, 0:C] (= or +=) in[p, 0:C]; zero_to > C also zeroes out[p, C:zero_to] (a padded copy)
 hipError_t launch_copy_cols(const float* in, int ldi, float* out, int ldo, int C, long long P, int accumulate,
-                            hipStream_t s);
+                            hipStream_t s, int zero_to = 0);
 // NCHW [B,C,H,W] -> NHWC view (out[p*ldo + c]); accumulate adds
 hipError_t launch_nchw_to_nhwc(const float* in, int C, int Bn, long long HW, float* out, int ldo, int accumulate,
                                hipStream_t s);
