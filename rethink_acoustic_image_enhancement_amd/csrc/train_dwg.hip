@@ -167,6 +167,13 @@ __global__ __launch_bounds__(256) void dwgate_fwd_kernel(const float* __restrict
 }
 
 // GATE: two halves, dyd from (dg, yd); else one tensor of C = `hid` channels, dyd read as given.
+// GATE carries the two halves of a channel as one float2 (x: first half, y: second half) so the
+// transposed conv and the weight-gradient FMAs issue as packed v_pk_fma_f32 (two per instruction;
+// the fused GDFN backward is VALU-bound).
+typedef float f2 __attribute__((ext_vector_type(2)));
+template <bool GATE> struct DwType { using T = float; };
+template <> struct DwType<true> { using T = f2; };
+
 template <bool GATE>
 __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ dg, int ldg,
                                                      const float* __restrict__ yd, int ldyd,
@@ -174,21 +181,27 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
                                                      const float* __restrict__ w, int hid, int H, int W, int tiles_x,
                                                      int ty, float* __restrict__ dy, int lddy,
                                                      float* __restrict__ part) {
+  using T = typename DwType<GATE>::T;
   constexpr int NH = GATE ? 2 : 1;
   __shared__ float red[4][64][10 * NH];
   const Geo o = geo(hid, H, W, tiles_x, ty);
   const int c = o.c;
-  float wf[NH][9];  // flipped taps (the transposed conv)
+  auto comp = [](const T& v, int h) -> float {
+    if constexpr (GATE) return h ? v.y : v.x;
+    else return v;
+  };
+  auto pack = [](float a, float b) -> T {
+    if constexpr (GATE) return f2{a, b};
+    else return a;
+  };
+  T wf[9];  // flipped taps (the transposed conv)
 #pragma unroll
-  for (int h = 0; h < NH; ++h)
+  for (int t = 0; t < 9; ++t)
+    wf[t] = pack(o.live ? w[c * 9 + 8 - t] : 0.f, (GATE && o.live) ? w[(hid + c) * 9 + 8 - t] : 0.f);
+  T acc[10];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wf[h][t] = o.live ? w[(h * hid + c) * 9 + 8 - t] : 0.f;
-  float acc[NH][10];
-#pragma unroll
-  for (int h = 0; h < NH; ++h)
-#pragma unroll
-    for (int t = 0; t < 10; ++t) acc[h][t] = 0.f;
-  float d[NH][3][kU + 2], x[NH][3][kU + 2];
+  for (int t = 0; t < 10; ++t) acc[t] = pack(0.f, 0.f);
+  T d[3][kU + 2], x[3][kU + 2];
   // raw inputs of one row (GATE: dg, yd1, yd2; else dyd in r1) and the layer input rows
   float rg[GATE ? kU + 2 : 1], r1[kU + 2], r2[GATE ? kU + 2 : 1], rx[NH][kU + 2];
   auto load_raw = [&](int yy) {
@@ -201,75 +214,69 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
     for (int h = 0; h < NH; ++h) load_row(yin, ldi, o, H, W, yy, h * hid + c, rx[h]);
   };
   // dyd of the raw row for both halves: gate backward of (dg, yd1, yd2), or the given gradient
-  auto row_d = [&](float (&d0)[kU + 2], float (&d1)[kU + 2]) {
-    if constexpr (GATE) {
+  auto row_d = [&](T (&dd)[kU + 2]) {
 #pragma unroll
-      for (int j = 0; j < kU + 2; ++j) {
+    for (int j = 0; j < kU + 2; ++j) {
+      if constexpr (GATE) {
         float ex;
         const float cdf = 0.5f * (1.f + erf_half(r1[j], ex));
         const float pdf = 0.39894228040143268f * ex;
-        d0[j] = rg[j] * r2[j] * (cdf + r1[j] * pdf);
-        d1[j] = rg[j] * r1[j] * cdf;
+        dd[j] = pack(rg[j] * r2[j] * (cdf + r1[j] * pdf), rg[j] * r1[j] * cdf);
+      } else {
+        dd[j] = r1[j];
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < kU + 2; ++j) d0[j] = r1[j];
-      (void)d1;
     }
   };
   auto take_x = [&](int slot) {
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
-#pragma unroll
-      for (int j = 0; j < kU + 2; ++j) x[h][slot][j] = rx[h][j];
+    for (int j = 0; j < kU + 2; ++j) x[slot][j] = pack(rx[0][j], rx[NH - 1][j]);
   };
   load_raw(o.y0 - 1);
-  row_d(d[0][0], d[NH - 1][0]);
+  row_d(d[0]);
   take_x(0);
   load_raw(o.y0);
-  row_d(d[0][1], d[NH - 1][1]);
+  row_d(d[1]);
   take_x(1);
   if constexpr (kPF) load_raw(o.y0 + 1);  // kPF: row yy + 1's loads are in flight during row yy - 1
   for (int yy = o.y0; yy < o.y1; ++yy) {
     if constexpr (!kPF) load_raw(yy + 1);
-    row_d(d[0][2], d[NH - 1][2]);
+    row_d(d[2]);
     take_x(2);
     if constexpr (kPF) load_raw(yy + 2);
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int xx = o.x0 + u;
+      T s = pack(0.f, 0.f);
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        float s = 0.f;
+      for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-        for (int ty = 0; ty < 3; ++ty)
+        for (int tx = 0; tx < 3; ++tx) s += wf[ty * 3 + tx] * d[ty][u + tx];
+      if (o.live && xx < W) {
+        float* dst = dy + (o.img0 + (long long)yy * W + xx) * lddy + c;
 #pragma unroll
-          for (int tx = 0; tx < 3; ++tx) s += wf[h][ty * 3 + tx] * d[h][ty][u + tx];
-        if (o.live && xx < W) dy[(o.img0 + (long long)yy * W + xx) * lddy + h * hid + c] = s;
-        // weight / bias gradient: centre dyd times the input at each tap (zero past the image)
-        const float dc = d[h][1][u + 1];
-#pragma unroll
-        for (int ty = 0; ty < 3; ++ty)
-#pragma unroll
-          for (int tx = 0; tx < 3; ++tx) acc[h][ty * 3 + tx] += dc * x[h][ty][u + tx];
-        acc[h][9] += dc;
+        for (int h = 0; h < NH; ++h) dst[h * hid] = comp(s, h);
       }
+      // weight / bias gradient: centre dyd times the input at each tap (zero past the image)
+      const T dc = d[1][u + 1];
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) acc[ty * 3 + tx] += dc * x[ty][u + tx];
+      acc[9] += dc;
     }
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
-#pragma unroll
-      for (int j = 0; j < kU + 2; ++j) {
-        d[h][0][j] = d[h][1][j];
-        d[h][1][j] = d[h][2][j];
-        x[h][0][j] = x[h][1][j];
-        x[h][1][j] = x[h][2][j];
-      }
+    for (int j = 0; j < kU + 2; ++j) {
+      d[0][j] = d[1][j];
+      d[1][j] = d[2][j];
+      x[0][j] = x[1][j];
+      x[1][j] = x[2][j];
+    }
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int h = 0; h < NH; ++h)
 #pragma unroll
-    for (int t = 0; t < 10; ++t) red[wv][lane][h * 10 + t] = acc[h][t];
+    for (int t = 0; t < 10; ++t) red[wv][lane][h * 10 + t] = comp(acc[t], h);
   __syncthreads();
   if (wv != 0 || !o.live) return;
   const int Ctot = NH * hid;
