@@ -24,6 +24,13 @@
  * LN + ffn.project_in GEMM separate for C = 48 blocks; "attn_in_split" fuses
  * the C = 96 blocks' first project_in weight group as well.  KDLAE_PROBE_DUMP
  * names a CSV file kdlae_t_probe_read writes per-launch timings to.
+ * One more KDLAE_DEBUG flag is read on EVERY training call (kdlae_tt_forward /
+ * kdlae_tt_backward / kdlae_tt_backward_marked), not at pack time:
+ * "train_trace" brackets each training launch with a pair of HIP events and
+ * synchronises the stream at the end of the call to dump them to
+ * KDLAE_PROBE_DUMP.  It does not change results, but the synchronisation
+ * removes the overlap of the bucketed all-reduce with the backward that the
+ * gradient-ready marks exist for: diagnostics only, never in production.
  */
 #ifndef KDLAE_H_
 #define KDLAE_H_
@@ -115,6 +122,16 @@ int kdlae_t_forward(kdlae_t_handle* h, const float* img, const float* rate, int 
  * count equals it.  */
 int kdlae_t_probe_arm(kdlae_t_handle* h, int kernel_class, int level_filter);
 int kdlae_t_probe_read(kdlae_t_handle* h, double* ms, int64_t* launches, double* bytes, double* flops);
+
+/* Diagnostics (tools/config1_taps.py; not part of the drop-in boundary): the outputs of every
+ * TransformerBlock in execution order.  kdlae_t_debug_tap_info names tap i (its state_dict prefix,
+ * e.g. "latent.3"), its channel count C and its resolution relative to the forward's input, H * num /
+ * den.  While kdlae_t_debug_taps(h, n, dst) is armed (n = 0 disarms), every kdlae_t_forward copies
+ * block i's output (i < n, dst[i] != NULL) into the device buffer dst[i] as compact NHWC
+ * [B][H_i][W_i][C] on the forward's stream.  Results are unchanged. */
+int kdlae_t_debug_tap_count(const kdlae_t_handle* h);
+int kdlae_t_debug_tap_info(const kdlae_t_handle* h, int i, char* name, int name_len, int* C, int* num, int* den);
+int kdlae_t_debug_taps(kdlae_t_handle* h, int n, float* const* dst);
 
 /* ------------------------------------------------------------------ KDLAE-S
  * Ctor kwargs of KDLAE_student (KDLAE/KDLAE_model.py:340-384): a 3-D U-Net over a burst of frames.

@@ -321,7 +321,9 @@ class KDLAE_teacher(nn.Module):
         stream = torch.cuda.current_stream(dev)
         eng = self.engine(dev)
         # a graph bakes in every pointer: parameter storages, the flat pack buffer, the workspace
-        key = (dev.index, B, H, W, stream.cuda_stream, tuple(p.data_ptr() for p in self.parameters()))
+        # (the same tensor list _Engine._sources packs: parameters and buffers)
+        key = (dev.index, B, H, W, stream.cuda_stream,
+               tuple(t.data_ptr() for t in list(self.parameters()) + list(self.buffers())))
         cache = self.__dict__.setdefault("_graphs", {})
         seen = self.__dict__.setdefault("_graph_seen", {})
         ent = cache.pop(key, None)
@@ -338,7 +340,9 @@ class KDLAE_teacher(nn.Module):
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(dev)
             try:
-                with torch.cuda.graph(g):
+                # thread_local: HIP calls other threads of the process make meanwhile (a DataLoader's
+                # pin_memory thread, an async checkpoint copy) are not captured and do not fail
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     s_out = self._forward_eager(s_img, s_rate)
             except RuntimeError:
                 seen[key] = 2  # this shape stays eager
@@ -454,8 +458,15 @@ class KDLAE_student(nn.Module):
         if H % m or W % m:
             raise RuntimeError(f"KDLAE_student needs H and W divisible by {m}, got {H}x{W}")
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            if self.training:
+                # BasicSR trains KDLAE_student (KDLAES.yml) with l_pix.backward(): a graph-less output
+                # would fail there, or silently train nothing
+                raise NotImplementedError(
+                    "KDLAE_student (MI355X build): the HIP path has no backward yet; wrap inference in "
+                    "torch.no_grad() or call .eval()")
             if not self._warned_grad:
-                warnings.warn("KDLAE_student HIP forward is inference-only: outputs carry no autograd graph")
+                warnings.warn("KDLAE_student in eval mode with grad enabled: the HIP inference path returns "
+                              "outputs without an autograd graph")
                 self._warned_grad = True
         dev = x.device
         stream = torch.cuda.current_stream(dev).cuda_stream

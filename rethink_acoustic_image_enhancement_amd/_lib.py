@@ -26,6 +26,7 @@ EXPORTS = (
     "kdlae_t_set_param", "kdlae_t_commit_params", "kdlae_t_params_numel", "kdlae_t_prepare", "kdlae_t_pack_device",
     "kdlae_t_workspace_bytes", "kdlae_t_forward",
     "kdlae_t_probe_arm", "kdlae_t_probe_read",
+    "kdlae_t_debug_tap_count", "kdlae_t_debug_tap_info", "kdlae_t_debug_taps",
     "kdlae_s_create", "kdlae_s_destroy", "kdlae_s_num_params", "kdlae_s_param_info",
     "kdlae_s_set_param", "kdlae_s_commit_params", "kdlae_s_params_numel", "kdlae_s_prepare", "kdlae_s_pack_device",
     "kdlae_s_workspace_bytes", "kdlae_s_forward",
@@ -105,6 +106,10 @@ def lib() -> ctypes.CDLL:
     L.kdlae_t_probe_arm.argtypes = [c_void_p, c_int, c_int]
     L.kdlae_t_probe_read.argtypes = [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int64),
                                      ctypes.POINTER(c_double), ctypes.POINTER(c_double)]
+    L.kdlae_t_debug_tap_count.argtypes = [c_void_p]
+    L.kdlae_t_debug_tap_info.argtypes = [c_void_p, c_int, c_char_p, c_int, ctypes.POINTER(c_int),
+                                         ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
+    L.kdlae_t_debug_taps.argtypes = [c_void_p, c_int, ctypes.POINTER(c_void_p)]
     L.kdlae_s_create.argtypes = [ctypes.POINTER(SConfig), c_int, ctypes.POINTER(c_void_p)]
     L.kdlae_s_destroy.argtypes = [c_void_p]
     L.kdlae_s_num_params.argtypes = [c_void_p]

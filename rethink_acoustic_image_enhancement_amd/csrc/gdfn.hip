@@ -75,6 +75,9 @@ template <int TH> struct GdTile {
 // (|error| <= 1.5e-7): branch-free, so the gate VALU stays in one basic block with the MFMAs it is
 // interleaved with.  The GELU error is <= 7.5e-8 |x|, at the level of fp32 rounding of the result.
 __device__ __forceinline__ float gelu_erf_g(float x) {
+#ifdef KDLAE_PRECISE_GELU  // diagnostics build (tools/config1_taps.py): the device library's erff
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+#endif
   const float z = fabsf(x) * 0.70710678118654752f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
   float poly = fmaf(1.061405429f, t, -1.453152027f);
@@ -92,6 +95,9 @@ __device__ __forceinline__ float gelu_erf_g(float x) {
 // C48 -1%, C192 +1.5% per launch, so the wide (NT = 12) kernel keeps the scalar form.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_gate2(f32x2 x, f32x2 v) {
+#ifdef KDLAE_PRECISE_GELU
+  return f32x2{gelu_erf_g(x.x) * v.x, gelu_erf_g(x.y) * v.y};
+#endif
   const f32x2 z = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
   const f32x2 a = __builtin_elementwise_fma(f32x2{0.3275911f, 0.3275911f}, z, f32x2{1.0f, 1.0f});
   const f32x2 t = f32x2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)};

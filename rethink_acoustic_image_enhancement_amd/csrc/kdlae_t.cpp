@@ -62,6 +62,9 @@ struct kdlae_t_handle {
   long long probe_launches = 0;
   struct ProbeRec { std::string tag; double bytes, flops; };
   std::vector<ProbeRec> probe_recs;
+  // diagnostics (kdlae_t_debug_taps): per TransformerBlock in execution order, a device buffer that
+  // receives the block's output as compact NHWC [B][H_i][W_i][C_i] (nullptr: not tapped)
+  std::vector<float*> taps;
 
   const float* P(size_t off) const { return dw.P(off); }
 };
@@ -652,10 +655,17 @@ struct Fwd {
     return gemm(b.pout, h->P(b.pout.w), 0, View{buf(pl.fg), b.hidS}, Hh, Ww, x, 0, x.p, x.ld, 0, 0, b.C);
   }
 
+  size_t tap_i = 0;  // TransformerBlocks run so far in this forward (kdlae_t_debug_taps)
   int stage(const std::vector<BlockW>& st, View x, int Hh, int Ww) {
     for (const BlockW& b : st) {
       int rc = block(b, x, Hh, Ww);
       if (rc) return rc;
+      const size_t i = tap_i++;
+      if (i < h->taps.size() && h->taps[i]) {
+        const size_t P = (size_t)B * Hh * Ww;
+        HIPCHK(hipMemcpy2DAsync(h->taps[i], (size_t)b.C * 4, x.p, (size_t)x.ld * 4, (size_t)b.C * 4, P,
+                                hipMemcpyDeviceToDevice, s));
+      }
     }
     return KDLAE_OK;
   }
@@ -921,6 +931,49 @@ int kdlae_t_forward(kdlae_t_handle* h, const float* img, const float* rate, int 
   if ((int64_t)f.pl.total > workspace_bytes) return fail(KDLAE_ESTATE, "workspace too small");
   DeviceGuard g(h->device);
   return f.run(img, rate, H, W, hq, sr);
+}
+
+// TransformerBlocks in the order kdlae_t_forward runs them: (state_dict prefix, channels, resolution
+// relative to the input as num / den)
+struct TapInfo { std::string name; int C, num, den; };
+static std::vector<TapInfo> tap_list(const kdlae_t_handle* h) {
+  const kdlae_t_config& c = h->cfg;
+  const int d = c.dim, nr = c.num_refinement_blocks;
+  std::vector<TapInfo> v;
+  auto add = [&](const char* n, int cnt, int C, int num, int den) {
+    for (int i = 0; i < cnt; ++i) v.push_back({std::string(n) + "." + std::to_string(i), C, num, den});
+  };
+  add("encoder_level1", c.num_blocks[0], d, 1, 1);
+  add("encoder_level2", c.num_blocks[1], 2 * d, 1, 2);
+  add("encoder_level3", c.num_blocks[2], 4 * d, 1, 4);
+  add("latent", c.num_blocks[3], 8 * d, 1, 8);
+  add("decoder_level3", c.num_blocks[2], 4 * d, 1, 4);
+  add("decoder_level2", c.num_blocks[1], 2 * d, 1, 2);
+  add("decoder_level1", c.num_blocks[0], 2 * d, 1, 1);
+  add("refinement", nr, 2 * d, 1, 1);
+  if (c.params_cat) add("refinement_out", nr, 2 * d, 1, 1);
+  if (c.static_train) add("enhance", nr, d, 2, 1);
+  return v;
+}
+
+int kdlae_t_debug_tap_count(const kdlae_t_handle* h) { return h ? (int)tap_list(h).size() : -1; }
+
+int kdlae_t_debug_tap_info(const kdlae_t_handle* h, int i, char* name, int name_len, int* C, int* num, int* den) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  const std::vector<TapInfo> v = tap_list(h);
+  if (i < 0 || i >= (int)v.size()) return fail(KDLAE_EPARAM, "tap index out of range");
+  if (name && name_len > 0) snprintf(name, (size_t)name_len, "%s", v[i].name.c_str());
+  if (C) *C = v[i].C;
+  if (num) *num = v[i].num;
+  if (den) *den = v[i].den;
+  return KDLAE_OK;
+}
+
+int kdlae_t_debug_taps(kdlae_t_handle* h, int n, float* const* dst) {
+  if (!h) return fail(KDLAE_ESTATE, "null handle");
+  if (n < 0 || (n > 0 && !dst)) return fail(KDLAE_EPARAM, "bad tap list");
+  h->taps.assign(dst, dst + n);
+  return KDLAE_OK;
 }
 
 int kdlae_t_probe_arm(kdlae_t_handle* h, int kernel_class, int level_filter) {

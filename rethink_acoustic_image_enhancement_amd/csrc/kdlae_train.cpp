@@ -74,7 +74,8 @@ struct kdlae_tt_handle {
   // cached, so a training step does not repeat the host-side dry run
   int mk_dsr = -1, mk_B = -1, mk_H = -1, mk_W = -1;
   size_t mk_fwd_end = 0, mk_peak = 0;
-  std::vector<int64_t> mk_keys;  // offsets of every key the backward writes (dry run), sorted
+  // per key offset the backward writes (dry run): the (first, last) mark at which it is written
+  std::map<int64_t, std::pair<int, int>> mk_touch;
   // KDLAE_DEBUG=train_trace: per-launch event pairs of the current call, dumped to KDLAE_PROBE_DUMP
   struct TraceRec {
     std::string tag;
@@ -199,6 +200,7 @@ struct Ctx {
   size_t red_off = 0;
 
   size_t red_cap = 0;  // floats of `red` (red_floats(): the largest single reduction's partials)
+  int red_err = KDLAE_OK;  // why the last red_take returned nullptr
   float* alloc(size_t n) {
     off = (off + 255) / 256 * 256;
     float* p = reinterpret_cast<float*>(base + off);
@@ -225,12 +227,23 @@ struct Ctx {
 int flush_reduce(Ctx& c);
 
 // a region of the reduction buffer for a queued reduction's partials (flushes when full)
+// Returns nullptr with c.red_err set (and the message in kdlae_last_error) when the flush fails
+// (a HIP error) or when one request alone exceeds the buffer (a sizing bug: KDLAE_ESTATE).
 float* red_take(Ctx& c, size_t n) {
   n = (n + 63) / 64 * 64;
   if (c.red_off + n > c.red_cap) {
-    if (flush_reduce(c) != KDLAE_OK) return nullptr;
+    const int rc = flush_reduce(c);
+    if (rc != KDLAE_OK) {
+      c.red_err = rc;
+      return nullptr;
+    }
   }
-  if (n > c.red_cap) return nullptr;  // red_floats() covers every reduction of the step
+  if (n > c.red_cap) {  // red_floats() must cover every reduction of the step
+    c.red_err = fail(KDLAE_ESTATE, "internal: a reduction needs " + std::to_string(n) +
+                                       " partial floats but the reduction buffer holds " +
+                                       std::to_string(c.red_cap) + " (red_floats() misses it)");
+    return nullptr;
+  }
   float* p = c.red + c.red_off;
   c.red_off += n;
   return p;
@@ -356,7 +369,7 @@ int bias_grad(Ctx& c, V dy, int N, long long P, float* out) {
   if (!out) return KDLAE_OK;
   const int nb = nblk_for(P, N);
   float* part = red_take(c, (size_t)nb * N);
-  if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+  if (!part) return c.red_err;
   LAUNCH(tr::launch_colsum(dy.p, dy.ld, N, P, 1, 0, part, nb, c.s));
   return queue_reduce(c, part, nb, N, N, out);
   return KDLAE_OK;
@@ -474,7 +487,7 @@ int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn
     const int ncols = Cin * Cout * 9;
     const int nb = tr::dw3_small_blocks(P, Cin, Cout, c.red_cap);
     float* part = red_take(c, (size_t)nb * ncols);
-    if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+    if (!part) return c.red_err;
     LAUNCH(tr::launch_dw3_small(dy.p, dy.ld, x.p, x.ld, Cin, Cout, Bn, H, W, dil, part, nb, c.s));
     TRY(queue_reduce(c, part, nb, ncols, ncols, gw));
   } else {
@@ -596,7 +609,7 @@ int ln_bwd(Ctx& c, const float* dy, const float* x, const float* st, int C, long
   const int ncol = bf ? C : 2 * C;
   const int nb = nblk_for(P, ncol);
   float* part = red_take(c, (size_t)nb * ncol);
-  if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+  if (!part) return c.red_err;
   LAUNCH(tr::launch_ln_bwd(dy, C, x, C, c.W(n + ".weight"), st, C, P, bf, R, C, dx, C, part, nb, c.s));
   // partial columns: [C weight | C bias (WithBias)], split when the keys are not adjacent
   float* gw = c.G(n + ".weight");
@@ -622,7 +635,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
     // gate backward + transposed dwconv + dwconv weight gradient in one pass (train_dwg.hip)
     const int nb = tr::dwg_blocks(Bn, r.H, r.W);
     float* part = red_take(c, (size_t)nb * 10 * 2 * hid);
-    if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+    if (!part) return c.red_err;
     LAUNCH(tr::launch_dwgate_bwd(dg, L1, r.yd, L2, r.y, L2, c.W(p + ".ffn.dwconv.weight"), hid, Bn, r.H, r.W, dy, L2,
                                  part, c.s));
     TRY(dw_reduce(c, part, nb, 2 * hid, p + ".ffn.dwconv"));
@@ -681,7 +694,7 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   {
     const int nb = tr::dwg_blocks(Bn, r.H, r.W);
     float* part = red_take(c, (size_t)nb * 10 * C3);
-    if (!part) return fail(KDLAE_EHIP, "reduction flush failed");
+    if (!part) return c.red_err;
     LAUNCH(tr::launch_dw_bwd(dqkvd, C3, r.qkv, C3, c.W(p + ".attn.qkv_dwconv.weight"), C3, Bn, r.H, r.W, dqkv, C3,
                              part, c.s));
     TRY(dw_reduce(c, part, nb, C3, p + ".attn.qkv_dwconv"));
@@ -1102,10 +1115,9 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
     // One pass from the end of the flat buffer: closed[m] <=> max over keys >= lo of last-write <= m
     h->mark_slot.assign(nmarks, -1);
     h->mark_lo.clear();
-    h->mk_keys.clear();
+    h->mk_touch = touch;
     std::vector<int64_t> first_lo(nmarks, h->total);  // lowest offset first written at or before mark m
     for (const auto& kv : touch) {
-      h->mk_keys.push_back(kv.first);
       for (int m = kv.second.first; m < nmarks && kv.first < first_lo[m]; ++m) first_lo[m] = kv.first;
     }
     int64_t prev_lo = h->total;
@@ -1149,12 +1161,23 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
   if (rc == KDLAE_OK) rc = flush_reduce(c);
   trace_dump(h, c.s, "bwd");
   if (rc) return rc;
-  // every gradient the launches wrote must have been seen by the dry run the marks came from (a
-  // write it missed could be all-reduced before it lands)
-  std::vector<int64_t> real;
-  for (const auto& kv : written) real.push_back(kv.first);
-  if (real != h->mk_keys)
+  // every gradient the launches wrote must have been written by the dry run the marks came from, at
+  // the same (first, last) marks: a write it missed, or one moved past the mark that declares its key
+  // final, could be all-reduced before it lands
+  if (written != h->mk_touch) {
+    for (const auto& kv : written) {
+      auto it = h->mk_touch.find(kv.first);
+      if (it == h->mk_touch.end())
+        return fail(KDLAE_ESTATE, "internal: the backward wrote gradient offset " + std::to_string(kv.first) +
+                                      " that the gradient-ready marks never saw");
+      if (it->second != kv.second)
+        return fail(KDLAE_ESTATE, "internal: gradient offset " + std::to_string(kv.first) + " written at marks [" +
+                                      std::to_string(kv.second.first) + ", " + std::to_string(kv.second.second) +
+                                      "] but the marks were planned for [" + std::to_string(it->second.first) +
+                                      ", " + std::to_string(it->second.second) + "]");
+    }
     return fail(KDLAE_ESTATE, "internal: gradient-ready marks disagree with the keys the backward writes");
+  }
   return KDLAE_OK;
 }
 

@@ -138,3 +138,52 @@ def test_module_replays_its_own_graph_for_repeated_shapes():
     assert torch.equal(ob["hq"], run(big, brate, graphs=False)["hq"])
     o4 = run(img2, torch.full_like(rate, 0.3))
     assert torch.equal(o4["hq"], run(img2, torch.full_like(rate, 0.3), graphs=False)["hq"])
+
+
+def test_implicit_capture_tolerates_other_threads():
+    """The module's implicit capture (second call of a shape) uses thread-local capture mode: another
+    thread of the process that allocates pinned host memory and copies it to the device meanwhile (a
+    DataLoader pin_memory thread, an async checkpoint copy) must neither fail nor be captured."""
+    import threading
+
+    kw = dict(dim=48, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, LayerNorm_type="BiasFree")
+    m = KDLAE_teacher(**kw)
+    load_hash_weights(m)
+    m = m.to(DEV).eval()
+    img = torch.from_numpy(hash_images("mt_a", (1, 3, 64, 64))).to(DEV)
+    rate = torch.full((1, 1, 64, 64), 0.6, device=DEV)
+    with torch.no_grad():
+        ref = m({"img": img, "denoise_rate": rate})  # eager: the next call of this shape captures
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    stop, errors, copies = threading.Event(), [], [0]
+
+    def worker():
+        n = 1 << 14
+        try:
+            while not stop.is_set():
+                n = n + 4096 if n < (1 << 20) else 1 << 14  # new sizes: fresh pinned allocations
+                h = torch.empty(n, pin_memory=True).fill_(1.0)
+                with torch.cuda.stream(side):  # every device call of this thread on its own stream
+                    d = h.to(DEV, non_blocking=True)
+                    back = d[-1:].to("cpu", non_blocking=True)
+                side.synchronize()
+                assert float(back[0]) == 1.0
+                copies[0] += 1
+        except Exception as e:  # noqa: BLE001 (reported by the main thread)
+            errors.append(repr(e))
+
+    t = threading.Thread(target=worker)
+    t.start()
+    try:
+        with torch.no_grad():
+            outs = [m({"img": img, "denoise_rate": rate}) for _ in range(3)]  # capture, replay, replay
+        torch.cuda.synchronize()
+    finally:
+        stop.set()
+        t.join(timeout=60)
+    assert not errors, errors
+    assert copies[0] > 0
+    assert len(m._graphs) == 1, "the shape should have been captured"
+    for o in outs:
+        assert torch.equal(o["hq"], ref["hq"]) and torch.equal(o["sr"], ref["sr"])

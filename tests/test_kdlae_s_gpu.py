@@ -91,3 +91,14 @@ def test_shape_and_device_errors():
         m(torch.zeros(1, 2, 30, 32, device=DEV))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         m.cpu()(torch.zeros(1, 2, 32, 32))
+
+
+def test_train_mode_with_grad_raises():
+    """KDLAE-S has no HIP backward yet: a training-mode forward that would need one raises instead of
+    returning a tensor without a graph (BasicSR's l_pix.backward() would fail on it, KDLAES.yml)."""
+    m = _model(dict(residual=True, hidden_channels=[16, 32, 64])).train()
+    x = torch.zeros(1, 2, 32, 32, device=DEV)
+    with pytest.raises(NotImplementedError, match="no backward"):
+        m(x)
+    with torch.no_grad():
+        assert m(x).shape == x.shape  # inference in train mode without grad is fine

@@ -1,6 +1,6 @@
 """Per-kernel-class MFMA / VALU busy and effective clock from a rocprofv3 --pmc pass.
 
-Counters (one pass, tools/gpu_pmc_busy.sh): SQ_VALU_MFMA_BUSY_CYCLES (per-SIMD cycles the matrix
+Counters (one pass, tools/gpu.sh pmc): SQ_VALU_MFMA_BUSY_CYCLES (per-SIMD cycles the matrix
 pipe is busy, summed over SIMDs), SQ_ACTIVE_INST_VALU (quad-cycles, summed over CUs... per the
 VALUBusy formula), GRBM_GUI_ACTIVE (GPU-busy cycles; rocprofv3 reports the sum over the 8 XCDs),
 SQ_WAVE_CYCLES / SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY (wave-state split).
