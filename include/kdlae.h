@@ -21,8 +21,7 @@
  * results.  KDLAE_DEBUG (comma-separated flags, read when a KDLAE-T handle
  * builds its pack program: kdlae_t_prepare or the first pack) selects between kernel schedules that produce
  * the same bits: "no_attn_in_fusion" keeps the attention-output GEMM and the
- * LN + ffn.project_in GEMM separate for C = 48 blocks; "attn_in_split" fuses
- * the C = 96 blocks' first project_in weight group as well.  KDLAE_PROBE_DUMP
+ * LN + ffn.project_in GEMM separate for C = 48 blocks.  KDLAE_PROBE_DUMP
  * names a CSV file kdlae_t_probe_read writes per-launch timings to.
  * One more KDLAE_DEBUG flag is read on EVERY training call (kdlae_tt_forward /
  * kdlae_tt_backward / kdlae_tt_backward_marked), not at pack time:
@@ -123,12 +122,13 @@ int kdlae_t_forward(kdlae_t_handle* h, const float* img, const float* rate, int 
 int kdlae_t_probe_arm(kdlae_t_handle* h, int kernel_class, int level_filter);
 int kdlae_t_probe_read(kdlae_t_handle* h, double* ms, int64_t* launches, double* bytes, double* flops);
 
-/* Diagnostics (tools/config1_taps.py; not part of the drop-in boundary): the outputs of every
- * TransformerBlock in execution order.  kdlae_t_debug_tap_info names tap i (its state_dict prefix,
- * e.g. "latent.3"), its channel count C and its resolution relative to the forward's input, H * num /
- * den.  While kdlae_t_debug_taps(h, n, dst) is armed (n = 0 disarms), every kdlae_t_forward copies
- * block i's output (i < n, dst[i] != NULL) into the device buffer dst[i] as compact NHWC
- * [B][H_i][W_i][C] on the forward's stream.  Results are unchanged. */
+/* Diagnostics (tools/config1_taps.py; not part of the drop-in boundary): activations at every
+ * TransformerBlock stage in execution order — per stage its input ("<stage>.in"), then per block the
+ * attention half's output x1 = x + attn(norm1 x) ("<stage>.<i>.attn", KDLAE_model.py:160) and the
+ * block output ("<stage>.<i>", :161).  kdlae_t_debug_tap_info names tap i, its channel count C and its
+ * resolution relative to the forward's input, H * num / den.  While kdlae_t_debug_taps(h, n, dst) is
+ * armed (n = 0 disarms), every kdlae_t_forward copies tap i (i < n, dst[i] != NULL) into the device
+ * buffer dst[i] as compact NHWC [B][H_i][W_i][C] on the forward's stream.  Results are unchanged. */
 int kdlae_t_debug_tap_count(const kdlae_t_handle* h);
 int kdlae_t_debug_tap_info(const kdlae_t_handle* h, int i, char* name, int name_len, int* C, int* num, int* den);
 int kdlae_t_debug_taps(kdlae_t_handle* h, int n, float* const* dst);
@@ -341,7 +341,8 @@ int kdlae_debug_tgemm(const kdlae_debug_tgemm_desc* d, void* stream);
  *   k = tap * 16 cg_per_tap + c, zero padding = dil; out_mode 1 / 2 stores through PixelUnshuffle(2)
  *   / PixelShuffle(2) (R then in the output geometry).  Wp: fragment-packed [ntiles][kgroups][64][4],
  *   element (l, e) of (t, g) = W(16 t + l % 16, 16 g + 4 (l / 16) + e); + b * w_img_stride per image.
- *   Wm != 0: fused attention output, x1 = R + Wm v (+ bias_m) stored to out1, then out = LN(x1) W.
+ *   Wm != 0: fused attention output, x1 = R + Wm v (+ bias_m) stored to out1, then out = LN(x1) W;
+ *   Wm (per image, w_img_stride apart) holds hi / lo virtual tiles [2 kgroups][kgroups][64][4].
  *   stats: [pixels][2] scratch when LN meets a chunked K.  group_tiles > 0: resident schedule.
  *   tiles_per_block 0: the engine's grid rule.  route 0: production dispatch; 1: the r01
  *   conv_gemm_kernel of (NT, KG) (the fallback for ld % 4 != 0 views). */
@@ -358,6 +359,8 @@ typedef struct kdlae_debug_gemm_desc {
   const float* Wm; int64_t wm_img_stride; const float* bias_m; float* out1; int ldo1;
   int NT, KG, wpe, group_tiles, tiles_per_block;
   int route;
+  const float* ln_w; const float* ln_b;  /* LN affine [kgroups * 16] (null: unit weight / zero bias) */
+  int dual;                              /* Wp holds hi / lo virtual tiles: out tile t = tile 2t + tile 2t+1 */
 } kdlae_debug_gemm_desc;
 int kdlae_debug_gemm(const kdlae_debug_gemm_desc* d, void* stream);
 /* Entry i of a compiled variant table: family 0 conv_gemm_kernel (NT, KG, CONV3, OUT, PF, WPE, RES),

@@ -4,7 +4,7 @@ ANALYSIS INFRASTRUCTURE (the cpu leg imports oracle/; nothing here is on the pro
 
   gpu leg (GPU box):  python tools/config1_taps.py gpu --tag base [--out gpurun_out/c1]
       runs the drop-in module (the library KDLAE_LIB names, default the in-tree build) on the config-1
-      input with kdlae_t_debug_taps armed and saves every TransformerBlock's output (subsampled to
+      input with kdlae_t_debug_taps armed and saves every stage input, block attention half and block output (subsampled to
       <= 65536 floats per block) plus hq / sr ([::2, ::2]) to <out>/taps_<tag>.npz.
   cpu leg (here):     python tools/config1_taps.py cpu [--out gpurun_out/c1] [--write profiles/...]
       runs the CPU oracle in fp64 and fp32 (and with the HIP path's Gram slot scheme) recording the same
@@ -83,26 +83,40 @@ def gpu_leg(args):
 
 
 def oracle_run(cfg, sd, img, rate, mdta=None):
-    """The oracle forward with every TransformerBlock's output recorded (same sampling as the taps)."""
+    """The oracle forward with the tap points recorded (same sampling as the taps): every stage's
+    input, every block's attention half x1 = x + attn(norm1 x) and its output (KDLAE_model.py:159-163)."""
     import oracle.kdlae_oracle as O
     rec = {}
-    orig_tb, orig_mdta = O.transformer_block, O.mdta
+    orig = {n: getattr(O, n) for n in ("transformer_block", "stage", "mdta")}
 
-    def tb(x, sd_, p, heads, lt):
-        y = orig_tb(x, sd_, p, heads, lt)
+    def keep(name, y):
         _, c, h, w = y.shape
         s = stride_for(h, w, c)
-        rec[p] = y[0, :, ::s, ::s].double()
+        rec[name] = y[0, :, ::s, ::s].double()
+
+    def tb(x, sd_, p, heads, lt):
+        x1 = x + O.mdta(O.layer_norm(x, sd_, p + ".norm1", lt), sd_, p + ".attn", heads)
+        keep(p + ".attn", x1)
+        y = x1 + O.gdfn(O.layer_norm(x1, sd_, p + ".norm2", lt), sd_, p + ".ffn")
+        keep(p, y)
         return y
 
-    O.transformer_block = tb
+    def stage(x, sd_, name, n, heads, lt):
+        if n > 0:
+            keep(name + ".in", x)
+        for i in range(n):
+            x = tb(x, sd_, f"{name}.{i}", heads, lt)
+        return x
+
+    O.transformer_block, O.stage = tb, stage
     if mdta is not None:
         O.mdta = mdta
     try:
         with torch.no_grad():
             out = O.teacher_forward(sd, img, rate, cfg)
     finally:
-        O.transformer_block, O.mdta = orig_tb, orig_mdta
+        for n, f in orig.items():
+            setattr(O, n, f)
     rec["hq"] = out["hq"][0, :, ::2, ::2].double()
     rec["sr"] = out["sr"][0, :, ::2, ::2].double()
     return rec
@@ -119,11 +133,18 @@ def cpu_leg(args):
     cfg = O.TeacherCfg(**kw)
     sd32 = hash_sd_for(O.teacher_param_shapes(cfg))
     sd64 = {k: v.double() for k, v in sd32.items()}
-    t = time.time()
-    r64 = oracle_run(cfg, sd64, img.double(), rate.double())
-    print(f"fp64 oracle {time.time() - t:.0f} s", flush=True)
-    cols = {"ref32": oracle_run(cfg, sd32, img, rate),
-            "slots32": oracle_run(cfg, sd32, img, rate, mdta=mdta_slots)}
+    cache = os.path.join(args.out, "oracle_cache.pt")  # this script's own output (weights_only load)
+    if os.path.exists(cache):
+        c = torch.load(cache, weights_only=True)
+        r64, cols = c["r64"], {"ref32": c["ref32"], "slots32": c["slots32"]}
+    else:
+        t = time.time()
+        r64 = oracle_run(cfg, sd64, img.double(), rate.double())
+        print(f"fp64 oracle {time.time() - t:.0f} s", flush=True)
+        cols = {"ref32": oracle_run(cfg, sd32, img, rate),
+                "slots32": oracle_run(cfg, sd32, img, rate, mdta=mdta_slots)}
+        os.makedirs(args.out, exist_ok=True)
+        torch.save({"r64": r64, **cols}, cache)
     for path in sorted(glob.glob(os.path.join(args.out, "taps_*.npz"))):
         d = np.load(path, allow_pickle=False)
         tag = os.path.basename(path)[5:-4]
@@ -133,7 +154,7 @@ def cpu_leg(args):
         cols["hip_" + tag] = rec
     keys = list(r64.keys())
     lines = [__doc__.strip(), "",
-             "relative error per TransformerBlock output = max-abs vs the fp64 oracle / max |x_fp64| over the",
+             "relative error per tap (stage input .in, attention half .attn, block output) = max-abs vs the fp64 oracle / max |x_fp64| over the",
              f"block's sample (<= {BUDGET} floats); hq / sr rows: absolute max-abs over [::2, ::2] and [::8, ::8].",
              "ref32 = the oracle in fp32 (= the reference's arithmetic); slots32 = ref32 with the HIP path's Gram",
              "scheme (fp32 sums over 1024-pixel slots, slots summed in fp64); hip_* = the HIP library builds.", "",
