@@ -21,7 +21,8 @@
  * results.  KDLAE_DEBUG (comma-separated flags, read when a KDLAE-T handle
  * builds its pack program: kdlae_t_prepare or the first pack) selects between kernel schedules that produce
  * the same bits: "no_attn_in_fusion" keeps the attention-output GEMM and the
- * LN + ffn.project_in GEMM separate for C = 48 blocks.  KDLAE_PROBE_DUMP
+ * LN + ffn.project_in GEMM separate for C = 48 blocks; "attn_in_split" fuses
+ * the C = 96 blocks' first project_in weight group as well.  KDLAE_PROBE_DUMP
  * names a CSV file kdlae_t_probe_read writes per-launch timings to.
  * One more KDLAE_DEBUG flag is read on EVERY training call (kdlae_tt_forward /
  * kdlae_tt_backward / kdlae_tt_backward_marked), not at pack time:
@@ -310,6 +311,39 @@ int kdlae_train_mixup(const float* in, float* out, int B, int64_t per_sample, co
 /* replaces BaseModel.model_ema(decay) (Train/basicsr/models/base_model.py:54-62) over the flat buffers. */
 int kdlae_train_ema(float* ema, const float* theta, int64_t n, float decay, void* stream);
 
+/* ------------------------------------------------------------------ KDLAE-S training
+ * One optimisation step of BasicSR's ImageCleanModel on KDLAE_student with KDLAES.yml
+ * (Train/Denoising/Options/paper202508/KDLAES.yml: L1LossForVideoFrames, clip_grad_norm_, AdamW):
+ * forward with saved activations and the backward of every layer (Conv3d 3x3x3 + ReLU, MaxPool3d
+ * (1,2,2), ConvTranspose3d (1,2,2) + skip, out_conv + residual; KDLAE/KDLAE_model.py:395-431).
+ * Parameters / gradients: flat caller-owned buffers of kdlae_st_num_floats floats in state_dict order,
+ * every key 16-byte aligned (pads zero), as for kdlae_tt_*; kdlae_train_clip_adamw / _ema / _mixup
+ * apply unchanged. */
+typedef struct kdlae_st_handle kdlae_st_handle;
+/* replaces KDLAE_student.__init__ for training (KDLAE_model.py:341-384); inp/out_channels 1, kernel_size 3 */
+int kdlae_st_create(const kdlae_s_config* cfg, int device, kdlae_st_handle** out);
+int kdlae_st_destroy(kdlae_st_handle* h);
+int kdlae_st_num_params(const kdlae_st_handle* h);
+int kdlae_st_param_info(const kdlae_st_handle* h, int index, const char** name, int64_t* numel, int64_t* offset);
+int64_t kdlae_st_num_floats(const kdlae_st_handle* h);
+int64_t kdlae_st_workspace_bytes(const kdlae_st_handle* h, int B, int F, int H, int W);
+/* replaces `preds = self.net_g(self.lq)` (image_restoration_model.py:200) for KDLAE_student: x, out [B, F, H, W];
+ * activations stay in `workspace` for kdlae_st_backward */
+int kdlae_st_forward(kdlae_st_handle* h, const float* theta, const float* x, int B, int F, int H, int W, float* out,
+                     void* workspace, int64_t workspace_bytes, void* stream);
+/* replaces `l_pix.backward()` (:213): dout [B, F, H, W] -> grad (flat, overwritten); x gets no gradient */
+int kdlae_st_backward(kdlae_st_handle* h, const float* theta, const float* dout, float* grad, void* workspace,
+                      int64_t workspace_bytes, void* stream);
+/* replaces L1LossForVideoFrames(l1loss_weight, reduction, temporal_weight, binary)(pred, target)
+ * (Train/basicsr/models/losses/losses.py:409-526) for pred / target [N, frames, H, W] (hw = H W):
+ * loss[0] = l1loss_weight (mean|p - t| + mean|bin(p) - bin(t)|) + temporal_weight mean|dp - dt| (frame
+ * differences; frames == 1: no temporal term); reduction 0 = 'mean', 1 = 'sum' ('max' / 'mix': EINVAL_CONFIG).
+ * dpred receives d loss / d pred.  scratch: kdlae_train_l1frames_scratch_floats() floats. */
+int64_t kdlae_train_l1frames_scratch_floats(void);
+int kdlae_train_l1frames(const float* pred, const float* target, int N, int frames, int64_t hw, float l1loss_weight,
+                         float temporal_weight, float binary, int reduction, float* dpred, float* loss, float* scratch,
+                         void* stream);
+
 /* ---- Kernel self-test entry points (tests/test_kernel_variants_gpu.py; not part of the drop-in
  * boundary).  One launch of the training GEMM family on caller device buffers:
  *   C(m, n) = sum_k A(m, k) B(k, n) [+ bias[n]] [+ rs[n] R(m, n)], batch z = z1 * nz2 + z2, every
@@ -341,8 +375,7 @@ int kdlae_debug_tgemm(const kdlae_debug_tgemm_desc* d, void* stream);
  *   k = tap * 16 cg_per_tap + c, zero padding = dil; out_mode 1 / 2 stores through PixelUnshuffle(2)
  *   / PixelShuffle(2) (R then in the output geometry).  Wp: fragment-packed [ntiles][kgroups][64][4],
  *   element (l, e) of (t, g) = W(16 t + l % 16, 16 g + 4 (l / 16) + e); + b * w_img_stride per image.
- *   Wm != 0: fused attention output, x1 = R + Wm v (+ bias_m) stored to out1, then out = LN(x1) W;
- *   Wm (per image, w_img_stride apart) holds hi / lo virtual tiles [2 kgroups][kgroups][64][4].
+ *   Wm != 0: fused attention output, x1 = R + Wm v (+ bias_m) stored to out1, then out = LN(x1) W.
  *   stats: [pixels][2] scratch when LN meets a chunked K.  group_tiles > 0: resident schedule.
  *   tiles_per_block 0: the engine's grid rule.  route 0: production dispatch; 1: the r01
  *   conv_gemm_kernel of (NT, KG) (the fallback for ld % 4 != 0 views). */
@@ -359,8 +392,6 @@ typedef struct kdlae_debug_gemm_desc {
   const float* Wm; int64_t wm_img_stride; const float* bias_m; float* out1; int ldo1;
   int NT, KG, wpe, group_tiles, tiles_per_block;
   int route;
-  const float* ln_w; const float* ln_b;  /* LN affine [kgroups * 16] (null: unit weight / zero bias) */
-  int dual;                              /* Wp holds hi / lo virtual tiles: out tile t = tile 2t + tile 2t+1 */
 } kdlae_debug_gemm_desc;
 int kdlae_debug_gemm(const kdlae_debug_gemm_desc* d, void* stream);
 /* Entry i of a compiled variant table: family 0 conv_gemm_kernel (NT, KG, CONV3, OUT, PF, WPE, RES),

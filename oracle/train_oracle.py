@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from .kdlae_oracle import TeacherCfg, teacher_forward
+from .kdlae_oracle import StudentCfg, TeacherCfg, student_forward, teacher_forward
 
 # KDLAET.yml (Train/Denoising/Options/paper202508/KDLAET.yml:113-128)
 YML_OPTIM = dict(lr=1e-5, weight_decay=0.5e-4, betas=(0.2, 0.999))
@@ -52,6 +52,36 @@ def loss_and_grads(sd: dict, img, rate, gt: dict, cfg: TeacherCfg):
     loss = l1sr_loss(out, gt)
     grads = torch.autograd.grad(loss, list(params.values()), allow_unused=True)
     return loss.detach(), {k: (g if g is not None else torch.zeros_like(params[k])) for k, g in zip(params, grads)}
+
+
+def l1_video_frames(pred, target, l1loss_weight=0.64, reduction="mean", temporal_weight=0.36, binary=0.1):
+    """L1LossForVideoFrames.forward (losses.py:440-526) for reduction 'mean' / 'sum' (no element weights):
+    l1loss_weight * reduce(|p - t| + |bin(p) - bin(t)|) + temporal_weight * reduce(|dp - dt|) over the frame
+    axis (dim 1); one frame: the first term only.  bin(x) = (x > binary), carrying no gradient."""
+    if reduction not in ("mean", "sum"):
+        raise NotImplementedError(f"reduction {reduction!r}")
+    red = (lambda t: t.mean()) if reduction == "mean" else (lambda t: t.sum())
+    pb = torch.where(pred > binary, torch.ones_like(pred), torch.zeros_like(pred))
+    tb = torch.where(target > binary, torch.ones_like(target), torch.zeros_like(target))
+    per_frame = torch.abs(pred - target) + torch.abs(pb - tb)
+    if pred.size(1) > 1:
+        dp = pred[:, 1:] - pred[:, :-1]
+        dt = target[:, 1:] - target[:, :-1]
+        return l1loss_weight * red(per_frame) + temporal_weight * red(torch.abs(dp - dt))
+    return l1loss_weight * red(per_frame)
+
+
+# KDLAES.yml (Train/Denoising/Options/paper202508/KDLAES.yml:88-110)
+YML_S_OPTIM = dict(lr=3e-4, weight_decay=1e-4, betas=(0.9, 0.999))
+YML_S_LOSS = dict(l1loss_weight=0.9, temporal_weight=0.1, reduction="mean")
+
+
+def student_loss_and_grads(sd: dict, x, target, cfg: StudentCfg, **loss_kw):
+    """KDLAE_student forward + L1LossForVideoFrames + autograd; returns (loss, {key: grad})."""
+    params = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
+    loss = l1_video_frames(student_forward(params, x, cfg), target, **loss_kw)
+    grads = torch.autograd.grad(loss, list(params.values()))
+    return loss.detach(), dict(zip(params, grads))
 
 
 class TrainStep:

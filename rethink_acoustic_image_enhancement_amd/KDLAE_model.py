@@ -458,12 +458,18 @@ class KDLAE_student(nn.Module):
         if H % m or W % m:
             raise RuntimeError(f"KDLAE_student needs H and W divisible by {m}, got {H}x{W}")
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
-            if self.training:
-                # BasicSR trains KDLAE_student (KDLAES.yml) with l_pix.backward(): a graph-less output
-                # would fail there, or silently train nothing
-                raise NotImplementedError(
-                    "KDLAE_student (MI355X build): the HIP path has no backward yet; wrap inference in "
-                    "torch.no_grad() or call .eval()")
+            if self.training and any(p.requires_grad for p in self.parameters()):
+                # BasicSR's KDLAE-S training (KDLAES.yml, l_pix.backward()): the HIP training engine
+                # behind an autograd node (train.py)
+                from .train import StudentTrainEngine, StudentTrainFn
+                if x.requires_grad and not self._warned_grad:
+                    warnings.warn("KDLAE_student HIP training path: the input frames receive no gradient")
+                    self._warned_grad = True
+                eng = self.__dict__.setdefault("_train_engines", {}).get(x.device.index)
+                if eng is None:
+                    eng = StudentTrainEngine(self, x.device)
+                    self._train_engines[x.device.index] = eng
+                return StudentTrainFn.apply(eng, x, *self.parameters())
             if not self._warned_grad:
                 warnings.warn("KDLAE_student in eval mode with grad enabled: the HIP inference path returns "
                               "outputs without an autograd graph")

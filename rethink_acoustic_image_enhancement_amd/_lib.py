@@ -38,6 +38,9 @@ EXPORTS = (
     "kdlae_tt_mark_count", "kdlae_tt_mark_lo", "kdlae_tt_mark_wait", "kdlae_tt_mark_sync",
     "kdlae_train_l1sr_scratch_floats", "kdlae_train_l1sr", "kdlae_train_adamw_scratch_floats",
     "kdlae_train_clip_adamw", "kdlae_train_mixup", "kdlae_train_ema",
+    "kdlae_st_create", "kdlae_st_destroy", "kdlae_st_num_params", "kdlae_st_param_info", "kdlae_st_num_floats",
+    "kdlae_st_workspace_bytes", "kdlae_st_forward", "kdlae_st_backward",
+    "kdlae_train_l1frames_scratch_floats", "kdlae_train_l1frames",
     "kdlae_debug_tgemm",
     "kdlae_debug_gemm",
     "kdlae_debug_gemm_variant",
@@ -169,6 +172,22 @@ def lib() -> ctypes.CDLL:
                                          c_void_p]
     L.kdlae_train_mixup.argtypes = [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_float, c_void_p]
     L.kdlae_train_ema.argtypes = [c_void_p, c_void_p, c_int64, c_float, c_void_p]
+    L.kdlae_st_create.argtypes = [ctypes.POINTER(SConfig), c_int, ctypes.POINTER(c_void_p)]
+    L.kdlae_st_destroy.argtypes = [c_void_p]
+    L.kdlae_st_num_params.argtypes = [c_void_p]
+    L.kdlae_st_param_info.argtypes = [c_void_p, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int64),
+                                      ctypes.POINTER(c_int64)]
+    L.kdlae_st_num_floats.argtypes = [c_void_p]
+    L.kdlae_st_num_floats.restype = c_int64
+    L.kdlae_st_workspace_bytes.argtypes = [c_void_p, c_int, c_int, c_int, c_int]
+    L.kdlae_st_workspace_bytes.restype = c_int64
+    L.kdlae_st_forward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                   c_int64, c_void_p]
+    L.kdlae_st_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]
+    L.kdlae_train_l1frames_scratch_floats.argtypes = []
+    L.kdlae_train_l1frames_scratch_floats.restype = c_int64
+    L.kdlae_train_l1frames.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int64, ctypes.c_float, ctypes.c_float,
+                                       ctypes.c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p]
     L.kdlae_debug_tgemm.argtypes = [c_void_p, c_void_p]
     for f in ("kdlae_debug_gemm", "kdlae_debug_gram", "kdlae_debug_ln", "kdlae_debug_small_in"):
         getattr(L, f).argtypes = [c_void_p, c_void_p]

@@ -86,49 +86,9 @@ __device__ __forceinline__ void load_a(const GemmParams& p, const float* __restr
   }
 }
 
-// a = a * w + b for the chunk's first kg_valid k-groups (the rest meet zero weights: left alone, so
-// the affine arrays need only cover the true K)
-template <int KG>
-__device__ __forceinline__ void ln_affine(f32x4 (&a)[kGemmRT][KG], const f32x4* lnw, const f32x4* lnb,
-                                          int kg_valid = KG) {
-  const int lq = (threadIdx.x & 63) >> 4;
-  // one k-group at a time (sched barriers keep the affine's loads from being hoisted together: the
-  // chunked kernels have no VGPRs to spare)
-#pragma unroll
-  for (int g = 0; g < KG; ++g) {
-    // kg_valid < KG only where the affine arrays end with the true K (the r01 kernel's global copies):
-    // no branch, no read past them.  The staged LDS copies are zero-padded instead.
-    const bool ok = g < kg_valid;
-    const int gi = ok ? g : 0;
-    if (lnw) {
-      const f32x4 w = lnw[4 * gi + lq];
-#pragma unroll
-      for (int r = 0; r < kGemmRT; ++r) a[r][g] = ok ? a[r][g] * w : a[r][g];
-    }
-    if (lnb) {
-      const f32x4 bb = lnb[4 * gi + lq];
-#pragma unroll
-      for (int r = 0; r < kGemmRT; ++r) a[r][g] = ok ? a[r][g] + bb : a[r][g];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// float4 q of the LN weight (half 0) or bias (half 1) for LDS staging: zero past ln_C; a null weight
-// stages ones, a null bias zeros
-__device__ __forceinline__ f32x4 ln_affine_at(const GemmParams& p, int half, int q) {
-  const float* src = half ? p.ln_b : p.ln_w;
-  if (!src) return half ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4{1.f, 1.f, 1.f, 1.f};
-  return 4 * q < p.ln_C ? *reinterpret_cast<const f32x4*>(src + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-}
-
-// LayerNorm of the A rows in registers: ((x - mean) * rstd) * w + b per element, the reference's
-// order (KDLAE_model.py:52, :70).  lnw / lnb: the affine of this chunk's k-groups as [4 g + lq]
-// float4s (LDS or global); null = unit weight / zero bias (self-test).
 template <int KG>
 __device__ __forceinline__ void apply_ln(const GemmParams& p, int b, int row0, int li, int HW,
-                                         f32x4 (&a)[kGemmRT][KG], const f32x4* lnw, const f32x4* lnb,
-                                         int kg_valid = KG) {
+                                         f32x4 (&a)[kGemmRT][KG]) {
   const float wb = (p.ln == 2) ? 1.f : 0.f;
 #pragma unroll
   for (int r = 0; r < kGemmRT; ++r) {
@@ -161,7 +121,6 @@ __device__ __forceinline__ void apply_ln(const GemmParams& p, int b, int row0, i
 #pragma unroll
     for (int g = 0; g < KG; ++g) a[r][g] = (a[r][g] - sh) * rstd;
   }
-  ln_affine<KG>(a, lnw, lnb, kg_valid);
 }
 
 // acc[t][r] += W-tile(t) x A(r) over KG k-groups; W tiles at wl[(t * ldk + g) * 64 + lane].
@@ -351,10 +310,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
       } else {
         load_a<KG, CONV3>(p, p.A + (long long)b * HW * p.lda, row0, 0, li, lq, HW, a);
       }
-      if constexpr (!CONV3)
-        if (p.ln)
-          apply_ln<KG>(p, b, row0, li, HW, a, reinterpret_cast<const f32x4*>(p.ln_w),
-                       reinterpret_cast<const f32x4*>(p.ln_b));
+      if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
       for (int c0 = 0; c0 < gtiles; c0 += NT) {
         f32x4 acc[NT][kGemmRT];
 #pragma unroll
@@ -402,11 +358,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
         __syncthreads();
         f32x4 a[kGemmRT][KG];
         load_a<KG, CONV3>(p, Ab, row0, kc, li, lq, HW, a);
-        if constexpr (!CONV3)
-          if (p.ln)
-            apply_ln<KG>(p, b, row0, li, HW, a,
-                         p.ln_w ? reinterpret_cast<const f32x4*>(p.ln_w) + kc * KG * 4 : nullptr,
-                         p.ln_b ? reinterpret_cast<const f32x4*>(p.ln_b) + kc * KG * 4 : nullptr, p.kgroups - kc * KG);
+        if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
         mfma_chunk<NT, KG>(wlds, KG, lane, a, acc);
       }
       if (p.R) epilogue<NT, OUT, true>(p, b, row0, nc * NT, NT, li, lq, HW, acc, wlds + NT * KG * 64);
@@ -442,12 +394,8 @@ __device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t r, unsigned of
 }
 constexpr unsigned kOOB = 0x80000000u;  // a byte offset past every descriptor's range
 
-// DUAL (GemmParams::dual, KG == 6 body only): the tile pairs (2u, 2u + 1) of a chunk are the hi / lo
-// halves of real output tile (chunk base + 2u) / 2: one residual load and one store of
-// (hi + lo) + bias + R per pair.
-template <int NT, int KG, int NCH, int WPE, bool HASR, bool PF, bool DUAL = false>
+template <int NT, int KG, int NCH, int WPE, bool HASR, bool PF>
 __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams p) {
-  static_assert(!DUAL || (KG == 6 && NT % 2 == 0), "dual tiles ride the unit-major KG = 6 body in pairs");
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
   const int tid = threadIdx.x;
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -474,13 +422,6 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
   };
   int staged = p.w_img_stride ? t_begin / p.tiles_per_img : 0;
   stage(staged);
-  // LN affine of the whole K (constant over the block): [KG * 4] weights then [KG * 4] biases
-  f32x4* lnl = wlds + TP * KG * 64 + TP * 4;
-  if (p.ln)
-    for (int idx = tid; idx < 2 * KG * 4; idx += kGemmThreads) {
-      const int half = idx / (KG * 4), q = idx - half * KG * 4;
-      lnl[idx] = ln_affine_at(p, half, q);
-    }
   __syncthreads();
   const unsigned a_bytes = (unsigned)HW * (unsigned)p.lda * 4u;
   const unsigned o_bytes = (unsigned)HW * (unsigned)p.ldo * 4u;
@@ -530,22 +471,17 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
     } else {
       load_rows(tile, a);
     }
-    if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a, lnl, p.ln_b ? lnl + KG * 4 : nullptr);
+    if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
     [[maybe_unused]] __amdgpu_buffer_rsrc_t rr;
     if constexpr (HASR) rr = buf_rsrc(p.R + (long long)b * HW * p.ldr, r_bytes);
     unsigned vo[kGemmRT], vr[kGemmRT];
-    const unsigned gch = (unsigned)(DUAL ? g0 / 2 : g0);  // the group's first real output tile
 #pragma unroll
     for (int r = 0; r < kGemmRT; ++r) {
       const unsigned pix = (unsigned)(row0 + r * 16 + li);
-      vo[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldo * 4u + 16u * lq + 64u * gch : o_bytes;
-      vr[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldr * 4u + 16u * lq + 64u * gch : r_bytes;
+      vo[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldo * 4u + 16u * lq + 64u * g0 : o_bytes;
+      vr[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldr * 4u + 16u * lq + 64u * g0 : r_bytes;
     }
-    // byte offset of staged (virtual) tile t: real tile t / 2 for DUAL
-    auto dvoff = [&](int t, unsigned v, unsigned bytes) -> int {
-      return DUAL ? (int)(((t < gtiles) ? v : bytes) + 64u * (unsigned)(t >> 1)) : tile_voff(t, v, bytes);
-    };
     if constexpr (KG == 6) {
     // K = 96: unit-major chunk body.  Each tile pair is accumulated over every k-group and stored
     // before the next pair starts, so a pair's stores issue beside the next pair's MFMAs instead of
@@ -567,12 +503,12 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
         [[maybe_unused]] f32x4 rs[2][kGemmRT];
         if constexpr (HASR) {
 #pragma unroll
-          for (int q = 0; q < (DUAL ? 1 : 2); ++q)
+          for (int q = 0; q < 2; ++q)
 #pragma unroll
             for (int r = 0; r < kGemmRT; ++r)
               rs[q][r] = (t + q < NT)
                              ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                             rr, dvoff(ch * NT + t + q, vr[r], r_bytes), 0, 0))
+                                                             rr, tile_voff(ch * NT + t + q, vr[r], r_bytes), 0, 0))
                              : f32x4{0.f, 0.f, 0.f, 0.f};
         }
         f32x4 a0[kGemmRT], a1[kGemmRT];
@@ -598,17 +534,6 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
           c0 = n0;
           c1 = n1;
         }
-        if constexpr (DUAL) {
-          // ((hi + lo) + bias) + R: the order gemm_attn_in_kernel uses for x1 (bit-identical paths)
-          const f32x4 bias = bl[4 * t + lq];
-#pragma unroll
-          for (int r = 0; r < kGemmRT; ++r) {
-            f32x4 v = (a0[r] + a1[r]) + bias;
-            if constexpr (HASR) v += rs[0][r];
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
-                                                   dvoff(ch * NT + t, vo[r], o_bytes), 0, 0);
-          }
-        } else {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           if (t + q >= NT) continue;
@@ -620,7 +545,6 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
                                                    tile_voff(ch * NT + t + q, vo[r], o_bytes), 0, 0);
           }
-        }
         }
       }
     }
@@ -671,10 +595,8 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
 // accumulators through the residual add and LayerNorm into the project_in MFMAs without leaving
 // registers; it is stored once (the FFN's residual) and never re-read.  The unfused pair wrote x1,
 // then read it back, and its N = 48 GEMM ran at ~4.5 TB/s / 36 TF/s.
-// M arrives as hi / lo virtual tiles (attn_fold; GemmParams::dual).
 // Numerics: both GEMMs accumulate k-group-major, k-step-minor exactly as gemm_res_kernel does, and
-// x1 = ((acc_hi + acc_lo) + bias_m) + x in that order, so the result equals the unfused (DUAL) path
-// bit for bit.
+// x1 = (acc + bias_m) + x in that order, so the result equals the unfused path bit for bit.
 template <int NT, int KG, int NCH>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
@@ -686,10 +608,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
   const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
   if (t_begin >= t_end) return;
   constexpr int TP = NT * NCH;       // project_in tiles staged (zero weights past ntiles)
-  // M fragments [2 KG virtual tiles (hi, lo)][KG groups][64], then bias_m [KG][4], then the LN affine
-  // [KG * 4] weights, [KG * 4] biases
-  f32x4* ml = wlds + TP * KG * 64 + TP * 4;
-  f32x4* lnl = ml + 2 * KG * KG * 64 + KG * 4;
+  f32x4* ml = wlds + TP * KG * 64 + TP * 4;  // M fragments [KG tiles][KG groups][64], then bias_m [KG][4]
   {
     const f32x4* wbase = reinterpret_cast<const f32x4*>(p.Wp);
     const int n4 = p.ntiles * KG * 64;
@@ -701,16 +620,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
                                      ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  for (int idx = tid; idx < 2 * KG * 4; idx += kGemmThreads) {
-    const int half = idx / (KG * 4);
-    lnl[idx] = ln_affine_at(p, half, idx - half * KG * 4);
-  }
   auto stage_m = [&](int b) {
     const f32x4* mb = reinterpret_cast<const f32x4*>(p.Wm + (long long)b * p.wm_img_stride);
-    for (int idx = tid; idx < 2 * KG * KG * 64; idx += kGemmThreads) ml[idx] = mb[idx];
+    for (int idx = tid; idx < KG * KG * 64; idx += kGemmThreads) ml[idx] = mb[idx];
     for (int idx = tid; idx < KG * 4; idx += kGemmThreads)
-      ml[2 * KG * KG * 64 + idx] =
-          p.bias_m ? *reinterpret_cast<const f32x4*>(p.bias_m + 4 * idx) : f32x4{0.f, 0.f, 0.f, 0.f};
+      ml[KG * KG * 64 + idx] = p.bias_m ? *reinterpret_cast<const f32x4*>(p.bias_m + 4 * idx) : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   int staged = t_begin / p.tiles_per_img;
   stage_m(staged);
@@ -768,14 +682,14 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
     if constexpr (KG < 6) load_rows(p.R, p.ldr, r_bytes, tile, xr);
     if constexpr (PFV) load_rows(p.A, p.lda, a_bytes, min(tile + 1, t_end - 1), an);  // next tile's v
     {
-      f32x4 acc1[2 * KG][kGemmRT];  // (hi, lo) accumulator pairs of the KG real x1 tiles
+      f32x4 acc1[KG][kGemmRT];
 #pragma unroll
-      for (int t = 0; t < 2 * KG; ++t)
+      for (int t = 0; t < KG; ++t)
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r) acc1[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_chunk<2 * KG, KG>(ml, KG, lane, a, acc1);
+      mfma_chunk<KG, KG>(ml, KG, lane, a, acc1);
       if constexpr (KG >= 6) load_rows(p.R, p.ldr, r_bytes, tile, xr);
-      const f32x4* bm = ml + 2 * KG * KG * 64;
+      const f32x4* bm = ml + KG * KG * 64;
       const __amdgpu_buffer_rsrc_t r1 = buf_rsrc(p.out1 + (long long)b * HW * p.ldo1, o1_bytes);
 #pragma unroll
       for (int r = 0; r < kGemmRT; ++r) {
@@ -783,14 +697,14 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
         const unsigned off = pix < (unsigned)HW ? pix * (unsigned)p.ldo1 * 4u + 16u * lq : o1_bytes;
 #pragma unroll
         for (int g = 0; g < KG; ++g) {
-          f32x4 v = (acc1[2 * g][r] + acc1[2 * g + 1][r]) + bm[4 * g + lq];
+          f32x4 v = acc1[g][r] + bm[4 * g + lq];
           v += xr[r][g];
           a[r][g] = v;
           buf_store4(r1, off + 64u * g, v);
         }
       }
     }
-    apply_ln<KG>(p, b, row0, li, HW, a, lnl, p.ln_b ? lnl + KG * 4 : nullptr);
+    apply_ln<KG>(p, b, row0, li, HW, a);
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
     unsigned vo[kGemmRT];
 #pragma unroll
@@ -830,11 +744,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
 //   16 x NT x KG MFMAs on this step's operands; at a tile's last k-chunk the epilogue.
 // r01's version staged each weight chunk through VGPRs behind two __syncthreads and loaded A only
 // after them, so every k-chunk exposed two memory latencies with both waves of a SIMD parked.
-// DUAL (OUT 0, 1x1): tiles (2u, 2u + 1) of a chunk are the hi / lo halves of real tile (chunk base +
-// 2u) / 2 (GemmParams::dual), stored once as (hi + lo) + bias + R.
-template <int NT, int KG, bool CONV3, int OUT, bool HASR, bool DUAL = false>
+template <int NT, int KG, bool CONV3, int OUT, bool HASR>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams p) {
-  static_assert(!DUAL || (OUT == 0 && !CONV3 && NT % 2 == 0), "dual: plain 1x1 stores, tile pairs");
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
   constexpr int SLOT = NT * KG * 64;                  // f32x4 per weight slot
   constexpr int PIECES = NT * KG;                     // 1 KiB records per chunk
@@ -847,21 +758,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
   if (t_begin >= t_end) return;
   const int nc = blockIdx.y;
   const int KC = p.kchunks;
-  const bool LN = !CONV3 && p.ln;  // (no implicit conv is LayerNorm'd: the LN code stays out of those)
   f32x4* bias_l = wlds + 2 * SLOT;
   for (int idx = tid; idx < NT * 4; idx += kGemmThreads) {
     const int n = nc * NT * 16 + 4 * idx;
     bias_l[idx] = (p.bias && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  // LN affine of the whole K: [kgroups * 4] weights, then [kgroups * 4] biases (ln GEMMs only)
-  // (zero-padded to whole k-chunks, so the last chunk's padding groups need no test)
-  f32x4* lnl = bias_l + NT * 4;
-  const int kgp = KC * KG;
-  if (LN)
-    for (int idx = tid; idx < 2 * kgp * 4; idx += kGemmThreads) {
-      const int half = idx / (kgp * 4), q = idx - half * kgp * 4;
-      lnl[idx] = q < p.kgroups * 4 ? ln_affine_at(p, half, q) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
   const unsigned w_bytes = (unsigned)p.ntiles * (unsigned)p.kgroups * 1024u;
   const unsigned a_bytes = (unsigned)HW * (unsigned)p.lda * 4u;
   // weights of step (tile, kc) -> slot; record (t, g) of the chunk = packed record (nc*NT + t, kc*KG + g)
@@ -931,11 +832,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
       st[r] = *reinterpret_cast<const float2*>(p.stats + 2 * ((long long)b * HW + prow));
     }
   };
-  auto ln_apply = [&](int kc, int b, int row0, const float2 (&st)[kGemmRT], f32x4 (&x)[kGemmRT][KG]) {
-    const f32x4* lw = lnl + kc * KG * 4;
-    const f32x4* lb = p.ln_b ? lnl + kgp * 4 + kc * KG * 4 : nullptr;
+  auto ln_apply = [&](int b, int row0, const float2 (&st)[kGemmRT], f32x4 (&x)[kGemmRT][KG]) {
     if (!p.stats) {
-      apply_ln<KG>(p, b, row0, li, HW, x, lw, lb);
+      apply_ln<KG>(p, b, row0, li, HW, x);
       return;
     }
     const float wb = (p.ln == 2) ? 1.f : 0.f;
@@ -943,7 +842,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
     for (int r = 0; r < kGemmRT; ++r)
 #pragma unroll
       for (int g = 0; g < KG; ++g) x[r][g] = (x[r][g] - st[r].x * wb) * st[r].y;
-    ln_affine<KG>(x, lw, lb);
   };
   f32x4 a[kGemmRT][KG], an[kGemmRT][KG];
   f32x4 acc[NT][kGemmRT];
@@ -969,54 +867,38 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
     float2 st[kGemmRT];
     for (int kc = 0; kc + 1 < KC; ++kc) {
       begin_step();
-      if (LN) load_stats(b, row0, st);
+      if (p.ln) load_stats(b, row0, st);
       issue_w(tile, kc + 1, slot ^ 1);
       load_a2(tile, kc + 1, an);
-      if (LN) ln_apply(kc, b, row0, st, a);
+      if (p.ln) ln_apply(b, row0, st, a);
       mfma_chunk<NT, KG>(wlds + slot * SLOT, KG, lane, a, acc);
       slot ^= 1;
     }
     // last k-chunk: residual loads, then the next tile's first operands (clamped, so the count of
     // memory ops is the same on every path), MFMAs, epilogue
     begin_step();
-    if (LN) load_stats(b, row0, st);
+    if (p.ln) load_stats(b, row0, st);
     [[maybe_unused]] f32x4 res[NT][kGemmRT];
     if constexpr (HASR && OUT == 0) {
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<float*>(p.R + (long long)b * HW * p.ldr), 0, (int)((unsigned)HW * (unsigned)p.ldr * 4u), 0x00020000);
 #pragma unroll
-      for (int t = 0; t < NT; t += (DUAL ? 2 : 1)) {
-        const int nq = (DUAL ? ((nc * NT + t) >> 1) * 16 : (nc * NT + t) * 16) + 4 * lq;
-        const int nlim = DUAL ? p.N / 2 : p.N;  // (DUAL: real channels)
+      for (int t = 0; t < NT; ++t) {
+        const int nq = (nc * NT + t) * 16 + 4 * lq;
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r) {
           const int pl = row0 + r * 16 + li;
-          res[t][r] = buf_load4(rr, (pl < HW && nq < nlim) ? (unsigned)(pl * p.ldr + nq) * 4u : kOOB);
+          res[t][r] = buf_load4(rr, (pl < HW && nq < p.N) ? (unsigned)(pl * p.ldr + nq) * 4u : kOOB);
         }
       }
     }
     const int ntile = min(tile + 1, t_end - 1);
     issue_w(ntile, 0, slot ^ 1);
     load_a2(ntile, 0, an);
-    if (LN) ln_apply(KC - 1, b, row0, st, a);
+    if (p.ln) ln_apply(b, row0, st, a);
     mfma_chunk<NT, KG>(wlds + slot * SLOT, KG, lane, a, acc);
     slot ^= 1;
-    if constexpr (DUAL) {
-      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-          p.out + (long long)b * HW * p.ldo, 0, (int)((unsigned)HW * (unsigned)p.ldo * 4u), 0x00020000);
-#pragma unroll
-      for (int t = 0; t < NT; t += 2) {
-        const int nq = ((nc * NT + t) >> 1) * 16 + 4 * lq;  // real channels
-        const f32x4 bias = bias_l[4 * t + lq];
-#pragma unroll
-        for (int r = 0; r < kGemmRT; ++r) {
-          const int pl = row0 + r * 16 + li;
-          f32x4 v = (acc[t][r] + acc[t + 1][r]) + bias;
-          if constexpr (HASR) v += res[t][r];
-          buf_store4(ro, (pl < HW && 2 * nq < p.N) ? (unsigned)(pl * p.ldo + nq) * 4u : kOOB, v);
-        }
-      }
-    } else if constexpr (OUT == 0) {
+    if constexpr (OUT == 0) {
       const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
           p.out + (long long)b * HW * p.ldo, 0, (int)((unsigned)HW * (unsigned)p.ldo * 4u), 0x00020000);
       const float relu_floor = p.relu ? 0.f : -__builtin_huge_valf();
@@ -1100,23 +982,6 @@ static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, si
 template <int NT, int KG, int NCH>
 constexpr bool res2_hasr_ok() { return NT * NCH <= 12 && NT * NCH * KG <= 72 && KG <= 8; }
 
-// hi / lo (GemmParams::dual) instances: the C = 96 attention projection (12 virtual tiles, KG 6)
-template <int NCH>
-static hipError_t launch_res2_dual(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
-  static size_t attr_lds[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (lds > attr_lds[dev]) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_res_kernel<6, 6, NCH, 2, true, true, true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr_lds[dev] = lds;
-  }
-  hipLaunchKernelGGL((gemm_res_kernel<6, 6, NCH, 2, true, true, true>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds,
-                     s, p);
-  return hipGetLastError();
-}
-
 template <int NT, int KG, int NCH, bool PF>
 static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
   constexpr bool RK = res2_hasr_ok<NT, KG, NCH>();
@@ -1155,9 +1020,7 @@ static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_
   X(4, 4, false, 2) X(8, 4, false, 2) X(4, 2, false, 2) X(3, 3, false, 2)
 
 // (NT, KG, NCH) of the fused attention-output + project_in kernel (C = 48: K = 3 groups)
-// (r04: the (8, 6, 2) entry of the retired C = 96 "attn_in_split" schedule no longer fits the LDS with
-// hi / lo M tiles)
-#define KDLAE_GEMM_ATTN_IN_VARIANTS(X) X(8, 3, 2) X(9, 3, 2) X(6, 3, 3)
+#define KDLAE_GEMM_ATTN_IN_VARIANTS(X) X(8, 3, 2) X(9, 3, 2) X(6, 3, 3) X(8, 6, 2)
 
 bool gemm_attn_in_variant(int NT, int KG, int nch) {
 #define X(a, b, c) \
@@ -1175,26 +1038,9 @@ bool gemm_has_variant2(int NT, int KG, bool conv3, int out_mode) {
   return false;
 }
 
-static hipError_t launch_chunk2_dual(const GemmParams& p, int grid_x, int grid_y, hipStream_t s) {
-  const size_t lds = (size_t)2 * 6 * 6 * 1024 + (size_t)6 * 64;
-  static size_t attr_lds[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (lds > attr_lds[dev]) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_chunk_kernel<6, 6, false, 0, true, true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr_lds[dev] = lds;
-  }
-  hipLaunchKernelGGL((gemm_chunk_kernel<6, 6, false, 0, true, true>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s,
-                     p);
-  return hipGetLastError();
-}
-
 template <int NT, int KG, bool C3, int OUT>
 static hipError_t launch_chunk2(const GemmParams& p, int grid_x, int grid_y, hipStream_t s) {
-  // two weight slots, the bias of the chunk's tiles, the LN affine of the whole K (LN GEMMs)
-  const size_t lds = (size_t)2 * NT * KG * 1024 + (size_t)NT * 64 + (p.ln && !C3 ? (size_t)p.kchunks * KG * 128 : 0);
+  const size_t lds = (size_t)2 * NT * KG * 1024 + (size_t)NT * 64;
   static size_t attr_lds[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
@@ -1226,30 +1072,9 @@ hipError_t launch_gemm_route(const GemmParams& p, int NT, int KG, int wpe, int g
   const bool c3 = p.ksize == 3;
   const bool res = p.group_tiles > 0;
   if (p.ln && !p.stats && (p.kchunks > 1 || p.kgroups > KG)) return hipErrorInvalidValue;  // LN needs whole rows
-  if (p.dual) {  // hi / lo attention projection (attn_fold): the two kernels that pair tiles
-    const long long HW = (long long)p.F * p.H * p.W;
-    const long long mx = HW * std::max({p.lda, p.ldo, p.ldr}) * 4;
-    if (route != 0 || c3 || p.out_mode || p.relu || p.ln || !p.R || p.Wm || p.ntiles % 2 || p.N != 16 * p.ntiles ||
-        p.lda % 4 || p.ldo % 4 || p.ldr % 4 || mx >= (1LL << 31) || NT != 6 || KG != 6)
-      return hipErrorInvalidValue;
-    if (res) {
-      const int nch = (p.group_tiles + NT - 1) / NT;
-      const int grid_y = (p.ntiles + p.group_tiles - 1) / p.group_tiles;
-      const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64 + (size_t)KG * 128;
-      if (p.kgroups != 6 || p.kchunks != 1 || p.group_tiles % 2 || lds > 160 * 1024) return hipErrorInvalidValue;
-      if (nch == 1) return launch_res2_dual<1>(p, grid_x, grid_y, lds, s);
-      if (nch == 2) return launch_res2_dual<2>(p, grid_x, grid_y, lds, s);
-      if (nch == 3) return launch_res2_dual<3>(p, grid_x, grid_y, lds, s);
-      return hipErrorInvalidValue;
-    }
-    if ((long long)p.ntiles * p.kgroups * 1024 >= (1LL << 31)) return hipErrorInvalidValue;
-    return launch_chunk2_dual(p, grid_x, (p.ntiles + NT - 1) / NT, s);
-  }
   if (p.Wm) {  // fused attention output + LN + GEMM: one resident group, K = N of the M GEMM = C
     const int nch = (p.ntiles + NT - 1) / NT;
-    // project_in weights + bias; M (hi / lo virtual tiles) + bias_m; the LN affine
-    const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64 + (size_t)2 * KG * KG * 1024 +
-                       (size_t)KG * 64 + (size_t)KG * 128;
+    const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64 + (size_t)KG * KG * 1024 + (size_t)KG * 64;
     const long long HW = (long long)p.F * p.H * p.W;
     const long long mx = HW * std::max({p.lda, p.ldo, p.ldr, p.ldo1}) * 4;
     if (!res || c3 || p.out_mode || p.group_tiles < p.ntiles || p.kgroups != KG || p.kchunks != 1 || p.relu ||
@@ -1279,7 +1104,7 @@ hipError_t launch_gemm_route(const GemmParams& p, int NT, int KG, int wpe, int g
     const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;
     const int nch = (p.group_tiles + NT - 1) / NT;
     const int grid_y = (p.ntiles + p.group_tiles - 1) / p.group_tiles;
-    const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64 + (size_t)KG * 128;  // + LN affine
+    const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64;
     // residual variants keep NT x 2 residual float4 live across the chunk's MFMAs: only where that
     // fits the 256-VGPR budget without spills (hipcc -Rpass-analysis), else the r01 kernel
     const bool res_ok = !p.R || (NT * nch <= 12 && NT * nch * KG <= 72 && KG <= 8 && p.ldr % 4 == 0);  // no VGPR spills

@@ -32,6 +32,10 @@ struct BlockW {
   size_t dwffn = kNone, dwffn_b = kNone;
   bool fused_gdfn = false;  // project_in output chunk-interleaved; dwconv+gate+project_out in one kernel
   bool fused_attn_in = false;  // x1 = x + M v, LN and project_in in one GEMM kernel (gemm_attn_in_kernel)
+  // when project_in needs two resident weight groups (C = 96): the fused kernel runs group 0 (and
+  // forms x1), a plain LN GEMM on x1 runs group 1
+  bool attn_in_split = false;
+  Gemm pin_g0, pin_g1;
 };
 
 }  // namespace kdlae
@@ -175,10 +179,8 @@ struct Packer {
     return prog.add(pack_fragments(ntiles, kgroups, Wf));
   }
 
-  // 1x1 conv [Cout][Cin]; with ln_prefix the GEMM applies that LayerNorm to its A rows, affine
-  // included (the weight and bias are NOT folded into W: a rounded fold is one perturbation shared by
-  // every pixel, profiles/r04_config1_taps.txt).  row_map(n) -> source output row or -1 (padding);
-  // stored N = nstore.
+  // 1x1 conv [Cout][Cin] with optional LN(weight, bias) folded on the input side.
+  // row_map(n) -> source output row or -1 (padding); stored N = nstore.
   template <class RowMap>
   Gemm pointwise(const std::string& name, int Cout, int Cin, int Kpad, int nstore, RowMap row_map,
                  const std::string& ln_prefix, bool conv_bias, bool prefer_single_k) {
@@ -199,24 +201,29 @@ struct Packer {
       if (n >= nstore || k >= Cin) return PEx{};
       const int src = row_map(n);
       if (src < 0) return PEx{};
-      return PEx{W + src * Cin + k, -1};
+      return PEx{W + src * Cin + k, lnw >= 0 ? lnw + k : -1};
     });
-    if (cb >= 0) {
+    if (cb >= 0 || lnb >= 0) {
+      // bias' = conv bias + W . ln_bias (the WithBias LN shift pushed through the 1x1 conv)
       std::vector<PEx> bv((size_t)g.ntiles * 16);
-      for (int n = 0; n < nstore; ++n) {
-        const int src = row_map(n);
-        if (src >= 0) bv[n].a = cb + src;
-      }
+      if (lnb < 0)
+        for (int n = 0; n < nstore; ++n) {
+          const int src = row_map(n);
+          if (src >= 0) bv[n].a = cb + src;
+        }
       g.bias = prog.add(bv);
-    }
-    if (lnw >= 0) {
-      std::vector<PEx> wv((size_t)Kpad), bv((size_t)Kpad);
-      for (int k = 0; k < Cin; ++k) {
-        wv[k].a = lnw + k;
-        if (lnb >= 0) bv[k].a = lnb + k;
-      }
-      g.ln_w = prog.add(wv);
-      if (lnb >= 0) g.ln_b = prog.add(bv);
+      if (lnb >= 0)
+        for (int n = 0; n < nstore; ++n) {
+          const int src = row_map(n);
+          if (src < 0) continue;
+          PDot d;
+          d.dst = (int64_t)g.bias + n;
+          d.base = cb >= 0 ? cb + src : -1;
+          d.w = W + src * Cin;
+          d.v = lnb;
+          d.K = Cin;
+          prog.dots.push_back(d);
+        }
     }
     choose_variant(g, prefer_single_k);
     return g;
@@ -285,26 +292,15 @@ struct Packer {
     b.proj = prog.copy(pw, (size_t)C * C);
     if (pb >= 0) b.proj_b = prog.copy(pb, C);
     b.temp = prog.copy(tp, heads);
-    // x += M v with M = W_proj blockdiag(A) as hi / lo virtual tiles (attn_fold, GemmParams::dual):
-    // 2 C / 16 tiles, the bias on the even (hi) ones
-    b.proj_gemm.dual = true;
-    b.proj_gemm.ntiles = 2 * C / 16;
+    b.proj_gemm.ntiles = C / 16;
     b.proj_gemm.kgroups = C / 16;
-    b.proj_gemm.N = 2 * C;
+    b.proj_gemm.N = C;
     b.proj_gemm.K = C;
     b.proj_gemm.n_true = C;
     b.proj_gemm.k_true = C;
-    if (pb >= 0) {
-      std::vector<PEx> v((size_t)2 * C);
-      for (int n = 0; n < C; ++n) v[(size_t)(n / 16) * 32 + (n % 16)].a = pb + n;
-      b.proj_gemm.bias = prog.add(v);
-    }
+    b.proj_gemm.bias = b.proj_b;
     b.proj_gemm.has_res = true;
-    b.proj_gemm.NT = 6;
-    b.proj_gemm.KG = 6;
-    b.proj_gemm.WPE = 2;
-    // resident (whole K in one group) where the dual kernel has the KG = 6 body: C = 96; else chunked
-    b.proj_gemm.group_tiles = b.proj_gemm.kgroups == 6 ? b.proj_gemm.ntiles : 0;
+    choose_variant(b.proj_gemm, true);
     // FFN: project_in rows [x1 (hid) | x2 (hid)].  Unfused: stored [x1 padded to hidS | x2 padded
     // to hidS] for the gate kernel.  Fused (gdfn.hip): chunk-interleaved, 16 channels of x1 then the
     // same 16 of x2 per 32-channel chunk, so each chunk of a pixel is one 128 B line.
@@ -351,6 +347,26 @@ struct Packer {
     const bool no_ai = debug_flag("no_attn_in_fusion");
     b.fused_attn_in = b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 && b.pin.WPE == 2 &&
                       gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.ntiles + b.pin.NT - 1) / b.pin.NT) && !no_ai;
+    // C = 96 (two weight groups): the fused kernel on group 0 + a plain LN GEMM on group 1 measured a
+    // wash (profiles/r02_attn_in_probe.txt: 4637 vs 4598 us at 512^2), so it stays behind the
+    // attn_in_split debug flag (bit-identity test)
+    if (!b.fused_attn_in && !no_ai && debug_flag("attn_in_split") && b.pin.group_tiles > 0 &&
+        b.pin.group_tiles < b.pin.ntiles && 2 * b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 &&
+        b.pin.WPE == 2 && gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.group_tiles + b.pin.NT - 1) / b.pin.NT)) {
+      const int gt = b.pin.group_tiles;
+      b.pin_g0 = b.pin;
+      b.pin_g0.ntiles = gt;
+      b.pin_g0.N = 16 * gt;
+      b.pin_g0.n_true = (int)((long long)b.pin.n_true * gt / b.pin.ntiles);
+      b.pin_g1 = b.pin;
+      b.pin_g1.w = b.pin.w + (size_t)gt * b.pin.kgroups * 256;
+      if (b.pin.bias != kNone) b.pin_g1.bias = b.pin.bias + (size_t)16 * gt;
+      b.pin_g1.ntiles = b.pin.ntiles - gt;
+      b.pin_g1.N = b.pin.N - 16 * gt;
+      b.pin_g1.n_true = b.pin.n_true - b.pin_g0.n_true;
+      b.pin_g1.group_tiles = b.pin_g1.ntiles;
+      b.fused_attn_in = b.attn_in_split = true;
+    }
     return b;
   }
 
@@ -423,8 +439,8 @@ static Plan make_plan(const kdlae_t_handle* h, int B, int H, int W) {
       if (!b.fused_gdfn) mfg = std::max(mfg, P * b.hidS);  // gated tensor: unfused FFN tails only
       mst = std::max(mst, P * 2);
       mpart = std::max(mpart, (long long)B * b.heads * nslots_for(Hh, Ww, B, b.heads) * slot);
-      mred = std::max(mred, 2LL * B * b.heads * slot);  // float64 slot sums
-      mM = std::max(mM, 2LL * B * b.C * b.C);           // M as hi / lo
+      mred = std::max(mred, (long long)B * b.heads * slot);
+      mM = std::max(mM, (long long)B * b.C * b.C);
     }
   };
   acc(h->enc1, P1, H, W);
@@ -505,8 +521,6 @@ struct Fwd {
     c.ldr = ldr;
     c.ln = ln;
     c.ln_C = ln_C;
-    c.ln_w = h->P(g.ln_w);
-    c.ln_b = h->P(g.ln_b);
     c.stats_buf = buf(pl.stats);
     int rc = probe_begin(1, probeC);
     if (rc) return rc;
@@ -554,14 +568,13 @@ struct Fwd {
     tag = "gram C" + std::to_string(b.C) + " Ch" + std::to_string(b.Ch) + " HW" + std::to_string(HW);
     HIPCHK(launch_dwconv_gram(gp, s));
     if ((rc = probe_end(2, b.C, 4.0 * P * 4 * b.C, 2.0 * P * (27.0 * b.C + (double)b.C * b.Ch)))) return rc;
-    double* red = reinterpret_cast<double*>(buf(pl.red));
-    HIPCHK(launch_gram_reduce(gp.partial, red, B, b.heads, gp.nslots, gp.slot_floats, true, s));
-    HIPCHK(launch_attn_fold(red, gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
+    HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
+    HIPCHK(launch_attn_fold(buf(pl.red), gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
     View fpre{buf(pl.fpre), 2 * b.hidS};
     const bool fuse_in = b.fused_attn_in;
     if (fuse_in) {
       // x1 = x + M v written back into x, LN(x1) -> project_in into fpre, one kernel
-      const Gemm& g0 = b.pin;
+      const Gemm& g0 = b.attn_in_split ? b.pin_g0 : b.pin;
       GemmCall c;
       c.g = &g0;
       c.W = h->P(g0.w);
@@ -576,11 +589,9 @@ struct Fwd {
       c.ldr = x.ld;
       c.ln = ln;
       c.ln_C = b.C;
-      c.ln_w = h->P(g0.ln_w);
-      c.ln_b = h->P(g0.ln_b);
       c.stats_buf = buf(pl.stats);
       c.Wm = buf(pl.Mp);
-      c.wm_img_stride = 2LL * b.C * b.C;  // hi / lo virtual tiles
+      c.wm_img_stride = (long long)b.C * b.C;
       c.bias_m = h->P(b.proj_b);
       c.out1 = x;
       if ((rc = probe_begin(1, b.C))) return rc;
@@ -594,8 +605,13 @@ struct Fwd {
       const double bytes = 4.0 * (Pd * 3.0 * b.C + Pd * g0.n_true + (double)B * b.C * b.C +
                                   (double)g0.n_true * b.C);
       if ((rc = probe_end(1, b.C, bytes, 2.0 * Pd * ((double)b.C * b.C + (double)b.C * g0.n_true)))) return rc;
+      if (b.attn_in_split) {  // project_in's second weight group on x1 (now in x)
+        rc = gemm(b.pin_g1, h->P(b.pin_g1.w), 0, x, Hh, Ww, View{fpre.p + 16 * b.pin_g0.ntiles, fpre.ld}, 0, nullptr,
+                  0, ln, b.C, b.C);
+        if (rc) return rc;
+      }
     } else {
-      rc = gemm(b.proj_gemm, buf(pl.Mp), 2LL * b.C * b.C, View{buf(pl.vbuf), b.C}, Hh, Ww, x, 0, x.p, x.ld, 0,
+      rc = gemm(b.proj_gemm, buf(pl.Mp), (long long)b.C * b.C, View{buf(pl.vbuf), b.C}, Hh, Ww, x, 0, x.p, x.ld, 0,
                 0, b.C);
       if (rc) return rc;
     }

@@ -46,16 +46,6 @@ struct GemmParams {
   // :160), stores x1 to out1, and runs LN + the GEMM on x1 (:161, :99) — x1 never round-trips HBM
   const float* Wm; long long wm_img_stride; const float* bias_m;
   float* out1; int ldo1;
-  // LayerNorm affine (ln != 0): y = LN(x) * ln_w (+ ln_b, WithBias) applied per element in the A
-  // prologue, as the reference does (KDLAE_model.py:52, :70) — not folded into W, whose rounding
-  // would be a perturbation shared by every pixel (config-1 analysis, profiles/r04_config1_taps.txt).
-  // [kgroups * 16] floats, zero past ln_C; ln_b may be null (BiasFree).
-  const float* ln_w; const float* ln_b;
-  // hi/lo weights (attention projection M = W_proj blockdiag(A), attn_fold): the packed weights hold
-  // 2 x (N / 2) output tiles, tile 2t = fl(M_t), tile 2t + 1 = fl(M_t - fl(M_t)); the kernel stores
-  // (acc_2t + acc_2t+1) + bias + R into real tile t.  N, ntiles and bias count the virtual tiles
-  // (bias: real values on the even tiles, zeros on the odd ones).
-  int dual;
 };
 
 struct GramParams {
@@ -115,12 +105,9 @@ bool gemm_has_variant2(int NT, int KG, bool conv3, int out_mode);  // r02 chunke
 hipError_t launch_ln_stats(const float* x, int ld, int C, long long P, float* stats, hipStream_t s);
 hipError_t launch_dwconv_gram(const GramParams& p, hipStream_t s);
 hipError_t launch_dwconv_gram_route(const GramParams& p, int route, hipStream_t s);  // 2: generic kernel
-// reduced: float (f64 == false, the self-test) or double (f64 == true, what attn_fold reads)
-hipError_t launch_gram_reduce(const float* partial, void* reduced, int Bn, int heads, int nslots,
-                              int slot_floats, bool f64, hipStream_t s);
-// A = softmax(temp G / (|q| |k|^T)) and M = W_proj blockdiag(A) in float64 from the f64 reduced Gram,
-// written as hi/lo virtual tiles (GemmParams::dual) in fragment order: [2 C/16][C/16][64][4] per image
-hipError_t launch_attn_fold(const double* reduced, int slot_floats, const float* proj, const float* temp,
+hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int heads, int nslots,
+                              int slot_floats, hipStream_t s);
+hipError_t launch_attn_fold(const float* reduced, int slot_floats, const float* proj, const float* temp,
                             float* Mpacked, int Bn, int C, int heads, hipStream_t s);
 hipError_t launch_dwconv_gate(const GateParams& p, hipStream_t s);
 hipError_t launch_conv_small_in(const SmallInParams& p, hipStream_t s);

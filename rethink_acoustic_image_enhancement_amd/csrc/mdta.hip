@@ -637,14 +637,12 @@ hipError_t launch_dwconv_gram_route(const GramParams& p, int route, hipStream_t 
 // f32 q.k^T over all HW pixels is what puts the reference's own f32 output 3e-3 from its f64 output
 // on the config-1 MDD input, profiles/r03_config1_precision.txt): wave w of a block sums the
 // slot range [w n / 8, (w+1) n / 8) sequentially for 64 consecutive floats (one 256 B line per
-// load), then lane i adds the 8 wave sums in wave order; the result stays float64 for attn_fold (the
-// self-test entry point asks for f32).  Deterministic and batch-invariant (the slot partition depends
-// on the image size only).  r01's kernel gave each float one thread that
+// load), then lane i adds the 8 wave sums in wave order.  Deterministic and batch-invariant (the
+// slot partition depends on the image size only).  r01's kernel gave each float one thread that
 // walked all slots (160 blocks at 1024^2: a latency-bound 64 us per launch).
 constexpr int kRedWaves = 8;
-template <typename OutT>
 __global__ __launch_bounds__(64 * kRedWaves) void gram_reduce_kernel(const float* __restrict__ partial,
-                                                                     OutT* __restrict__ reduced, int nslots,
+                                                                     float* __restrict__ reduced, int nslots,
                                                                      int slot_floats) {
   __shared__ double part[kRedWaves][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -663,42 +661,31 @@ __global__ __launch_bounds__(64 * kRedWaves) void gram_reduce_kernel(const float
     double t = part[0][lane];
 #pragma unroll
     for (int w = 1; w < kRedWaves; ++w) t += part[w][lane];
-    reduced[bh * slot_floats + idx] = (OutT)t;
+    reduced[bh * slot_floats + idx] = (float)t;
   }
 }
 
-hipError_t launch_gram_reduce(const float* partial, void* reduced, int Bn, int heads, int nslots,
-                              int slot_floats, bool f64, hipStream_t s) {
+hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int heads, int nslots,
+                              int slot_floats, hipStream_t s) {
   dim3 grid((slot_floats + 63) / 64, Bn * heads);
-  if (f64)
-    hipLaunchKernelGGL(gram_reduce_kernel<double>, grid, dim3(64 * kRedWaves), 0, s, partial,
-                       static_cast<double*>(reduced), nslots, slot_floats);
-  else
-    hipLaunchKernelGGL(gram_reduce_kernel<float>, grid, dim3(64 * kRedWaves), 0, s, partial,
-                       static_cast<float*>(reduced), nslots, slot_floats);
+  hipLaunchKernelGGL(gram_reduce_kernel, grid, dim3(64 * kRedWaves), 0, s, partial, reduced, nslots, slot_floats);
   return hipGetLastError();
 }
 
 // --------------------------------------------------------------------------- softmax + fold
 // grid (C/16, heads, B).  Each block rebuilds A for (b, h) in LDS, then computes 16 rows of
 // M[n][h*Ch + c2] = sum_c1 Wproj[n][h*Ch + c1] * A[c1][c2], stored in fragment order.
-// Everything here is float64: the logits S = temp G / (|q| |k|^T) from the f64 slot sums, the softmax
-// and M.  M is applied to every pixel of the image, so its rounding is a perturbation shared by all
-// of them; on the ill-conditioned config-1 input such shared perturbations (M rounded to f32, or the
-// LN weight folded into W) each moved the output ~1e-3 (profiles/r04_config1_taps.txt).  M therefore
-// leaves as an unevaluated sum hi + lo of two f32 (dual virtual tiles: 2t = hi, 2t + 1 = lo, see
-// GemmParams::dual), whose MFMA products are summed per pixel: the shared error drops to ~2^-48.
-__global__ __launch_bounds__(256) void attn_fold_kernel(const double* __restrict__ reduced, int slot_floats,
+__global__ __launch_bounds__(256) void attn_fold_kernel(const float* __restrict__ reduced, int slot_floats,
                                                         const float* __restrict__ proj,
                                                         const float* __restrict__ temp,
                                                         float* __restrict__ Mp, int C, int heads) {
-  extern __shared__ double smd[];
+  extern __shared__ float sm[];
   const int Ch = C / heads;
   const int CT = Ch / 16;
-  double* A = smd;                  // [Ch][Ch + 1]
-  double* nrm = smd + Ch * (Ch + 1);  // [2 Ch]: 1/max(|q|,eps), 1/max(|k|,eps)
+  float* A = sm;                  // [Ch][Ch + 1]
+  float* nrm = sm + Ch * (Ch + 1);  // [2 Ch]: 1/max(|q|,eps), 1/max(|k|,eps)
   const int nb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const double* G = reduced + ((long long)b * heads + h) * slot_floats;
+  const float* G = reduced + ((long long)b * heads + h) * slot_floats;
   const int ldA = Ch + 1;
   // decode the accumulator layout: G[(i*CT + j)*256 + lane*4 + e] = Gram[16i + 4(lane>>4) + e][16j + (lane&15)]
   for (int idx = threadIdx.x; idx < CT * CT * 256; idx += 256) {
@@ -707,57 +694,48 @@ __global__ __launch_bounds__(256) void attn_fold_kernel(const double* __restrict
     A[(16 * i + 4 * (lane >> 4) + e) * ldA + 16 * j + (lane & 15)] = G[idx];
   }
   for (int c = threadIdx.x; c < 2 * Ch; c += 256) {
-    const double n2 = G[CT * CT * 256 + c];
-    nrm[c] = 1.0 / fmax(sqrt(n2), 1e-12);
+    const float n2 = G[CT * CT * 256 + c];
+    nrm[c] = 1.0f / fmaxf(sqrtf(n2), 1e-12f);
   }
   __syncthreads();
-  const double tp = (double)temp[h];
+  const float tp = temp[h];
   for (int r = threadIdx.x; r < Ch; r += 256) {
-    double* row = A + r * ldA;
-    const double sq = nrm[r];
-    double mx = -INFINITY;
+    float* row = A + r * ldA;
+    const float sq = nrm[r];
+    float mx = -INFINITY;
     for (int c = 0; c < Ch; ++c) {
-      const double l = (row[c] * sq * nrm[Ch + c]) * tp;
+      const float l = (row[c] * sq * nrm[Ch + c]) * tp;
       row[c] = l;
-      mx = fmax(mx, l);
+      mx = fmaxf(mx, l);
     }
-    double sum = 0.0;
+    float sum = 0.f;
     for (int c = 0; c < Ch; ++c) {
-      const double e = exp(row[c] - mx);
+      const float e = expf(row[c] - mx);
       row[c] = e;
       sum += e;
     }
-    const double inv = 1.0 / sum;
+    const float inv = 1.0f / sum;
     for (int c = 0; c < Ch; ++c) row[c] *= inv;
   }
   __syncthreads();
   const int kgroups = C / 16;
-  float* Mb = Mp + (long long)b * 2 * C * C;
+  float* Mb = Mp + (long long)b * C * C;
   for (int idx = threadIdx.x; idx < 16 * Ch; idx += 256) {
     const int nl = idx / Ch, c2 = idx - (idx / Ch) * Ch;
     const int n = nb * 16 + nl;
     const float* wr = proj + (long long)n * C + h * Ch;
-    double s = 0.0;
-    for (int c1 = 0; c1 < Ch; ++c1) s = fma((double)wr[c1], A[c1 * ldA + c2], s);
-    const float hi = (float)s;
-    const float lo = (float)(s - (double)hi);
+    float s = 0.f;
+    for (int c1 = 0; c1 < Ch; ++c1) s = fmaf(wr[c1], A[c1 * ldA + c2], s);
     const int k = h * Ch + c2;
     const int lane = (n & 15) + 16 * ((k & 15) >> 2);
-    const long long rec = ((long long)(2 * (n >> 4)) * kgroups + (k >> 4)) * 64 + lane;
-    Mb[rec * 4 + (k & 3)] = hi;
-    Mb[(rec + (long long)kgroups * 64) * 4 + (k & 3)] = lo;  // virtual tile 2t + 1
+    Mb[(((long long)(n >> 4) * kgroups + (k >> 4)) * 64 + lane) * 4 + (k & 3)] = s;
   }
 }
 
-hipError_t launch_attn_fold(const double* reduced, int slot_floats, const float* proj, const float* temp,
+hipError_t launch_attn_fold(const float* reduced, int slot_floats, const float* proj, const float* temp,
                             float* Mpacked, int Bn, int C, int heads, hipStream_t s) {
   const int Ch = C / heads;
-  const size_t lds = (size_t)(Ch * (Ch + 1) + 2 * Ch) * sizeof(double);
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_fold_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
+  const size_t lds = (size_t)(Ch * (Ch + 1) + 2 * Ch) * sizeof(float);
   dim3 grid(C / 16, heads, Bn);
   hipLaunchKernelGGL(attn_fold_kernel, grid, dim3(256), lds, s, reduced, slot_floats, proj, temp, Mpacked,
                      C, heads);

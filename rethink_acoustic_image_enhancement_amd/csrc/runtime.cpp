@@ -52,8 +52,7 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
         if (!gemm_has_variant(nt, g.kgroups, false, w, true, g.out_mode)) continue;
         const long long padded = ceil_div(gt, nt) * nt;
         // weights (1 KiB per tile x k-group) + the group's bias (64 B per tile) must fit 160 KiB
-        // (+ the LN affine: 128 B per k-group)
-        if (padded * g.kgroups + ceil_div(padded, 16) + ceil_div(g.kgroups, 8) > (w == 4 ? 80 : 158)) continue;
+        if (padded * g.kgroups + ceil_div(padded, 16) > (w == 4 ? 80 : 158)) continue;
         // default policy: 2 waves/SIMD.  4 waves/SIMD used to win on the store-heavy K <= 48 shapes
         // while every epilogue load drained the stores; with that fixed, 2 waves measure 10-15%
         // faster on all of them (r01 probe: C48 project_in @1024^2 5864 -> 5099 us)
@@ -191,9 +190,6 @@ int run_gemm(const GemmCall& c, hipStream_t s) {
   p.bias_m = c.bias_m;
   p.out1 = c.out1.p;
   p.ldo1 = c.out1.ld;
-  p.ln_w = c.ln ? c.ln_w : nullptr;
-  p.ln_b = c.ln ? c.ln_b : nullptr;
-  p.dual = g.dual ? 1 : 0;
   p.stats = nullptr;
   if (c.ln && (p.kchunks > 1 || g.kgroups * 16 != c.ln_C)) {
     if (!c.stats_buf) return fail(KDLAE_ESTATE, "LN GEMM needs a stats buffer");

@@ -40,8 +40,6 @@ struct Gemm {
   int NT = 0, KG = 0, group_tiles = 0, WPE = 2;
   int n_true = 0, k_true = 0;  // un-padded sizes (FLOP accounting)
   bool has_res = false;         // launched with a residual epilogue (variant choice)
-  size_t ln_w = kNone, ln_b = kNone;  // LN affine applied in the A prologue ([K] floats; GemmParams::ln_w)
-  bool dual = false;            // hi / lo virtual tiles (GemmParams::dual)
 };
 struct SmallW {
   size_t w = kNone, bias = kNone;
@@ -171,8 +169,6 @@ struct GemmCall {
   int ldr = 0;
   int relu = 0;
   int ln = 0, ln_C = 0;
-  const float* ln_w = nullptr;  // LN weight / bias ([K] floats, ln_b null for BiasFree)
-  const float* ln_b = nullptr;
   float* stats_buf = nullptr;  // scratch [P][2] used when LN needs precomputed row stats
   // fused attention output (GemmParams::Wm): in = v, R = x, out1 = where x1 goes (x itself)
   const float* Wm = nullptr;

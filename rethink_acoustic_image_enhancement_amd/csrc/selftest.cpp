@@ -65,7 +65,7 @@ extern "C" int kdlae_debug_gemm(const kdlae_debug_gemm_desc* d, void* stream) {
   if (d->ksize == 3 && ((kt != 1 && kt != 3) || d->kgroups != 9 * kt * d->cg_per_tap || d->lda < 16 * d->cg_per_tap))
     return fail(KDLAE_EINVAL_SHAPE, "implicit conv needs kgroups = 9 kt cg_per_tap and lda >= 16 cg_per_tap");
   if (d->ksize == 1 && d->lda < 16 * d->kgroups) return fail(KDLAE_EINVAL_SHAPE, "lda < K");
-  if (d->out_mode == 0 && d->ldo < (d->dual ? d->N / 2 : d->N)) return fail(KDLAE_EINVAL_SHAPE, "ldo < N");
+  if (d->out_mode == 0 && d->ldo < d->N) return fail(KDLAE_EINVAL_SHAPE, "ldo < N");
   if (d->out_mode == 1 && (d->H % 2 || d->W % 2 || d->ldo < 4 * d->N)) return fail(KDLAE_EINVAL_SHAPE, "unshuffle geometry");
   if (d->out_mode == 2 && (d->N % 4 || d->ldo < d->N / 4)) return fail(KDLAE_EINVAL_SHAPE, "shuffle geometry");
   if (d->route != 0 && d->route != 1) return fail(KDLAE_EINVAL_CONFIG, "route must be 0 or 1");
@@ -104,9 +104,6 @@ extern "C" int kdlae_debug_gemm(const kdlae_debug_gemm_desc* d, void* stream) {
   p.bias_m = d->bias_m;
   p.out1 = d->out1;
   p.ldo1 = d->ldo1;
-  p.ln_w = d->ln_w;
-  p.ln_b = d->ln_b;
-  p.dual = d->dual;
   hipStream_t s = (hipStream_t)stream;
   if (d->ln && !d->Wm && (p.kchunks > 1 || d->kgroups * 16 != d->ln_C)) {
     if (!d->stats || d->ln_C > 512 || d->lda % 4) return fail(KDLAE_EINVAL_CONFIG, "chunked LN needs stats scratch");
@@ -156,7 +153,7 @@ extern "C" int kdlae_debug_gram(const kdlae_debug_gram_desc* d, void* stream) {
     return fail(KDLAE_EINVAL_SHAPE, "partial scratch too small");
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(kdlae::launch_dwconv_gram_route(p, d->route, s));
-  HIPCHK(kdlae::launch_gram_reduce(p.partial, d->reduced, d->Bn, d->heads, p.nslots, p.slot_floats, false, s));
+  HIPCHK(kdlae::launch_gram_reduce(p.partial, d->reduced, d->Bn, d->heads, p.nslots, p.slot_floats, s));
   return KDLAE_OK;
 }
 

@@ -1,0 +1,276 @@
+// KDLAE-S training kernels (gfx950): the data-movement and elementwise pieces of the student's
+// backward that are not GEMMs (kdlae_st.cpp sequences them around the training GEMM, train.hip).
+//
+// Activations are NDHWC: [B][F][H][W] pixels, channels contiguous at pixel stride ld.  The Conv3d
+// 3x3x3 (padding 1, KDLAE/KDLAE_model.py:386-393) goes through an explicit column matrix
+//   Xcol[p][c * 27 + tap],  tap = dt * 9 + dy * 3 + dx,  source pixel (f + dt - 1, y + dy - 1, x + dx - 1)
+// whose column order is the OIDHW weight's own ([Cout][Cin][3][3][3] = [Cout][Cin * 27]), so the forward
+// is Xcol . W^T, the weight gradient dZ^T . Xcol and the input gradient col2im(dZ . W).
+#include "train_kernels.h"
+#include "train_s.h"
+
+namespace kdlae {
+namespace train {
+
+namespace {
+
+struct Geo {
+  int B, F, H, W;
+  __device__ void coords(long long p, int& b, int& f, int& y, int& x) const {
+    x = (int)(p % W);
+    long long r = p / W;
+    y = (int)(r % H);
+    r /= H;
+    f = (int)(r % F);
+    b = (int)(r / F);
+  }
+};
+
+constexpr int kThreads = 256;
+
+inline unsigned grid_for(long long n, int per_block = kThreads) {
+  long long g = (n + per_block - 1) / per_block;
+  if (g > (1LL << 20)) g = 1LL << 20;  // grid-stride loops cover the rest
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+// one thread per column element (p, k), k fastest: coalesced Xcol writes
+__global__ __launch_bounds__(kThreads) void im2col3d_kernel(const float* __restrict__ x, int ldx, int C, Geo g,
+                                                            float* __restrict__ col) {
+  const int K = 27 * C;
+  const long long n = (long long)g.B * g.F * g.H * g.W * K;
+  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const long long p = i / K;
+    const int k = (int)(i - p * K);
+    const int c = k / 27, tap = k - c * 27;
+    int b, f, y, xx;
+    g.coords(p, b, f, y, xx);
+    const int ff = f + tap / 9 - 1, yy = y + (tap / 3) % 3 - 1, xs = xx + tap % 3 - 1;
+    float v = 0.f;
+    if ((unsigned)ff < (unsigned)g.F && (unsigned)yy < (unsigned)g.H && (unsigned)xs < (unsigned)g.W)
+      v = x[((((long long)b * g.F + ff) * g.H + yy) * g.W + xs) * ldx + c];
+    col[i] = v;
+  }
+}
+
+// dX[q][c] (+)= sum over taps of dcol[q - off(tap)][c * 27 + tap] (the pixels whose window put q at that
+// tap): a gather, so every dX element is written once, in a fixed order (deterministic, no atomics)
+__global__ __launch_bounds__(kThreads) void col2im3d_kernel(const float* __restrict__ dcol, int C, Geo g,
+                                                            float* __restrict__ dx, int lddx, int accumulate) {
+  const long long n = (long long)g.B * g.F * g.H * g.W * C;
+  const int K = 27 * C;
+  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const long long q = i / C;
+    const int c = (int)(i - q * C);
+    int b, f, y, x;
+    g.coords(q, b, f, y, x);
+    float s = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 27; ++tap) {
+      // source pixel p with p + off(tap) = q
+      const int pf = f - (tap / 9 - 1), py = y - ((tap / 3) % 3 - 1), px = x - (tap % 3 - 1);
+      if ((unsigned)pf < (unsigned)g.F && (unsigned)py < (unsigned)g.H && (unsigned)px < (unsigned)g.W) {
+        const long long p = (((long long)b * g.F + pf) * g.H + py) * g.W + px;
+        s += dcol[p * K + c * 27 + tap];
+      }
+    }
+    float* d = dx + q * lddx + c;
+    *d = accumulate ? *d + s : s;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void relu_kernel(float* __restrict__ y, int ld, int C, long long P) {
+  const long long n = P * C;
+  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const long long p = i / C;
+    float* v = y + p * ld + (i - p * C);
+    *v = fmaxf(*v, 0.f);
+  }
+}
+
+// dz = dy * (y > 0): ReLU backward (y is the ReLU output; y > 0 <=> the pre-activation > 0)
+__global__ __launch_bounds__(kThreads) void relu_mask_kernel(float* __restrict__ dy, int ldd, const float* __restrict__ y,
+                                                             int ldy, int C, long long P) {
+  const long long n = P * C;
+  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    if (!(y[p * ldy + c] > 0.f)) dy[p * ldd + c] = 0.f;
+  }
+}
+
+// MaxPool3d (1,2,2) backward (KDLAE_model.py:366): each pooled element's gradient goes to the first
+// maximal input of its 2 x 2 window in (row, column) order — PyTorch's tie rule (ReLU zeros tie often);
+// din = dskip (the same tensor's gradient through the decoder's skip add, or 0) + that routed gradient.
+__global__ __launch_bounds__(kThreads) void maxpool2_bwd_kernel(const float* __restrict__ in, int ldi,
+                                                                const float* __restrict__ dout, int ldo,
+                                                                const float* __restrict__ dskip, int lds,
+                                                                float* __restrict__ din, int ldd, int C, Geo lo) {
+  const long long n = (long long)lo.B * lo.F * lo.H * lo.W * C;
+  const int Wi = 2 * lo.W, Hi = 2 * lo.H;
+  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const long long pl = i / C;
+    const int c = (int)(i - pl * C);
+    int b, f, y, x;
+    lo.coords(pl, b, f, y, x);
+    const long long p0 = (((long long)b * lo.F + f) * Hi + 2 * y) * Wi + 2 * x;
+    const long long ps[4] = {p0, p0 + 1, p0 + Wi, p0 + Wi + 1};
+    int am = 0;
+    float mx = in[ps[0] * ldi + c];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      const float v = in[ps[j] * ldi + c];
+      if (v > mx || (v != v && mx == mx)) {
+        mx = v;
+        am = j;
+      }
+    }
+    const float g = dout[pl * ldo + c];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float base = dskip ? dskip[ps[j] * lds + c] : 0.f;
+      din[ps[j] * ldd + c] = base + (j == am ? g : 0.f);
+    }
+  }
+}
+
+// ConvTranspose3d (1,2,2) stride (1,2,2) epilogue (KDLAE_model.py:378-379, :416-417):
+// D[b, f, 2y + i, 2x + j, o] = U[b, f, y, x, 4 o + 2 i + j] + bias[o] + skip[b, f, 2y + i, 2x + j, o]
+__global__ __launch_bounds__(kThreads) void upshuffle_add_kernel(const float* __restrict__ U, int ldu,
+                                                                 const float* __restrict__ bias,
+                                                                 const float* __restrict__ skip, int lds,
+                                                                 float* __restrict__ D, int ldd, int C, Geo hi) {
+  const long long n = (long long)hi.B * hi.F * hi.H * hi.W * C;
+  const int Wl = hi.W / 2, Hl = hi.H / 2;
+  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const long long p = i / C;
+    const int o = (int)(i - p * C);
+    int b, f, y, x;
+    hi.coords(p, b, f, y, x);
+    const long long pl = (((long long)b * hi.F + f) * Hl + (y >> 1)) * Wl + (x >> 1);
+    float v = U[pl * ldu + 4 * o + 2 * (y & 1) + (x & 1)];
+    if (bias) v += bias[o];
+    v += skip[p * lds + o];
+    D[p * ldd + o] = v;
+  }
+}
+
+// L1LossForVideoFrames (Train/basicsr/models/losses/losses.py:409-526), pred / target [N][Cf][HW]:
+// part[blk] = (sum |p - t|, sum |bin(p) - bin(t)|, sum |(p_f+1 - p_f) - (t_f+1 - t_f)|), and the
+// gradient of  w_l1 (S_l1 + S_bin) / n1 + w_t S_t / n2  (torch.where's binarisation carries none;
+// d|u| = sign(u), sign(0) = 0)
+constexpr int kLossBlocks = 1024;
+__global__ __launch_bounds__(kThreads) void l1frames_kernel(const float* __restrict__ pred, const float* __restrict__ tgt,
+                                                            int N, int Cf, long long HW, float binary, float g1,
+                                                            float gt, float* __restrict__ dpred,
+                                                            float* __restrict__ part) {
+  const long long n = (long long)N * Cf * HW;
+  float s1 = 0.f, sb = 0.f, st = 0.f;
+  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const long long s = i % HW;
+    const long long nf = i / HW;
+    const int f = (int)(nf % Cf);
+    const float p = pred[i], t = tgt[i];
+    const float d = p - t;
+    s1 += fabsf(d);
+    sb += fabsf((p > binary ? 1.f : 0.f) - (t > binary ? 1.f : 0.f));
+    float g = g1 * (float)((d > 0.f) - (d < 0.f));
+    if (f + 1 < Cf) {  // temporal term of the pair (f, f + 1)
+      const float u = (pred[i + HW] - p) - (tgt[i + HW] - t);
+      st += fabsf(u);
+      g -= gt * (float)((u > 0.f) - (u < 0.f));
+    }
+    if (f > 0) {  // ... and of the pair (f - 1, f)
+      const float u = (p - pred[i - HW]) - (t - tgt[i - HW]);
+      g += gt * (float)((u > 0.f) - (u < 0.f));
+    }
+    (void)s;
+    dpred[i] = g;
+  }
+  __shared__ float red[3][kThreads];
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = sb;
+  red[2][threadIdx.x] = st;
+  __syncthreads();
+  for (int w = kThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int j = 0; j < 3; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) part[blockIdx.x * 3 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void l1frames_final_kernel(const float* __restrict__ part, int nblk, float w1, float wt, double inv1,
+                                      double inv2, float* __restrict__ loss) {
+  if (threadIdx.x) return;
+  double a = 0, b = 0, c = 0;
+  for (int i = 0; i < nblk; ++i) {
+    a += part[3 * i];
+    b += part[3 * i + 1];
+    c += part[3 * i + 2];
+  }
+  loss[0] = (float)(w1 * ((a + b) * inv1) + (inv2 > 0 ? wt * (c * inv2) : 0.0));
+}
+
+}  // namespace
+
+hipError_t launch_im2col3d(const float* x, int ldx, int C, int B, int F, int H, int W, float* col, hipStream_t s) {
+  const long long n = (long long)B * F * H * W * 27 * C;
+  hipLaunchKernelGGL(im2col3d_kernel, dim3(grid_for(n)), dim3(kThreads), 0, s, x, ldx, C, Geo{B, F, H, W}, col);
+  return hipGetLastError();
+}
+
+hipError_t launch_col2im3d(const float* dcol, int C, int B, int F, int H, int W, float* dx, int lddx, int accumulate,
+                           hipStream_t s) {
+  const long long n = (long long)B * F * H * W * C;
+  hipLaunchKernelGGL(col2im3d_kernel, dim3(grid_for(n)), dim3(kThreads), 0, s, dcol, C, Geo{B, F, H, W}, dx, lddx,
+                     accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_relu(float* y, int ld, int C, long long P, hipStream_t s) {
+  hipLaunchKernelGGL(relu_kernel, dim3(grid_for(P * C)), dim3(kThreads), 0, s, y, ld, C, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_relu_mask(float* dy, int ldd, const float* y, int ldy, int C, long long P, hipStream_t s) {
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(P * C)), dim3(kThreads), 0, s, dy, ldd, y, ldy, C, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_maxpool2_bwd(const float* in, int ldi, const float* dout, int ldo, const float* dskip, int lds,
+                               float* din, int ldd, int C, int B, int F, int h, int w, hipStream_t s) {
+  const long long n = (long long)B * F * h * w * C;
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(n)), dim3(kThreads), 0, s, in, ldi, dout, ldo, dskip, lds,
+                     din, ldd, C, Geo{B, F, h, w});
+  return hipGetLastError();
+}
+
+hipError_t launch_upshuffle_add(const float* U, int ldu, const float* bias, const float* skip, int lds, float* D,
+                                int ldd, int C, int B, int F, int H, int W, hipStream_t s) {
+  const long long n = (long long)B * F * H * W * C;
+  hipLaunchKernelGGL(upshuffle_add_kernel, dim3(grid_for(n)), dim3(kThreads), 0, s, U, ldu, bias, skip, lds, D, ldd,
+                     C, Geo{B, F, H, W});
+  return hipGetLastError();
+}
+
+int l1frames_scratch_floats() { return 3 * kLossBlocks; }
+
+hipError_t launch_l1frames(const float* pred, const float* tgt, int N, int Cf, long long HW, float l1_weight,
+                           float temporal_weight, float binary, int sum_reduction, float* dpred, float* loss,
+                           float* scratch, hipStream_t s) {
+  const long long n = (long long)N * Cf * HW;
+  const long long n2 = (long long)N * (Cf - 1) * HW;
+  const double inv1 = sum_reduction ? 1.0 : 1.0 / (double)n;
+  const double inv2 = Cf > 1 ? (sum_reduction ? 1.0 : 1.0 / (double)n2) : 0.0;
+  const float g1 = (float)(l1_weight * inv1), gt = (float)(temporal_weight * inv2);
+  const unsigned blocks = (unsigned)std::min<long long>(kLossBlocks, (n + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL(l1frames_kernel, dim3(blocks), dim3(kThreads), 0, s, pred, tgt, N, Cf, HW, binary, g1, gt, dpred,
+                     scratch);
+  hipLaunchKernelGGL(l1frames_final_kernel, dim3(1), dim3(64), 0, s, scratch, (int)blocks, l1_weight,
+                     temporal_weight, inv1, inv2, loss);
+  return hipGetLastError();
+}
+
+}  // namespace train
+}  // namespace kdlae

@@ -27,7 +27,8 @@ import torch.distributed as dist
 from . import _lib
 
 __all__ = ["TrainEngine", "TeacherTrainFn", "L1LossSr", "KDLAETrainer", "MixingAugment", "sync_gradients",
-           "grad_buckets", "sync_gradients_bucketed"]
+           "grad_buckets", "sync_gradients_bucketed", "StudentTrainEngine", "StudentTrainFn",
+           "L1LossForVideoFrames", "KDLAESTrainer"]
 
 
 def _vp(t):
@@ -239,6 +240,228 @@ class L1LossSr(torch.nn.Module):
             raise RuntimeError("L1LossSr (MI355X build) runs on ROCm devices only")
         return _L1LossSrFn.apply(pred["hq"], target["hq"], pred.get("sr"), target.get("sr") if pred.get("sr")
                                  is not None else None, float(self.loss_weight))
+
+
+# ------------------------------------------------------------------ KDLAE-S (KDLAES.yml)
+class StudentTrainEngine:
+    """``kdlae_st_*`` handle for one KDLAE_student config on one device (KDLAE_model.py:340-431)."""
+
+    def __init__(self, model, device: torch.device):
+        L = _lib.lib()
+        self.device = device
+        h = ctypes.c_void_p()
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        _lib.check(L.kdlae_st_create(ctypes.byref(model._c_config()), idx, ctypes.byref(h)), "kdlae_st_create")
+        self.handle = h
+        self._L = L
+        self.keys = []
+        for i in range(L.kdlae_st_num_params(h)):
+            name, numel, off = ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_int64()
+            _lib.check(L.kdlae_st_param_info(h, i, ctypes.byref(name), ctypes.byref(numel), ctypes.byref(off)),
+                       "kdlae_st_param_info")
+            self.keys.append((name.value.decode(), int(numel.value), int(off.value)))
+        self.numel = int(L.kdlae_st_num_floats(h))
+        if [k for k, _, _ in self.keys] != [k for k, _ in model.named_parameters()]:
+            raise RuntimeError("KDLAE_student parameters do not match the training handle's state_dict layout")
+        self.ws = None
+        self.generation = 0
+        self._dtor = L.kdlae_st_destroy
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self._dtor(self.handle)
+        except Exception:
+            pass
+
+    def used_ranges(self):
+        return [[0, self.numel]]
+
+    flatten = TrainEngine.flatten
+    packed = TrainEngine.packed
+
+    def forward(self, theta, x):
+        """KDLAE_student.forward with activations kept for ``backward``: x [B, F, H, W] -> [B, F, H, W]."""
+        if x.device.type != "cuda":
+            raise RuntimeError("KDLAE training runs on ROCm devices only; there is no CPU fallback")
+        x = x.detach().to(torch.float32).contiguous()
+        B, F, H, W = x.shape
+        nbytes = int(self._L.kdlae_st_workspace_bytes(self.handle, B, F, H, W))
+        if nbytes < 0:
+            _lib.check(1, "kdlae_st_workspace_bytes")
+        if self.ws is None or self.ws.numel() < nbytes:
+            self.ws = None
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+        out = torch.empty_like(x)
+        self._x = x  # the residual input must outlive the backward
+        rc = self._L.kdlae_st_forward(self.handle, _vp(theta), _vp(x), B, F, H, W, _vp(out), _vp(self.ws),
+                                      self.ws.numel(), _stream(x.device))
+        _lib.check(rc, "kdlae_st_forward")
+        self.generation += 1
+        return out
+
+    def backward(self, theta, dout, grad):
+        dout = dout.detach().to(torch.float32).contiguous()
+        rc = self._L.kdlae_st_backward(self.handle, _vp(theta), _vp(dout), _vp(grad), _vp(self.ws), self.ws.numel(),
+                                       _stream(grad.device))
+        _lib.check(rc, "kdlae_st_backward")
+        return grad
+
+
+class StudentTrainFn(torch.autograd.Function):
+    """Autograd node for one KDLAE_student forward on the training engine (the input gets no gradient)."""
+
+    @staticmethod
+    def forward(ctx, engine, x, *params):
+        theta = engine.flatten(params)
+        out = engine.forward(theta, x)
+        ctx.engine = engine
+        ctx.generation = engine.generation
+        ctx.theta = theta
+        ctx.shapes = [p.shape for p in params]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        eng = ctx.engine
+        if eng.generation != ctx.generation:
+            raise RuntimeError("KDLAE_student: a second training forward ran before this graph's backward; "
+                               "the HIP engine keeps one set of saved activations per model and device")
+        grad = torch.empty(eng.numel, dtype=torch.float32, device=ctx.theta.device)
+        eng.backward(ctx.theta, dout, grad)
+        return (None, None, *[grad[off:off + n].view(shape) for (k, n, off), shape in zip(eng.keys, ctx.shapes)])
+
+
+class _L1FramesFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, target, l1w, tw, binary, red):
+        L = _lib.lib()
+        dev = pred.device
+        p = pred.detach().to(torch.float32).contiguous()
+        t = target.detach().to(device=dev, dtype=torch.float32).contiguous()
+        N, Cf = p.shape[0], p.shape[1]
+        hw = p.numel() // max(1, N * Cf)
+        dp = torch.empty_like(p)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        scratch = torch.empty(int(L.kdlae_train_l1frames_scratch_floats()), dtype=torch.float32, device=dev)
+        rc = L.kdlae_train_l1frames(_vp(p), _vp(t), N, Cf, hw, float(l1w), float(tw), float(binary), red, _vp(dp),
+                                    _vp(loss), _vp(scratch), _stream(dev))
+        _lib.check(rc, "kdlae_train_l1frames")
+        ctx.save_for_backward(dp)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dp,) = ctx.saved_tensors
+        return dp * g, None, None, None, None, None
+
+
+class L1LossForVideoFrames(torch.nn.Module):
+    """L1LossForVideoFrames (Train/basicsr/models/losses/losses.py:409-526) on the HIP path, autograd-aware:
+    l1loss_weight * reduce(|p - t| + |bin(p) - bin(t)|) + temporal_weight * reduce(|dp - dt|) over the
+    frame axis (dim 1) of [N, frames, H, W] tensors.  The reference's 'max' / 'mix' reductions (and
+    element weights) are not used by its configs and raise NotImplementedError here."""
+
+    def __init__(self, l1loss_weight=0.64, reduction="mean", sigma=2.0, weight=[1.5, 1.0], invert=False,
+                 temporal_weight=0.36, binary=0.1):
+        super().__init__()
+        if reduction not in ["none", "mean", "sum", "max", "mix"]:
+            raise ValueError(f"Unsupported reduction mode: {reduction}. "
+                             f'Supported ones are: ["none", "mean", "sum", "max", "mix"]')
+        self.l1loss_weight = l1loss_weight
+        self.reduction = reduction
+        self.temporal_weight = temporal_weight
+        self.binary = binary
+
+    def forward(self, pred, target, weight=None, **kwargs):
+        if weight is not None:
+            raise NotImplementedError("element-wise loss weights are not used by the reference configs")
+        if self.reduction not in ("mean", "sum"):
+            raise NotImplementedError(f"L1LossForVideoFrames reduction {self.reduction!r} on the HIP path "
+                                      "(KDLAES.yml uses 'mean')")
+        if pred.device.type != "cuda":
+            raise RuntimeError("L1LossForVideoFrames (MI355X build) runs on ROCm devices only")
+        return _L1FramesFn.apply(pred, target, self.l1loss_weight, self.temporal_weight, self.binary,
+                                 0 if self.reduction == "mean" else 1)
+
+
+class KDLAESTrainer:
+    """ImageCleanModel.optimize_parameters for KDLAE_student with KDLAES.yml (AdamW lr 3e-4 wd 1e-4 betas
+    (0.9, 0.999); use_grad_clip -> clip_grad_norm_(0.01); L1LossForVideoFrames(0.9, mean, temporal 0.1);
+    mixup): flat buffers end to end, one RCCL all-reduce of the flat gradient for DDP."""
+
+    def __init__(self, model, lr=3e-4, weight_decay=1e-4, betas=(0.9, 0.999), eps=1e-8, use_grad_clip=True,
+                 max_norm=0.01, loss_kw=None, group=None, mixing_augs=None):
+        params = list(model.parameters())
+        if not params or params[0].device.type != "cuda":
+            raise RuntimeError("KDLAESTrainer: move the model to a ROCm device first (no CPU fallback)")
+        dev = params[0].device
+        self.model = model
+        self.engine = StudentTrainEngine(model, dev)
+        eng = self.engine
+        self.theta = eng.flatten(params).contiguous()
+        with torch.no_grad():
+            for (k, n, off), p in zip(eng.keys, params):
+                p.data = self.theta[off:off + n].view(p.shape)
+        self.grad = torch.zeros(eng.numel, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros_like(self.grad)
+        self.exp_avg_sq = torch.zeros_like(self.grad)
+        self.lr, self.weight_decay, self.betas, self.eps = lr, weight_decay, tuple(betas), eps
+        self.max_norm = max_norm if use_grad_clip else 0.0
+        kw = dict(l1loss_weight=0.9, temporal_weight=0.1, reduction="mean")
+        kw.update(loss_kw or {})
+        self.loss_fn = L1LossForVideoFrames(**kw)
+        self.group = group
+        self.step_count = 0
+        self.loss = None
+        L = _lib.lib()
+        self._opt_scratch = torch.empty(int(L.kdlae_train_adamw_scratch_floats()), dtype=torch.float32, device=dev)
+        self._l1_scratch = torch.empty(int(L.kdlae_train_l1frames_scratch_floats()), dtype=torch.float32,
+                                       device=dev)
+        self._loss = torch.zeros((), dtype=torch.float32, device=dev)
+        m = mixing_augs or {}
+        self.mixing = (MixingAugment(m.get("mixup_beta", 1.2), m.get("use_identity", False), dev)
+                       if m.get("mixup", False) else None)
+
+    def feed_train_data(self, lq, gt):
+        if self.mixing is not None:
+            gt, lq = self.mixing(gt, lq)
+        return lq, gt
+
+    def forward_backward(self, lq, gt):
+        eng, L = self.engine, _lib.lib()
+        out = eng.forward(self.theta, lq)
+        self.output = out
+        dout = torch.empty_like(out)
+        gt = gt.to(torch.float32).contiguous()
+        N, Cf = out.shape[0], out.shape[1]
+        lf = self.loss_fn
+        if lf.reduction not in ("mean", "sum"):
+            raise NotImplementedError(f"reduction {lf.reduction!r}")
+        rc = L.kdlae_train_l1frames(_vp(out), _vp(gt), N, Cf, out.numel() // (N * Cf), float(lf.l1loss_weight),
+                                    float(lf.temporal_weight), float(lf.binary), 0 if lf.reduction == "mean" else 1,
+                                    _vp(dout), _vp(self._loss), _vp(self._l1_scratch), _stream(out.device))
+        _lib.check(rc, "kdlae_train_l1frames")
+        eng.backward(self.theta, dout, self.grad)
+        self.loss = self._loss
+        return self.loss
+
+    def step(self, gscale: float = 1.0):
+        self.step_count += 1
+        b1, b2 = self.betas
+        rc = _lib.lib().kdlae_train_clip_adamw(
+            _vp(self.theta), _vp(self.grad), _vp(self.exp_avg), _vp(self.exp_avg_sq), self.engine.numel,
+            float(gscale), float(self.max_norm), float(self.lr), float(b1), float(b2), float(self.eps),
+            float(self.weight_decay), self.step_count, None, 0, _vp(self._opt_scratch), _stream(self.theta.device))
+        _lib.check(rc, "kdlae_train_clip_adamw")
+
+    def optimize_parameters(self, lq, gt):
+        loss = self.forward_backward(lq, gt)
+        self.step(sync_gradients(self.grad, self.group))
+        return loss
+
+    def grad_norm(self) -> torch.Tensor:
+        return self._opt_scratch[2048]
 
 
 def _mix(t, perm, lam):

@@ -249,6 +249,79 @@ def train_goldens(KM, out):
         print(name, losses, norms, grad1.shape, f"{time.time() - t0:.1f}s")
 
 
+# ---------------------------------------------------------------- KDLAE-S training (KDLAES.yml)
+S_TRAIN_CASES = {
+    # name: (ctor kwargs, x shape [B, F, H, W], loss kwargs)
+    "train_s_kdlaes": (dict(inp_channels=1, out_channels=1, residual=True, hidden_channels=[16, 32, 64]), (2, 7, 32, 32),
+                       dict(l1loss_weight=0.9, temporal_weight=0.1, reduction="mean")),
+    "train_s_4lvl_sum": (dict(inp_channels=1, out_channels=1, residual=False, hidden_channels=[8, 16, 16, 32]),
+                         (1, 3, 16, 24), dict(reduction="sum")),
+    "train_s_1frame": (dict(inp_channels=1, out_channels=1, residual=True, hidden_channels=[12, 20]), (2, 1, 8, 12),
+                       dict(l1loss_weight=0.9, temporal_weight=0.1, reduction="mean")),
+}
+S_TRAIN_OPT = dict(lr=3e-4, weight_decay=1e-4, betas=(0.9, 0.999))  # KDLAES.yml optim_g
+S_TRAIN_SUB = 4  # flat gradients / parameter deltas kept at every 4th element (+ per-key float64 sums)
+
+
+def _ref_video_loss():
+    """L1LossForVideoFrames from the reference's own losses.py, loaded by path (its only import outside
+    torch / numpy is basicsr.models.losses.loss_util, registered under that name from the reference's
+    loss_util.py; the basicsr package itself needs cv2)."""
+    import importlib.util
+    import types
+    base = os.path.join(REF, "Train", "basicsr", "models", "losses")
+    for pkg in ("basicsr", "basicsr.models", "basicsr.models.losses"):
+        if pkg not in sys.modules:
+            m = types.ModuleType(pkg)
+            m.__path__ = []
+            sys.modules[pkg] = m
+    for mod, fn in (("basicsr.models.losses.loss_util", "loss_util.py"), ("ref_losses", "losses.py")):
+        spec = importlib.util.spec_from_file_location(mod, os.path.join(base, fn))
+        m = importlib.util.module_from_spec(spec)
+        sys.modules[mod] = m
+        spec.loader.exec_module(m)
+    return sys.modules["ref_losses"].L1LossForVideoFrames
+
+
+def student_train_goldens(KM, out):
+    """Loss + every parameter gradient of the reference KDLAE_student under the reference's
+    L1LossForVideoFrames (autograd through both), then the parameters after two clip_grad_norm_(0.01)
+    + AdamW steps (image_restoration_model.py:198-218, KDLAES.yml optim_g)."""
+    Loss = _ref_video_loss()
+    for name, (kw, shape, lkw) in S_TRAIN_CASES.items():
+        t0 = time.time()
+        m = _load_hash(KM.KDLAE_student(**kw)).train()
+        x = hash_images(f"sx:{name}", shape)
+        tgt = hash_images(f"st:{name}", shape)
+        crit = Loss(**lkw)
+        params = list(m.parameters())
+        params0 = np.concatenate([p.detach().reshape(-1).numpy() for p in params]).astype(np.float64)
+        opt = torch.optim.AdamW(params, **S_TRAIN_OPT)
+        losses, norms = [], []
+        for step in range(2):
+            opt.zero_grad()
+            loss = crit(m(torch.from_numpy(x)), torch.from_numpy(tgt))
+            loss.backward()
+            if step == 0:
+                gl = [p.grad.detach().reshape(-1).numpy() for p in params]
+                grad1 = np.concatenate(gl)
+                gsums = np.array([[g.astype(np.float64).sum(), np.abs(g).astype(np.float64).sum()] for g in gl])
+            norms.append(float(torch.nn.utils.clip_grad_norm_(params, TRAIN_CLIP)))
+            opt.step()
+            losses.append(float(loss))
+        keys = [k for k, _ in m.named_parameters()]
+        params2 = np.concatenate([p.detach().reshape(-1).numpy() for p in params]).astype(np.float64)
+        d = dict(x=x, target=tgt, loss=np.array(losses, np.float64), norm=np.array(norms, np.float64),
+                 grad1_sub=grad1[::S_TRAIN_SUB].astype(np.float32), grad_sums=gsums,
+                 delta2_sub=(params2 - params0)[::S_TRAIN_SUB].astype(np.float32),
+                 keys=np.frombuffer(json.dumps(keys).encode(), dtype=np.uint8),
+                 cfg=np.frombuffer(json.dumps(kw).encode(), dtype=np.uint8),
+                 loss_kw=np.frombuffer(json.dumps(lkw).encode(), dtype=np.uint8),
+                 opt=np.frombuffer(json.dumps(dict(S_TRAIN_OPT, clip=TRAIN_CLIP)).encode(), dtype=np.uint8))
+        np.savez_compressed(os.path.join(out, f"{name}.npz"), **d)
+        print(name, losses, norms, grad1.shape, f"{time.time() - t0:.1f}s")
+
+
 # ---------------------------------------------------------------- checkpoint layout (SURVEY §8f rank 3)
 CKPT_CASES = {
     # name: (which model, ctor kwargs, input shape)
@@ -477,9 +550,12 @@ def asdqe_scoring_goldens(AM, out):
 def main():
     KM, AM = _import_ref()
     out = HERE
-    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512", "train", "ckpt", "keys", "lr", "frames", "scoring"]
+    which = sys.argv[1:] or ["teacher", "student", "asdqe", "t512", "train", "ckpt", "keys", "lr", "frames", "scoring",
+                             "train_s"]
     if "train" in which:
         train_goldens(KM, out)
+    if "train_s" in which:
+        student_train_goldens(KM, out)
     if "teacher" in which:
         teacher_goldens(KM, out)
     if "student" in which:

@@ -93,12 +93,14 @@ def test_shape_and_device_errors():
         m.cpu()(torch.zeros(1, 2, 32, 32))
 
 
-def test_train_mode_with_grad_raises():
-    """KDLAE-S has no HIP backward yet: a training-mode forward that would need one raises instead of
-    returning a tensor without a graph (BasicSR's l_pix.backward() would fail on it, KDLAES.yml)."""
-    m = _model(dict(residual=True, hidden_channels=[16, 32, 64])).train()
-    x = torch.zeros(1, 2, 32, 32, device=DEV)
-    with pytest.raises(NotImplementedError, match="no backward"):
-        m(x)
+def test_train_mode_forward_has_a_graph():
+    """KDLAE_student in train mode with grad routes through the HIP training engine (KDLAES.yml's
+    l_pix.backward() needs a graph): same outputs as the inference kernels within 1e-5, and a grad_fn."""
+    m = _model(dict(residual=True, hidden_channels=[16, 32, 64]))
+    x = torch.from_numpy(hash_images("s_train_fwd", (2, 3, 32, 32))).to(DEV)
     with torch.no_grad():
-        assert m(x).shape == x.shape  # inference in train mode without grad is fine
+        ref = m(x)
+    m.train()
+    y = m(x)
+    assert y.grad_fn is not None
+    assert max_abs(y.detach().cpu(), ref.cpu()) <= 1e-5

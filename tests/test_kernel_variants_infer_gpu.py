@@ -39,7 +39,7 @@ class GemmDesc(ctypes.Structure):
                 ("Wm", c_void_p), ("wm_img_stride", c_int64), ("bias_m", c_void_p), ("out1", c_void_p),
                 ("ldo1", c_int),
                 ("NT", c_int), ("KG", c_int), ("wpe", c_int), ("group_tiles", c_int), ("tiles_per_block", c_int),
-                ("route", c_int), ("ln_w", c_void_p), ("ln_b", c_void_p), ("dual", c_int)]
+                ("route", c_int)]
 
 
 class GramDesc(ctypes.Structure):
@@ -106,29 +106,14 @@ def pack_fragments(Wmat, ntiles, kgroups):
     return Wp.view(ntiles, 16, kgroups, 4, 4).permute(0, 2, 3, 1, 4).contiguous().view(-1)
 
 
-def _ln_ref(x, mode, w=None, b=None):
+def _ln_ref(x, mode):
     mu = x.mean(-1, keepdim=True)
     var = ((x - mu) ** 2).mean(-1, keepdim=True)
-    y = (x - mu) / torch.sqrt(var + 1e-5) if mode == 2 else x / torch.sqrt(var + 1e-5)
-    if w is not None:
-        y = y * w.double()
-    if b is not None:
-        y = y + b.double()
-    return y
-
-
-def pack_dual(Mmat, ntiles, kgroups):
-    """hi / lo virtual tiles (GemmParams::dual): tile 2t = fl(M_t), 2t + 1 = fl(M_t - fl(M_t)) of a float64
-    [N][K] matrix, each in fragment order."""
-    hi = Mmat.float()
-    lo = (Mmat - hi.double()).float()
-    ph = pack_fragments(hi, ntiles, kgroups).view(ntiles, -1)
-    pl = pack_fragments(lo, ntiles, kgroups).view(ntiles, -1)
-    return torch.stack([ph, pl], 1).reshape(-1)
+    return (x - mu) / torch.sqrt(var + 1e-5) if mode == 2 else x / torch.sqrt(var + 1e-5)
 
 
 def _gemm_case(NT, KG, c3, out_mode, route, group_tiles=0, ntiles=None, with_r=False, ln=0, attn_in=False,
-               seed=0, kchunks=1, dil=1, kt=1, relu=0, affine=True):
+               seed=0, kchunks=1, dil=1, kt=1, relu=0):
     """One GEMM launch with the tile shape (NT, KG) forced, checked against float64 torch.
     group_tiles > 0: resident schedule (KG = kgroups); else ~kchunks chunks of KG k-groups."""
     Bn, Fr, H, W = 2, (3 if kt == 3 else 1), 10, 14
@@ -155,20 +140,16 @@ def _gemm_case(NT, KG, c3, out_mode, route, group_tiles=0, ntiles=None, with_r=F
     bias[:N] = _rand(N, seed=seed + 2)
     Wp = pack_fragments(Wt, ntiles, kgroups)
     x = A[:, :, :Cin].double()
-    # the LN affine the GEMM applies in its prologue (random weight, and bias for WithBias)
-    lnw = (1.0 + 0.5 * _rand(K, seed=seed + 8)) if (ln and affine) else None
-    lnb = (0.2 * _rand(K, seed=seed + 9)) if (ln == 2 and affine) else None
     if not c3:
         xa = x
         if attn_in:
-            # M in float64 as the hi / lo pair attn_fold writes
-            M = (_rand(Bn, K, K, seed=seed + 5) / (K ** 0.5)).double() * (1 + 1e-7 * _rand(Bn, K, K, seed=seed + 10).double())
+            M = _rand(Bn, K, K, seed=seed + 5) / (K ** 0.5)
             bm = _rand(K, seed=seed + 6)
             Xr = _rand(Bn, HW, K + 4, seed=seed + 7)
-            x1 = Xr[:, :, :K].double() + torch.einsum("bpk,bnk->bpn", x, M) + bm.double()
+            x1 = Xr[:, :, :K].double() + torch.einsum("bpk,bnk->bpn", x, M.double()) + bm.double()
             xa = x1
         if ln:
-            xa = _ln_ref(xa, ln, lnw, lnb)
+            xa = _ln_ref(xa, ln)
         ref = xa @ Wt.double().T + bias[:N].double()
         ref = ref.view(Bn * Fr, H, W, N).permute(0, 3, 1, 2)
     elif kt == 1:
@@ -197,12 +178,11 @@ def _gemm_case(NT, KG, c3, out_mode, route, group_tiles=0, ntiles=None, with_r=F
     kw = dict(A=_ptr(A), lda=lda, Bn=Bn, F=Fr, H=H, W=W, ksize=3 if c3 else 1, kt=kt, dil=dil,
               cg_per_tap=cg if c3 else 0, kgroups=kgroups, Wp=_ptr(Wp), ntiles=ntiles, N=N, bias=_ptr(bias),
               out=_ptr(out), ldo=ldo, R=_ptr(R), ldr=ldo, ln=ln, ln_C=K, relu=relu, out_mode=out_mode,
-              stats=_ptr(stats), NT=NT, KG=KG, wpe=2, group_tiles=group_tiles, route=route,
-              ln_w=_ptr(lnw), ln_b=_ptr(lnb))
+              stats=_ptr(stats), NT=NT, KG=KG, wpe=2, group_tiles=group_tiles, route=route)
     if attn_in:
-        Mp = torch.cat([pack_dual(M[b], KG, KG) for b in range(Bn)])
+        Mp = torch.cat([pack_fragments(M[b], KG, KG) for b in range(Bn)])
         out1 = torch.full((Bn, HW, K + 4), 7.0, device=DEV)
-        kw.update(Wm=_ptr(Mp), wm_img_stride=2 * K * K, bias_m=_ptr(bm), out1=_ptr(out1), ldo1=K + 4,
+        kw.update(Wm=_ptr(Mp), wm_img_stride=K * K, bias_m=_ptr(bm), out1=_ptr(out1), ldo1=K + 4,
                   R=_ptr(Xr), ldr=K + 4, group_tiles=ntiles)
     _call("kdlae_debug_gemm", GemmDesc, **kw)
     _close(out[:, :Nout], ref, K, "out")
@@ -295,29 +275,6 @@ def test_gemm_attn_in_variant(v, ln):
     out = LN(x1) W^T + b over (NCH - 1) NT + 1 output tiles."""
     NT, KG, NCH = v[:3]
     _gemm_case(NT, KG, False, 0, 0, attn_in=True, ln=ln, ntiles=(NCH - 1) * NT + 1, seed=500 + ATTN.index(v))
-
-
-@pytest.mark.parametrize("kgroups,resident", [(6, True), (6, False), (12, False), (2, False)])
-def test_gemm_dual_projection(kgroups, resident):
-    """GemmParams::dual (the attention projection M = W_proj blockdiag(A) as hi / lo tiles): the resident
-    KG = 6 kernel (C = 96) and the chunked one (any C) store R + M v + bias with M the float64 matrix
-    the two halves represent."""
-    Bn, H, W = 2, 10, 14
-    K = N = 16 * kgroups
-    A = _rand(Bn, H * W, K + 4, seed=600 + kgroups)
-    M = (_rand(N, K, seed=601) / (K ** 0.5)).double() * (1 + 1e-7 * _rand(N, K, seed=602).double())
-    bias = torch.zeros(2 * N, device=DEV)
-    bvals = _rand(N, seed=603)
-    bias.view(-1, 2, 16)[:, 0, :] = bvals.view(-1, 16)          # real bias on the hi tiles
-    R = _rand(Bn * H * W, N + 4, seed=604)
-    out = torch.full((Bn * H * W, N + 4), 7.0, device=DEV)
-    Wp = pack_dual(M, N // 16, kgroups)
-    _call("kdlae_debug_gemm", GemmDesc, A=_ptr(A), lda=K + 4, Bn=Bn, F=1, H=H, W=W, ksize=1, kt=1, dil=1,
-          kgroups=kgroups, Wp=_ptr(Wp), ntiles=2 * N // 16, N=2 * N, bias=_ptr(bias), out=_ptr(out), ldo=N + 4,
-          R=_ptr(R), ldr=N + 4, NT=6, KG=6, wpe=2, group_tiles=2 * N // 16 if resident else 0, route=0, dual=1)
-    ref = A[:, :, :K].reshape(-1, K).double() @ M.T + bvals.double() + R[:, :N].double()
-    _close(out[:, :N], ref, K, "dual")
-    assert torch.all(out[:, N:] == 7.0), "wrote past N"
 
 
 def test_gemm_route_agreement_bits():

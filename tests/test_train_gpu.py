@@ -28,7 +28,7 @@ from tests.util import GOLDEN, hash_sd_for
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("train_"))
+CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("train_") and not f.startswith("train_s_"))
 
 
 def load_case(name):
