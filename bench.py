@@ -415,11 +415,91 @@ def bench_train(args, world, rank, dev, distributed):
         dist.destroy_process_group()
 
 
+def bench_train_s(args, world, rank, dev, distributed):
+    """KDLAE-S training iterations (KDLAES.yml: batch_size_per_gpu 4, num_pairs 7 frames, first progressive
+    patch 128^2; L1LossForVideoFrames(0.9, mean, temporal 0.1); clip_grad_norm_ 0.01; AdamW lr 3e-4 wd 1e-4;
+    mixup).  One step = forward + loss + backward + all-reduce (N > 1) + clip + AdamW."""
+    from rethink_acoustic_image_enhancement_amd.train import KDLAESTrainer
+
+    B = args.batch or 4
+    H = W = args.size or 128
+    Fr = 7
+    model = KDLAE_student(**S_KW)
+    load_hash_weights(model)
+    model = model.to(dev)
+    x = torch.from_numpy(np.stack([hash_images(f"trs_x:{rank * B + i}", (Fr, H, W)) for i in range(B)])).to(dev)
+    gt = torch.from_numpy(np.stack([hash_images(f"trs_gt:{rank * B + i}", (Fr, H, W)) for i in range(B)])).to(dev)
+    trainer = KDLAESTrainer(model, mixing_augs={"mixup": True, "mixup_beta": 1.2, "use_identity": True})
+    import random
+    random.seed(rank)
+    torch.manual_seed(rank)
+
+    def train_step():
+        lq_m, gt_m = trainer.feed_train_data(x, gt)
+        return trainer.optimize_parameters(lq_m, gt_m)
+
+    loss = None
+    for _ in range(args.warmup):
+        loss = train_step()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed():
+        ev0.record()
+        out = None
+        for _ in range(args.steps):
+            out = train_step()
+        ev1.record()
+        return out
+
+    elapsed, _, loss = timed_steps(timed, 1, distributed, dev)
+    dev_ms = ev0.elapsed_time(ev1)
+    flops = 3 * student_flops(S_KW["hidden_channels"], B, Fr, H, W)  # forward + dX + dW
+    ach = flops * args.steps / (dev_ms / 1e3) / 1e12
+    total = world * B * args.steps
+    res = {"metric": "samples/sec KDLAE-S training step 7x128x128 fp32 (KDLAES.yml)",
+           "value": round(total / elapsed, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic (hash-uniform frames and targets, hash weights of the real architecture)",
+           "config": {"workload": f"KDLAE-S train step bs={B}/GPU {Fr}x{H}x{W}, L1LossForVideoFrames, "
+                                  "clip_grad_norm_ 0.01, AdamW, mixup", "global_batch": world * B, "per_gpu_batch": B,
+                      "parallelism": f"dp{world}" + (" (RCCL all-reduce of the flat gradient every step)"
+                                                     if distributed else "")},
+           "roofline": {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                        "kernel": "whole training step (all launches, algorithmic 3x forward FLOPs)",
+                        "algorithmic_flops_per_step": flops},
+           "final_loss": float(loss)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.kdlae_oracle import StudentCfg
+        from oracle.train_oracle import YML_S_LOSS, student_loss_and_grads
+        threads, tdesc = host_cores() if not args.cpu_threads else (args.cpu_threads, "--cpu-threads")
+        torch.set_num_threads(threads)
+        sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        t0 = time.perf_counter()
+        l_ref, g_ref = student_loss_and_grads(sd, x[:1].cpu(), gt[:1].cpu(), StudentCfg(**S_KW), **YML_S_LOSS)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(1.0 / dt, 5), "unit": "samples/s", "cores": threads, "kind": "port",
+                               "cores_from": tdesc,
+                               "sample": f"1 sample of the batch, forward + L1LossForVideoFrames + backward of the "
+                                         f"torch-CPU oracle, {threads} threads, {dt:.1f} s"}
+        trainer.forward_backward(x[:1], gt[:1])
+        g = trainer.engine.packed(trainer.grad).cpu()
+        gr = torch.cat([g_ref[k].reshape(-1) for k, _ in model.named_parameters()])
+        res["parity"] = {"vs": "torch-CPU training oracle, sample 0, current weights",
+                         "loss_rel_err": abs(float(trainer.loss) - float(l_ref)) / abs(float(l_ref)),
+                         "grad_max_abs_err_rel_to_max": float((g - gr).abs().max() / gr.abs().max())}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["t16", "s8", "a64", "train"], default="t16",
+    ap.add_argument("--workload", choices=["t16", "s8", "a64", "train", "train_s"], default="t16",
                     help="t16 = KDLAE-T bs16 512^2 (headline); s8 = KDLAE-S; a64 = ASDQE; train = KDLAE-T "
-                         "training step (KDLAET.yml 6x128^2)")
+                         "training step (KDLAET.yml 6x128^2); train_s = KDLAE-S training step (KDLAES.yml 4x7x128^2)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -466,6 +546,8 @@ def main():
     dev = torch.device("cuda", local)
     if args.workload == "train":
         return bench_train(args, world, rank, dev, distributed)
+    if args.workload == "train_s":
+        return bench_train_s(args, world, rank, dev, distributed)
     if args.workload != "t16":
         res = bench_secondary(args, world, rank, dev, distributed, args.workload, args.batch, args.size,
                               cpu=not args.no_cpu_baseline)

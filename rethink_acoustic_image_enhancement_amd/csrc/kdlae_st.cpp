@@ -2,9 +2,10 @@
 // ImageCleanModel with KDLAES.yml: Train/basicsr/models/image_restoration_model.py:198-218).
 //
 // Forward with every activation kept (NDHWC, ld = channels), then the hand-sequenced backward:
-//   Conv3d 3x3x3 + bias + ReLU (:386-393)   fwd  Y = relu(Xcol . W^T + b)            (train GEMM)
+//   Conv3d 3x3x3 + bias + ReLU (:386-393)   fwd  Y = relu(Xcol . W'^T + b)           (train GEMM)
 //                                           bwd  dZ = dY (Y > 0); db = colsum dZ;
-//                                                dW = dZ^T . Xcol; dX = col2im(dZ . W)
+//                                                dW' = dZ^T . Xcol; dX = col2im(dZ . W')
+//                                           (W' = the weight in the columns' tap-major order, train_s.hip)
 //   MaxPool3d (1,2,2) (:366)                fwd  inference kernel; bwd first-max routing
 //   ConvTranspose3d (1,2,2) s2 (:378-379)   fwd  U = L . Wu (N = 4 Cout), D = shuffle(U) + b + skip (:417)
 //                                           bwd  dU = unshuffle(dD); db = colsum dD; dWu = L^T dU; dL = dU Wu^T
@@ -48,7 +49,8 @@ constexpr int kColsumBlocks = 256;
 struct SPlanT {
   size_t total = 0;
   std::vector<size_t> ea, e, pool, ua, da, dd, dl, gskip;  // per level / decoder
-  size_t fa = 0, fo = 0, col = 0, gA = 0, gB = 0, partial = 0, part = 0;
+  std::unordered_map<std::string, size_t> xcol;            // each Conv3d's forward column matrix
+  size_t fa = 0, fo = 0, col = 0, gA = 0, gB = 0, partial = 0, part = 0, wp = 0, dwp = 0;
   size_t take(long long floats) {
     const size_t o = total;
     total += ((size_t)floats * 4 + 255) / 256 * 256;
@@ -91,7 +93,28 @@ SPlanT make_plan(const kdlae_st_handle* h, int B, int F, int H, int W) {
     pl.dl.push_back(pl.take(P * c));
     colmax = std::max(colmax, P * 27 * c);
   }
-  pl.col = pl.take(colmax);
+  pl.col = pl.take(colmax);  // the input-gradient columns dZ . W' (and the ConvTranspose dU)
+  // every Conv3d's Xcol is kept from the forward for its weight gradient (about 4.4 GB at KDLAES.yml's
+  // B 4 x 7 x 128^2: one HBM write + read instead of a second im2col per conv)
+  for (int i = 0; i < L; ++i) {
+    const long long P = npx(h, i, B, F, H, W);
+    const std::string p = "encoders." + std::to_string(i);
+    pl.xcol[p + ".0"] = pl.take(P * 27 * (i ? h->hc[i - 1] : 1));
+    pl.xcol[p + ".2"] = pl.take(P * 27 * h->hc[i]);
+  }
+  pl.xcol["st_fusion.0"] = pl.take(PL * 27 * h->hc[L - 1]);
+  pl.xcol["st_fusion.2"] = pl.take(PL * 27 * h->hc[L]);
+  for (int j = 0; j < L; ++j) {
+    const int i = L - 1 - j;
+    const long long P = npx(h, i, B, F, H, W);
+    const std::string d = "decoders." + std::to_string(j);
+    pl.xcol[d + ".0"] = pl.take(P * 27 * h->hc[i]);
+    pl.xcol[d + ".2"] = pl.take(P * 27 * h->hc[i]);
+  }
+  long long wmax = 0;  // the largest Conv3d weight, for its tap-major copy and gradient
+  for (int i = 0; i <= L; ++i) wmax = std::max(wmax, 27LL * h->hc[i] * std::max(i ? h->hc[i - 1] : 1, h->hc[i]));
+  pl.wp = pl.take(wmax);
+  pl.dwp = pl.take(wmax);
   pl.gA = pl.take(gmax);
   pl.gB = pl.take(gmax);
   pl.partial = pl.take((long long)kPartialFloats);
@@ -137,15 +160,17 @@ int colsum(Ctx& c, const float* x, int ld, int ncols, long long rows, float* out
   return KDLAE_OK;
 }
 
-// Y = relu(Xcol . W^T + b) over P pixels at level lvl
+// Y = relu(Xcol . W'^T + b) over P pixels at level lvl (W' = the weight in tap-major order)
 int conv_fwd(Ctx& c, const std::string& p, const float* X, int cin, float* Y, int cout, int lvl) {
   const int Hl = c.H >> lvl, Wl = c.W >> lvl;
   const long long P = (long long)c.B * c.F * Hl * Wl;
-  float* col = c.buf(c.pl.col);
+  float* col = c.buf(c.pl.xcol.at(p));
+  float* wp = c.buf(c.pl.wp);
+  HIPCHK(tr::launch_wperm(c.P(p + ".weight"), wp, cout, cin, 0, c.s));
   HIPCHK(tr::launch_im2col3d(X, cin, cin, c.B, c.F, Hl, Wl, col, c.s));
   tr::TGemm g;
   g.A = col; g.sam = 27LL * cin; g.sak = 1;
-  g.B = c.P(p + ".weight"); g.sbk = 1; g.sbn = 27LL * cin;
+  g.B = wp; g.sbk = 1; g.sbn = 27LL * cin;
   g.C = Y; g.scm = cout; g.scn = 1;
   g.bias = c.P(p + ".bias");
   g.M = (int)P; g.N = cout; g.K = 27 * cin;
@@ -161,18 +186,23 @@ int conv_bwd(Ctx& c, const std::string& p, const float* X, int cin, const float*
   const long long P = (long long)c.B * c.F * Hl * Wl;
   HIPCHK(tr::launch_relu_mask(dY, cout, Y, cout, cout, P, c.s));
   TRY(colsum(c, dY, cout, cout, P, c.G(p + ".bias")));
+  (void)X;  // its columns are the forward's
+  const float* xcol = c.buf(c.pl.xcol.at(p));
   float* col = c.buf(c.pl.col);
-  HIPCHK(tr::launch_im2col3d(X, cin, cin, c.B, c.F, Hl, Wl, col, c.s));
-  tr::TGemm g;  // dW[o][k] = sum_p dZ[p][o] Xcol[p][k]
+  float* wp = c.buf(c.pl.wp);
+  float* dwp = c.buf(c.pl.dwp);
+  tr::TGemm g;  // dW'[o][k] = sum_p dZ[p][o] Xcol[p][k], then back to OIDHW order
   g.A = dY; g.sam = 1; g.sak = cout;
-  g.B = col; g.sbk = 27LL * cin; g.sbn = 1;
-  g.C = c.G(p + ".weight"); g.scm = 27LL * cin; g.scn = 1;
+  g.B = xcol; g.sbk = 27LL * cin; g.sbn = 1;
+  g.C = dwp; g.scm = 27LL * cin; g.scn = 1;
   g.M = cout; g.N = 27 * cin; g.K = (int)P;
   TRY(gemm(c, g, true));
+  HIPCHK(tr::launch_wperm(dwp, c.G(p + ".weight"), cout, cin, 1, c.s));
   if (!dX) return KDLAE_OK;
-  tr::TGemm d;  // dXcol = dZ . W, then the gather
+  HIPCHK(tr::launch_wperm(c.P(p + ".weight"), wp, cout, cin, 0, c.s));
+  tr::TGemm d;  // dXcol = dZ . W', then the gather
   d.A = dY; d.sam = cout; d.sak = 1;
-  d.B = c.P(p + ".weight"); d.sbk = 27LL * cin; d.sbn = 1;
+  d.B = wp; d.sbk = 27LL * cin; d.sbn = 1;
   d.C = col; d.scm = 27LL * cin; d.scn = 1;
   d.M = (int)P; d.N = 27 * cin; d.K = cout;
   TRY(gemm(c, d, false));

@@ -8,11 +8,13 @@
 namespace kdlae {
 namespace train {
 
-// Xcol[p][c * 27 + tap] = x[p + off(tap)][c] (zero padding 1 in frames, rows, columns); [P][27 C]
+// Xcol[p][tap * C + c] = x[p + off(tap)][c] (zero padding 1 in frames, rows, columns); [P][27 C]
 hipError_t launch_im2col3d(const float* x, int ldx, int C, int B, int F, int H, int W, float* col, hipStream_t s);
-// dx[q][c] (+)= sum_tap dcol[q - off(tap)][c * 27 + tap]
+// dx[q][c] (+)= sum_tap dcol[q - off(tap)][tap * C + c]
 hipError_t launch_col2im3d(const float* dcol, int C, int B, int F, int H, int W, float* dx, int lddx, int accumulate,
                            hipStream_t s);
+// Conv3d weight order: dir 0 [O][C][27] (OIDHW) -> [O][27][C] (the column order); dir 1 back
+hipError_t launch_wperm(const float* src, float* dst, int O, int C, int dir, hipStream_t s);
 hipError_t launch_relu(float* y, int ld, int C, long long P, hipStream_t s);
 // dy *= (y > 0)
 hipError_t launch_relu_mask(float* dy, int ldd, const float* y, int ldy, int C, long long P, hipStream_t s);

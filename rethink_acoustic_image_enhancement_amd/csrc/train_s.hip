@@ -3,9 +3,11 @@
 //
 // Activations are NDHWC: [B][F][H][W] pixels, channels contiguous at pixel stride ld.  The Conv3d
 // 3x3x3 (padding 1, KDLAE/KDLAE_model.py:386-393) goes through an explicit column matrix
-//   Xcol[p][c * 27 + tap],  tap = dt * 9 + dy * 3 + dx,  source pixel (f + dt - 1, y + dy - 1, x + dx - 1)
-// whose column order is the OIDHW weight's own ([Cout][Cin][3][3][3] = [Cout][Cin * 27]), so the forward
-// is Xcol . W^T, the weight gradient dZ^T . Xcol and the input gradient col2im(dZ . W).
+//   Xcol[p][tap * C + c],  tap = dt * 9 + dy * 3 + dx,  source pixel (f + dt - 1, y + dy - 1, x + dx - 1)
+// tap-major, so consecutive threads touch consecutive channels of one source pixel (coalesced on both
+// sides; a channel-major order made im2col / col2im 75% of the step).  The weights are permuted to the
+// same order per step ([Cout][27][Cin], launch_wperm), so the forward is Xcol . W'^T, the weight
+// gradient dZ^T . Xcol (permuted back into the OIDHW gradient) and the input gradient col2im(dZ . W').
 #include "train_kernels.h"
 #include "train_s.h"
 
@@ -34,48 +36,93 @@ inline unsigned grid_for(long long n, int per_block = kThreads) {
   return (unsigned)(g < 1 ? 1 : g);
 }
 
-// one thread per column element (p, k), k fastest: coalesced Xcol writes
-__global__ __launch_bounds__(kThreads) void im2col3d_kernel(const float* __restrict__ x, int ldx, int C, Geo g,
-                                                            float* __restrict__ col) {
-  const int K = 27 * C;
-  const long long n = (long long)g.B * g.F * g.H * g.W * K;
-  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-    const long long p = i / K;
-    const int k = (int)(i - p * K);
-    const int c = k / 27, tap = k - c * 27;
-    int b, f, y, xx;
-    g.coords(p, b, f, y, xx);
-    const int ff = f + tap / 9 - 1, yy = y + (tap / 3) % 3 - 1, xs = xx + tap % 3 - 1;
-    float v = 0.f;
-    if ((unsigned)ff < (unsigned)g.F && (unsigned)yy < (unsigned)g.H && (unsigned)xs < (unsigned)g.W)
-      v = x[((((long long)b * g.F + ff) * g.H + yy) * g.W + xs) * ldx + c];
-    col[i] = v;
+// 32-bit pixel coordinates (P < 2^31; only addresses are 64-bit: 64-bit division is a long software
+// sequence on CDNA and dominated the first version of these kernels)
+struct Geo32 {
+  int F, H, W;
+  __device__ void coords(int p, int& bf, int& f, int& y, int& x) const {
+    x = p % W;
+    int r = p / W;
+    y = r % H;
+    r /= H;
+    f = r % F;
+    bf = r - f;  // b * F
+  }
+};
+
+template <int V> struct VecT;
+template <> struct VecT<1> { using T = float; };
+template <> struct VecT<4> { using T = float4; };
+
+// Xcol rows are K = 27 C floats; a thread owns V consecutive channels of one (tap, channel group) column
+// slot, fixed for the whole launch, and walks pixels.  With KV = 27 C / V <= 256 slots a block covers
+// 256 / KV pixels per step; otherwise each block covers one pixel per step and threads stride the row.
+template <int V>
+__global__ __launch_bounds__(kThreads) void im2col3d_kernel(const float* __restrict__ x, int ldx, int C, Geo32 g,
+                                                            int P, float* __restrict__ col) {
+  using T = typename VecT<V>::T;
+  const int CV = C / V, KV = 27 * CV;
+  const int ppb = KV <= kThreads ? kThreads / KV : 1;
+  const int sub = KV <= kThreads ? (int)threadIdx.x / KV : 0;
+  if (sub >= ppb) return;
+  const int kv0 = KV <= kThreads ? (int)threadIdx.x - sub * KV : (int)threadIdx.x;
+  for (int p = blockIdx.x * ppb + sub; p < P; p += gridDim.x * ppb) {
+    int bf, f, y, xx;
+    g.coords(p, bf, f, y, xx);
+    T* dst = reinterpret_cast<T*>(col + (long long)p * 27 * C);
+    for (int kv = kv0; kv < KV; kv += kThreads) {
+      const int tap = kv / CV, c = (kv - tap * CV) * V;
+      const int ff = f + tap / 9 - 1, yy = y + (tap / 3) % 3 - 1, xs = xx + tap % 3 - 1;
+      T v;
+      if ((unsigned)ff < (unsigned)g.F && (unsigned)yy < (unsigned)g.H && (unsigned)xs < (unsigned)g.W)
+        v = *reinterpret_cast<const T*>(x + ((long long)((bf + ff) * g.H + yy) * g.W + xs) * ldx + c);
+      else
+        v = T{};
+      dst[kv] = v;
+    }
   }
 }
 
-// dX[q][c] (+)= sum over taps of dcol[q - off(tap)][c * 27 + tap] (the pixels whose window put q at that
-// tap): a gather, so every dX element is written once, in a fixed order (deterministic, no atomics)
-__global__ __launch_bounds__(kThreads) void col2im3d_kernel(const float* __restrict__ dcol, int C, Geo g,
+// dX[q][c] (+)= sum over taps of dcol[q - off(tap)][tap * C + c] (the pixels whose window put q at that
+// tap): a gather, so every dX element is written once, in a fixed order (deterministic, no atomics).
+// One thread per (pixel, V-channel group).
+template <int V>
+__global__ __launch_bounds__(kThreads) void col2im3d_kernel(const float* __restrict__ dcol, int C, Geo32 g, int P,
                                                             float* __restrict__ dx, int lddx, int accumulate) {
-  const long long n = (long long)g.B * g.F * g.H * g.W * C;
-  const int K = 27 * C;
-  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-    const long long q = i / C;
-    const int c = (int)(i - q * C);
-    int b, f, y, x;
-    g.coords(q, b, f, y, x);
-    float s = 0.f;
+  using T = typename VecT<V>::T;
+  const int CV = C / V;
+  const int n = P * CV;  // < 2^31 (checked by the launcher)
+  const long long K = 27LL * C;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const int q = i / CV;
+    const int c = (i - q * CV) * V;
+    int bf, f, y, x;
+    g.coords(q, bf, f, y, x);
+    T s{};
 #pragma unroll
     for (int tap = 0; tap < 27; ++tap) {
       // source pixel p with p + off(tap) = q
       const int pf = f - (tap / 9 - 1), py = y - ((tap / 3) % 3 - 1), px = x - (tap % 3 - 1);
       if ((unsigned)pf < (unsigned)g.F && (unsigned)py < (unsigned)g.H && (unsigned)px < (unsigned)g.W) {
-        const long long p = (((long long)b * g.F + pf) * g.H + py) * g.W + px;
-        s += dcol[p * K + c * 27 + tap];
+        const int p = ((bf + pf) * g.H + py) * g.W + px;
+        s += *reinterpret_cast<const T*>(dcol + p * K + tap * C + c);
       }
     }
-    float* d = dx + q * lddx + c;
+    T* d = reinterpret_cast<T*>(dx + (long long)q * lddx + c);
     *d = accumulate ? *d + s : s;
+  }
+}
+
+// dir 0: w [O][C][27] -> wp [O][27][C]; dir 1: the inverse
+__global__ __launch_bounds__(kThreads) void wperm_kernel(const float* __restrict__ src, float* __restrict__ dst, int O,
+                                                         int C, int dir) {
+  const int n = O * C * 27;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const int o = i / (27 * C), r = i - o * 27 * C;
+    const int c = r / 27, t = r - c * 27;  // i = OIDHW index
+    const int j = (o * 27 + t) * C + c;    // tap-major index
+    if (dir == 0) dst[j] = src[i];
+    else dst[i] = src[j];
   }
 }
 
@@ -214,17 +261,38 @@ __global__ void l1frames_final_kernel(const float* __restrict__ part, int nblk, 
 
 }  // namespace
 
+bool vec4_ok(const void* a, int ld, int C) { return C % 4 == 0 && ld % 4 == 0 && ((uintptr_t)a & 15) == 0; }
+
 hipError_t launch_im2col3d(const float* x, int ldx, int C, int B, int F, int H, int W, float* col, hipStream_t s) {
-  const long long n = (long long)B * F * H * W * 27 * C;
-  hipLaunchKernelGGL(im2col3d_kernel, dim3(grid_for(n)), dim3(kThreads), 0, s, x, ldx, C, Geo{B, F, H, W}, col);
+  const long long P = (long long)B * F * H * W;
+  if (P >= (1LL << 31)) return hipErrorInvalidValue;
+  const Geo32 g{F, H, W};
+  if (vec4_ok(x, ldx, C) && ((uintptr_t)col & 15) == 0) {
+    const int KV = 27 * C / 4, ppb = KV <= kThreads ? kThreads / KV : 1;
+    hipLaunchKernelGGL(im2col3d_kernel<4>, dim3(grid_for(P, ppb)), dim3(kThreads), 0, s, x, ldx, C, g, (int)P, col);
+  } else {
+    const int KV = 27 * C, ppb = KV <= kThreads ? kThreads / KV : 1;
+    hipLaunchKernelGGL(im2col3d_kernel<1>, dim3(grid_for(P, ppb)), dim3(kThreads), 0, s, x, ldx, C, g, (int)P, col);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_col2im3d(const float* dcol, int C, int B, int F, int H, int W, float* dx, int lddx, int accumulate,
                            hipStream_t s) {
-  const long long n = (long long)B * F * H * W * C;
-  hipLaunchKernelGGL(col2im3d_kernel, dim3(grid_for(n)), dim3(kThreads), 0, s, dcol, C, Geo{B, F, H, W}, dx, lddx,
-                     accumulate);
+  const long long P = (long long)B * F * H * W;
+  if (P * C >= (1LL << 31)) return hipErrorInvalidValue;
+  const Geo32 g{F, H, W};
+  if (vec4_ok(dx, lddx, C) && ((uintptr_t)dcol & 15) == 0)
+    hipLaunchKernelGGL(col2im3d_kernel<4>, dim3(grid_for(P * C / 4)), dim3(kThreads), 0, s, dcol, C, g, (int)P, dx,
+                       lddx, accumulate);
+  else
+    hipLaunchKernelGGL(col2im3d_kernel<1>, dim3(grid_for(P * C)), dim3(kThreads), 0, s, dcol, C, g, (int)P, dx, lddx,
+                       accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_wperm(const float* src, float* dst, int O, int C, int dir, hipStream_t s) {
+  hipLaunchKernelGGL(wperm_kernel, dim3(grid_for((long long)O * C * 27)), dim3(kThreads), 0, s, src, dst, O, C, dir);
   return hipGetLastError();
 }
 

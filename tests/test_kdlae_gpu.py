@@ -4,6 +4,7 @@ Tolerance: 1e-3 fp32 max-abs on hq and sr (BASELINE.json north_star).  Every tes
 cuda:0 and calls KDLAE_teacher.forward -> libkdlae.so; there is no fallback path to hide behind.
 """
 import glob
+import json
 import os
 
 import numpy as np
@@ -74,17 +75,20 @@ def test_rand_512_full_size():
 
 
 def test_mdd_512_config1():
-    """Config 1 (MDD sonar sample 512x512, denoise_rate 0.6).
+    """Config 1 (MDD sonar sample 512x512, denoise_rate 0.6), judged against the reference's fp64 output.
 
-    The reference's OWN fp32 output is 3.1e-3 (hq) / 3.4e-3 (sr) max-abs from its fp64 output on
-    this input, so no fp32 implementation that sums in a different order can be held to 1e-3 of the
-    reference fp32 numbers.  profiles/r03_config1_precision.txt localises that error: it comes from
-    torch's fp32 q.k^T / norm reductions over all HW pixels in MDTA (with those in fp64 the fp32
-    forward is 5e-4 from fp64).  The HIP path sums 1024-pixel slots in fp32 and the slots in fp64
-    (csrc/mdta.hip gram_reduce).  The bar, per output over every fixture sample (the [::8, ::8]
-    subsample plus one full row): ours is at least 25% closer to the reference fp64 output than the
-    reference fp32 is in max-abs, and no farther in the mean; PSNR >= 60 dB against the reference fp32."""
+    On this input the forward is ill-conditioned: multiplying the LayerNorm outputs of the reference's
+    own fp32 forward by (1 + u 2^-24), u ~ U[-1, 1] — what any other fp32 summation order produces —
+    moves its output 1.0e-3 .. 2.4e-3 (hq) / 1.0e-3 .. 2.9e-3 (sr) from fp64 over 8 seeds (median
+    2.0e-3 / 1.9e-3; tests/golden/t_mdd_512_ensemble.json, profiles/r04_config1_ensemble.txt), and the
+    unperturbed reference fp32 is 3.1e-3 / 3.4e-3 away.  The sensitivity sits in the full- and
+    double-resolution stages (profiles/r04_config1_sensitivity.txt), so no fp32 evaluation can be held
+    to 1e-3 of fp64 here except by chance.  The bar, per output over every fixture sample (the [::8, ::8]
+    subsample plus one full row): ours is no farther from fp64 than the MEDIAN perturbed-reference fp32
+    evaluation and than the reference fp32 itself (max-abs), no farther in the mean than the reference
+    fp32, and PSNR >= 60 dB against the reference fp32."""
     d, _ = load_fixture("t_mdd_512")
+    ens = json.load(open(os.path.join(GOLDEN, "t_mdd_512_ensemble.json")))
     d, out, sub = _run_512("t_mdd_512", mdd_input_tensor(d))
     for k, row, r32, r64, w32, w64 in (("hq", "hq_row", "hq_sub", "hq64_sub", "hq_row257", "hq64_row257"),
                                        ("sr", "sr_row", "sr_sub", "sr64_sub", "sr_row515", "sr64_row515")):
@@ -93,9 +97,12 @@ def test_mdd_512_config1():
         ref64 = torch.cat([torch.from_numpy(d[r64]).double().flatten(), torch.from_numpy(d[w64]).double().flatten()])
         e_ours, e_ref = float((ours - ref64).abs().max()), float((ref32 - ref64).abs().max())
         m_ours, m_ref = float((ours - ref64).abs().mean()), float((ref32 - ref64).abs().mean())
-        print(f"t_mdd_512 {k}: ours-vs-fp64 max {e_ours:.3e} mean {m_ours:.2e}; ref32-vs-fp64 max {e_ref:.3e} "
+        med = ens[k + "_median"]
+        print(f"t_mdd_512 {k}: ours-vs-fp64 max {e_ours:.3e} mean {m_ours:.2e}; perturbed-ref32 median {med:.3e} "
+              f"(range {min(ens[k + '_max']):.3e} .. {max(ens[k + '_max']):.3e}); ref32-vs-fp64 max {e_ref:.3e} "
               f"mean {m_ref:.2e}; ours-vs-ref32 max {float((ours - ref32).abs().max()):.3e}")
-        assert e_ours <= 0.75 * e_ref, (k, e_ours, e_ref)
+        assert e_ours <= med, (k, e_ours, med)
+        assert e_ours <= e_ref, (k, e_ours, e_ref)
         assert m_ours <= m_ref, (k, m_ours, m_ref)
         assert psnr(sub[k], torch.from_numpy(d[r32])) >= 60.0
 

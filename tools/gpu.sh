@@ -6,6 +6,7 @@
 #   smoke     __graft_entry__.smoke()
 #   bench     bench.py with the given args (default: the driver's default run)
 #   prof      rocprofv3 --kernel-trace --stats of the T16 bench and of the training bench
+#   profb     rocprofv3 --kernel-trace --stats of one bench.py run with the given args
 #   pmc       PMC passes over one T16 step: FETCH_SIZE, WRITE_SIZE, busy counters (one group per run)
 #   ab        library A/B: for each "name=path[,ENV=V...]" in $VARIANTS ("default" = in-tree build), the
 #             per-launch probe of class $PROBE (default 1) and a short T16 bench; CHECK=1 runs
@@ -53,6 +54,11 @@ prof)
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-bs1 --no-secondary > $O/prof_bench.log 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run -- python3 $R/bench.py --workload train --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_train.log 2>&1 || exit $?
+  ;;
+profb)  # rocprofv3 kernel trace + stats of one bench.py invocation (args)
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py "$@" > $O/prof_bench.log 2>&1 || exit $?
+  tail -2 $O/prof_bench.log
   ;;
 pmc)
   cd /tmp && export TMPDIR=/tmp
