@@ -81,7 +81,9 @@ def test_mdd_512_config1():
     own fp32 forward by (1 + u 2^-24), u ~ U[-1, 1] — what any other fp32 summation order produces —
     moves its output 1.0e-3 .. 2.4e-3 (hq) / 1.0e-3 .. 2.9e-3 (sr) from fp64 over 8 seeds (median
     2.0e-3 / 1.9e-3; tests/golden/t_mdd_512_ensemble.json, profiles/r04_config1_ensemble.txt), and the
-    unperturbed reference fp32 is 3.1e-3 / 3.4e-3 away.  The sensitivity sits in the full- and
+    unperturbed reference fp32 is 3.1e-3 / 3.4e-3 away; the same reference forward at torch thread
+    counts 8 / 4 / 2 / 1 is 3.1e-3 / 1.2e-3 / 7.5e-4 / 4.0e-3 (hq) from fp64 and up to 8.6e-3 from itself
+    (profiles/r04_config1_threads.txt).  The sensitivity sits in the full- and
     double-resolution stages (profiles/r04_config1_sensitivity.txt), so no fp32 evaluation can be held
     to 1e-3 of fp64 here except by chance.  The bar, per output over every fixture sample (the [::8, ::8]
     subsample plus one full row): ours is no farther from fp64 than the MEDIAN perturbed-reference fp32
