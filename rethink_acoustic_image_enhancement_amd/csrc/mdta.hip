@@ -205,10 +205,13 @@ __syncthreads();
 __host__ __device__ constexpr int gram_waves(int ct) {
   return ct == 1 ? 3 : ct == 2 ? 6 : ct == 3 ? 9 : ct == 4 ? 12 : ct == 5 ? 15 : ct == 6 ? 9 : ct == 7 ? 7 : 12;
 }
-// Ch = 96 ring: 10 waves (one block per CU) measured 2.3% faster per launch than 9 in alternating
-// same-box runs (profiles/r02_gram_ring6_waves10_probe.txt); 11 waves were slower
+// Ch = 96 ring: 12 waves (one block per CU).  The DMA waves are the ones without a v job, and at 10
+// waves only 2 of the 18 jobs' waves qualified: each issued 11 of the row's 21 LDS-DMA pieces, and that
+// issue (60-185 cycles a piece beside MFMAs) paced the row.  At 12 waves the v jobs ride as second jobs
+// on waves 0-5, waves 6-11 are DMA waves with 4 pieces each: 2170 -> 1847 us per C96@512^2 launch
+// (r04 same-box probe, gpurun_out/ring6b; 13 waves 1954, 14 1947, 16 2032)
 #ifndef KDLAE_RING6_WAVES
-#define KDLAE_RING6_WAVES 10
+#define KDLAE_RING6_WAVES 12
 #endif
 // r03 A/B (profiles/r03_gram_ab_probe.txt, retired): a stencil window rolled in registers across rows
 // (6 LDS reads per job and row instead of 18) and q / k staged transposed with a quad swizzle
@@ -388,10 +391,22 @@ struct GramRing {
   static constexpr int S = (Ch % 32 == 16) ? Ch : Ch + 16;
   static constexpr int Stage = 16 * S;  // floats per staging buffer
   static constexpr size_t lds_bytes = (size_t)NSlot * RowF4 * 16 + 4 * Stage * 4 + 2 * Ch * 4;
-  // DMA waves: the leading waves none of whose jobs (w, w + NW, ...) is a v job (job >= 2 CT)
+  // DMA waves: the waves none of whose jobs (w, w + NW, ...) is a v job (job >= 2 CT); with
+  // NW > 2 CT these are the trailing waves (the leading ones carry a second, v, job)
+  static constexpr bool has_v(int w) {
+    for (int jb = w; jb < NJ; jb += NW)
+      if (jb >= 2 * CT) return true;
+    return false;
+  }
   static constexpr int dma_waves() {
     int n = 0;
-    while (n < NW && n + NW * ((NJ - 1 - n) / NW) < 2 * CT) ++n;
+    for (int w = 0; w < NW; ++w) n += has_v(w) ? 0 : 1;
+    return n;
+  }
+  // rank of wave w among the DMA waves
+  static constexpr int dma_rank(int w) {
+    int n = 0;
+    for (int v = 0; v < w; ++v) n += has_v(v) ? 0 : 1;
     return n;
   }
   static constexpr int NDW = dma_waves();
@@ -444,10 +459,12 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
   }
   // DMA sources (DMA waves): piece k covers ring items 64k..64k+63; byte offset of the item's
   // column within an image row, ~0u -> zero line
+  const bool dma_wave = !R::has_v(wave);
+  const int drank = R::dma_rank(wave);
   unsigned colo[PPD];
 #pragma unroll
   for (int j = 0; j < PPD; ++j) {
-    const int k = min(wave + NDW * j, R::Pieces - 1);
+    const int k = min(drank + NDW * j, R::Pieces - 1);
     const int it = k * 64 + lane;
     const int px = it / PS4, r = it - (it / PS4) * PS4;
     const int xx = xs - 1 + px;
@@ -462,7 +479,7 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
     const bool oky = (unsigned)yy < (unsigned)p.H;
 #pragma unroll
     for (int j = 0; j < PPD; ++j) {
-      const int k = min(wave + NDW * j, R::Pieces - 1);
+      const int k = min(drank + NDW * j, R::Pieces - 1);
       const void* src = (oky && colo[j] != ~0u) ? (const void*)(Xb + (unsigned)yy * rowbytes + colo[j])
                                                  : (const void*)p.zeros;
       dma::dma16(src, sl + 64 * k);
@@ -563,7 +580,7 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
       buf ^= 1;
     }
   };
-  if (wave < NDW) run(std::true_type{});
+  if (dma_wave) run(std::true_type{});
   else run(std::false_type{});
 
   float* out = p.partial + (((long long)b * p.heads + h) * p.nslots + slot) * p.slot_floats;
