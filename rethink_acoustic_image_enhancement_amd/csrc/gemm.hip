@@ -86,14 +86,17 @@ __device__ __forceinline__ void load_a(const GemmParams& p, const float* __restr
   }
 }
 
-template <int KG>
+// STATS = false: the caller guarantees p.stats == nullptr (the straight-line resident kernels).  A
+// runtime stats branch there put its global load after the next tile's A prefetch, and the join of
+// the two paths waited vmcnt(0): every tile drained the prefetch and the previous tile's stores.
+template <int KG, bool STATS = true>
 __device__ __forceinline__ void apply_ln(const GemmParams& p, int b, int row0, int li, int HW,
                                          f32x4 (&a)[kGemmRT][KG]) {
   const float wb = (p.ln == 2) ? 1.f : 0.f;
 #pragma unroll
   for (int r = 0; r < kGemmRT; ++r) {
     float mean, rstd;
-    if (p.stats) {
+    if (STATS && p.stats) {
       const int prow = min(row0 + r * 16 + li, HW - 1);
       const float2 st = *reinterpret_cast<const float2*>(p.stats + 2 * ((long long)b * HW + prow));
       mean = st.x;
@@ -453,7 +456,11 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
   f32x4 a[kGemmRT][KG];
   [[maybe_unused]] f32x4 an[kGemmRT][KG];
   if constexpr (PF) load_rows(t_begin, an);
-  for (int tile = t_begin; tile < t_end; ++tile) {
+  // The tile body runs once peeled, then in the loop: hipcc's waitcnt pass merges the loop header's
+  // predecessors and keeps the smaller outstanding count, so with the prologue (12 loads in flight)
+  // as a predecessor it waited for the previous tile's stores before the next tile's first use of its
+  // prefetched rows; peeled, both predecessors have stores behind the prefetch.
+  auto body = [&](int tile) __attribute__((always_inline)) {
     int b, row0;
     rows_of(tile, b, row0);
     if (p.w_img_stride && b != staged) {  // block-uniform: the tile range crossed into the next image
@@ -471,7 +478,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
     } else {
       load_rows(tile, a);
     }
-    if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
+    if (p.ln) apply_ln<KG, false>(p, b, row0, li, HW, a);
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
     [[maybe_unused]] __amdgpu_buffer_rsrc_t rr;
     if constexpr (HASR) rr = buf_rsrc(p.R + (long long)b * HW * p.ldr, r_bytes);
@@ -583,7 +590,9 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
     }
     }
-  }
+  };
+  body(t_begin);
+  for (int tile = t_begin + 1; tile < t_end; ++tile) body(tile);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -655,10 +664,18 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
   // v rows are prefetched a tile ahead at K = 48; at K = 96 the extra 48 VGPRs would spill, and the
   // SIMD partner wave's MFMAs cover the load instead
   constexpr bool PFV = KG < 6;
+#ifndef KDLAE_ATTN_IN_PFX
+#define KDLAE_ATTN_IN_PFX 0
+#endif
+  constexpr bool PFX = PFV && KDLAE_ATTN_IN_PFX;  // x rows a tile ahead as well
   f32x4 a[kGemmRT][KG];
   [[maybe_unused]] f32x4 an[kGemmRT][KG];
+  [[maybe_unused]] f32x4 xn[kGemmRT][KG];
   if constexpr (PFV) load_rows(p.A, p.lda, a_bytes, t_begin, an);
-  for (int tile = t_begin; tile < t_end; ++tile) {
+  if constexpr (PFX) load_rows(p.R, p.ldr, r_bytes, t_begin, xn);
+  // first tile peeled, as in gemm_res_kernel: the loop header then has no predecessor without the
+  // previous tile's stores queued behind the v prefetch, so the first use of v waits for the loads only
+  auto body = [&](int tile) __attribute__((always_inline)) {
     int b, row0;
     rows_of(tile, b, row0);
     if (b != staged) {  // block-uniform: the tile range crossed into the next image
@@ -679,8 +696,16 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
     // the M GEMM; a one-tile-ahead prefetch of x measured no faster (registers).  At K = 96 the
     // x rows are loaded after the M GEMM: live across it they would spill
     f32x4 xr[kGemmRT][KG];
-    if constexpr (KG < 6) load_rows(p.R, p.ldr, r_bytes, tile, xr);
+    if constexpr (PFX) {
+#pragma unroll
+      for (int r = 0; r < kGemmRT; ++r)
+#pragma unroll
+        for (int g = 0; g < KG; ++g) xr[r][g] = xn[r][g];
+    } else if constexpr (KG < 6) {
+      load_rows(p.R, p.ldr, r_bytes, tile, xr);
+    }
     if constexpr (PFV) load_rows(p.A, p.lda, a_bytes, min(tile + 1, t_end - 1), an);  // next tile's v
+    if constexpr (PFX) load_rows(p.R, p.ldr, r_bytes, min(tile + 1, t_end - 1), xn);
     {
       f32x4 acc1[KG][kGemmRT];
 #pragma unroll
@@ -704,7 +729,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
         }
       }
     }
-    apply_ln<KG>(p, b, row0, li, HW, a);
+    apply_ln<KG, false>(p, b, row0, li, HW, a);
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
     unsigned vo[kGemmRT];
 #pragma unroll
@@ -731,7 +756,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
       }
       __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
     }
-  }
+  };
+  body(t_begin);
+  for (int tile = t_begin + 1; tile < t_end; ++tile) body(tile);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1099,7 +1126,8 @@ hipError_t launch_gemm_route(const GemmParams& p, int NT, int KG, int wpe, int g
 #undef X
     return hipErrorInvalidValue;
   }
-  if (route == 0 && res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && !p.relu) {
+  if (route == 0 && res && !c3 && p.out_mode == 0 && wpe == 2 && p.kgroups == KG && p.kchunks == 1 && !p.relu &&
+      !p.stats) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;
     const int nch = (p.group_tiles + NT - 1) / NT;
