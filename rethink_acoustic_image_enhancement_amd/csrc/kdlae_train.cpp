@@ -321,8 +321,25 @@ int queue_reduce(Ctx& c, const float* part, int nblk, int ncols, int pstride, fl
   return KDLAE_OK;
 }
 
+// Forward / input-gradient GEMMs of the deep low-resolution levels (M = 1536..6144 pixels at
+// 6 x 128^2, K up to 2042) fill a few hundred 64 x 64 tiles: under one wave of blocks on 256 CUs.
+// The K >= 1024 ones take the split-K partials too (launch_tgemm splits only where the grid is short).
+// r04 trace A/B (gpurun_out/trab): dX 1536 x 384 K 2042 0.544 -> 0.386 ms, 6144 x 192 K 1020 0.688 ->
+// 0.660; at K = 510 / 576 the partial round trip lost (0.42 -> 0.53, 0.42 -> 0.50 ms).
+#ifndef KDLAE_TRAIN_SPLIT_SMALL
+#define KDLAE_TRAIN_SPLIT_SMALL 1
+#endif
+constexpr long long kSplitSmallRows = 24576;  // below the row-streaming kernel's threshold
+constexpr int kSplitSmallK = 1000;
+
 // one tgemm launch; `what` (+ the shape) labels it in the launch trace
-int gemm(Ctx& c, const tr::TGemm& g, size_t cap, const std::string& what) {
+int gemm(Ctx& c, const tr::TGemm& g0, size_t cap, const std::string& what) {
+  tr::TGemm g = g0;
+  if (KDLAE_TRAIN_SPLIT_SMALL && cap == 0 && !g.partial && (long long)g.M * g.nz1 * g.nz2 < kSplitSmallRows &&
+      g.K >= kSplitSmallK) {
+    g.partial = c.splitk;
+    cap = kSplitCap;
+  }
   if (c.trace) {
     const std::string keep = c.tag;
     c.tag += " " + what + " M" + std::to_string(g.M) + " N" + std::to_string(g.N) + " K" + std::to_string(g.K) + " z" +
