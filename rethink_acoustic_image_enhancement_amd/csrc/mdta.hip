@@ -370,9 +370,9 @@ __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(
 //    4 pixel groups per wave) fall on 64 distinct banks.  Pad items and out-of-image pixels read
 //    p.zeros;
 //  * two wave classes.  "DMA waves" (those whose stencil jobs are all q/k) issue every ring DMA,
-//    exactly PPD pieces each per row (an uneven tail re-issues the last piece: same source, same
-//    destination), and their only VMEM ops are those DMAs, so "row y+2 has landed" is the
-//    compile-time s_waitcnt vmcnt(PPD * rows issued after it).  The other waves store v and never
+//    PPD or PPD - 1 pieces each per row (a compile-time count per instantiation; r03 re-issued the
+//    last piece of the short waves instead), and their only VMEM ops are those DMAs, so "row y+2
+//    has landed" is the compile-time s_waitcnt vmcnt(count * rows issued after it).  The other waves store v and never
 //    wait on vmcnt: the barrier after the DMA waves' wait covers them.  The loop body is
 //    instantiated per class, so neither carries the other's branches;
 //  * Gram MFMA k-step s takes pixel 4 s + (lane >> 4), so the q/k operand reads are
@@ -474,11 +474,14 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
   }
   const unsigned rowbytes = (unsigned)p.W * (unsigned)p.ld * 4u;
   const char* Xb = reinterpret_cast<const char*>(X);
-  auto issue = [&](int yy) {
+  // a DMA wave issues N = PPD or PPD - 1 pieces per row (ranks below Pieces % NDW carry the extra
+  // one), a compile-time count per instantiation of the loop body so its vmcnt waits stay exact
+  auto issue = [&](int yy, auto ntag) {
+    constexpr int N = decltype(ntag)::value;
     f32x4* sl = gring + ((yy + R::NSlot) % R::NSlot) * R::RowF4;
     const bool oky = (unsigned)yy < (unsigned)p.H;
 #pragma unroll
-    for (int j = 0; j < PPD; ++j) {
+    for (int j = 0; j < N; ++j) {
       const int k = min(drank + NDW * j, R::Pieces - 1);
       const void* src = (oky && colo[j] != ~0u) ? (const void*)(Xb + (unsigned)yy * rowbytes + colo[j])
                                                  : (const void*)p.zeros;
@@ -486,10 +489,11 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
     }
   };
   // DMA waves: wait until only the DMAs of the `ra` youngest rows are outstanding
-  auto wait_rows = [&](int ra) {
-    if (ra >= 3) dma::wait_vmcnt<3 * PPD>();
-    else if (ra == 2) dma::wait_vmcnt<2 * PPD>();
-    else if (ra == 1) dma::wait_vmcnt<PPD>();
+  auto wait_rows = [&](int ra, auto ntag) {
+    constexpr int N = decltype(ntag)::value;
+    if (ra >= 3) dma::wait_vmcnt<3 * N>();
+    else if (ra == 2) dma::wait_vmcnt<2 * N>();
+    else if (ra == 1) dma::wait_vmcnt<N>();
     else dma::wait_vmcnt<0>();
   };
 
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
 
   dma::wait_vmcnt<0>();  // the weight loads above, so the first stencil does not drain the ring
 
-  auto run = [&](auto dma_wave) {
+  auto run = [&](auto dma_wave, auto ntag) {
     constexpr bool D = decltype(dma_wave)::value;
     // stencil of output pixel s (of this lane's 4) of ring row r for every job; q/k -> staging
     // buffer sb, v -> HBM (non-DMA waves only)
@@ -542,9 +546,9 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
 
     // prologue: rows y0-1 .. min(y0+4, y1) in flight; stencil(y0) once rows y0-1..y0+1 landed
     if (D)
-      for (int yy = y0 - 1; yy <= min(y0 + 4, y1); ++yy) issue(yy);
+      for (int yy = y0 - 1; yy <= min(y0 + 4, y1); ++yy) issue(yy, ntag);
     if (y0 < y1) {
-      if (D) wait_rows(max(0, min(y0 + 4, y1) - (y0 + 1)));
+      if (D) wait_rows(max(0, min(y0 + 4, y1) - (y0 + 1)), ntag);
       dma::barrier_lds();
       load_win(y0);
 #pragma unroll
@@ -554,9 +558,9 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
     for (int y = y0; y < y1; ++y) {
       const bool st = y + 1 < y1;
       // rows y..y+2 landed: the younger DMAs are rows y+3 .. min(y+4, y1)
-      if (D && st) wait_rows(max(0, min(y + 4, y1) - (y + 2)));
+      if (D && st) wait_rows(max(0, min(y + 4, y1) - (y + 2)), ntag);
       dma::barrier_lds();
-      if (D && y + 5 <= y1) issue(y + 5);  // into the slot of row y-1, last read by stencil(y)
+      if (D && y + 5 <= y1) issue(y + 5, ntag);  // into the slot of row y-1, last read by stencil(y)
       float qv[PPW][4], kv[PPW][4];
 #pragma unroll
       for (int k = 0; k < PPW; ++k) {
@@ -580,8 +584,10 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
       buf ^= 1;
     }
   };
-  if (dma_wave) run(std::true_type{});
-  else run(std::false_type{});
+  constexpr int PX = R::Pieces % NDW;  // DMA ranks below PX issue PPD pieces, the rest PPD - 1
+  if (!dma_wave) run(std::false_type{}, std::integral_constant<int, 0>{});
+  else if (PX == 0 || drank < PX) run(std::true_type{}, std::integral_constant<int, PPD>{});
+  else run(std::true_type{}, std::integral_constant<int, (PX == 0 ? PPD : PPD - 1)>{});
 
   float* out = p.partial + (((long long)b * p.heads + h) * p.nslots + slot) * p.slot_floats;
 #pragma unroll
