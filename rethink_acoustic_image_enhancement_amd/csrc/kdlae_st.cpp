@@ -18,6 +18,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "kernels.h"
 #include "runtime.h"
 #include "train_kernels.h"
 #include "train_s.h"
@@ -44,13 +45,16 @@ struct kdlae_st_handle {
 namespace {
 
 constexpr size_t kPartialFloats = 16u << 20;  // split-K partials of the weight-gradient GEMMs
+#ifndef KDLAE_ST_DX_CONV
+#define KDLAE_ST_DX_CONV 1
+#endif
 constexpr int kColsumBlocks = 256;
 
 struct SPlanT {
   size_t total = 0;
   std::vector<size_t> ea, e, pool, ua, da, dd, dl, gskip;  // per level / decoder
   std::unordered_map<std::string, size_t> xcol;            // each Conv3d's forward column matrix
-  size_t fa = 0, fo = 0, col = 0, gA = 0, gB = 0, partial = 0, part = 0, wp = 0, dwp = 0;
+  size_t fa = 0, fo = 0, col = 0, gA = 0, gB = 0, partial = 0, part = 0, wp = 0, dwp = 0, wpk = 0, zb = 0;
   size_t take(long long floats) {
     const size_t o = total;
     total += ((size_t)floats * 4 + 255) / 256 * 256;
@@ -115,6 +119,8 @@ SPlanT make_plan(const kdlae_st_handle* h, int B, int F, int H, int W) {
   for (int i = 0; i <= L; ++i) wmax = std::max(wmax, 27LL * h->hc[i] * std::max(i ? h->hc[i - 1] : 1, h->hc[i]));
   pl.wp = pl.take(wmax);
   pl.dwp = pl.take(wmax);
+  pl.wpk = pl.take(wmax + 16LL * 27 * 16);  // packed dX weights (channel counts padded to 16)
+  pl.zb = pl.take(64);                      // a zero bias for the inference conv kernels
   pl.gA = pl.take(gmax);
   pl.gB = pl.take(gmax);
   pl.partial = pl.take((long long)kPartialFloats);
@@ -199,6 +205,32 @@ int conv_bwd(Ctx& c, const std::string& p, const float* X, int cin, const float*
   TRY(gemm(c, g, true));
   HIPCHK(tr::launch_wperm(dwp, c.G(p + ".weight"), cout, cin, 1, c.s));
   if (!dX) return KDLAE_OK;
+  // dX = the forward conv of dZ with flipped taps (cout -> cin channels) on the inference kernels:
+  // conv3d_c16 for 16 -> 16, conv_lds for 2..16 output tiles; no column matrix, no col2im
+  if (KDLAE_ST_DX_CONV && cout % 16 == 0 && cin % 16 == 0 && ((cin == 16 && cout == 16) ||
+                                                               conv_lds_supported(3, cin / 16, cout))) {
+    float* wpk = c.buf(c.pl.wpk);
+    HIPCHK(tr::launch_pack_dx(c.P(p + ".weight"), cout, cin, wpk, c.s));
+    if (cin == 16 && cout == 16) {
+      Conv3dC16Params q{};
+      q.in = dY; q.ldi = cout;
+      q.wp = wpk; q.bias = c.buf(c.pl.zb);
+      q.out = dX; q.ldo = cin;
+      q.Bn = c.B; q.F = c.F; q.H = Hl; q.W = Wl;
+      q.relu = 0; q.kt = 3;
+      HIPCHK(launch_conv3d_c16(q, c.s));
+    } else {
+      ConvLdsParams q{};
+      q.in = dY; q.ldi = cout; q.cin_pad = cout;
+      q.wp = wpk; q.ntiles = cin / 16; q.kgroups = 27 * cout / 16;
+      q.bias = nullptr;
+      q.out = dX; q.ldo = cin;
+      q.Bn = c.B; q.F = c.F; q.H = Hl; q.W = Wl;
+      q.kt = 3; q.relu = 0;
+      HIPCHK(launch_conv_lds(q, c.s));
+    }
+    return KDLAE_OK;
+  }
   HIPCHK(tr::launch_wperm(c.P(p + ".weight"), wp, cout, cin, 0, c.s));
   tr::TGemm d;  // dXcol = dZ . W', then the gather
   d.A = dY; d.sam = cout; d.sak = 1;
@@ -442,6 +474,7 @@ int kdlae_st_backward(kdlae_st_handle* h, const float* theta, const float* dout,
   if ((int64_t)c.pl.total > workspace_bytes) return fail(KDLAE_ESTATE, "training workspace too small");
   DeviceGuard dg(h->device);
   HIPCHK(hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), c.s));  // the pad floats stay zero
+  HIPCHK(hipMemsetAsync(c.buf(c.pl.zb), 0, 64 * sizeof(float), c.s));
   return net_bwd(c, h->x, dout);
 }
 

@@ -126,6 +126,23 @@ __global__ __launch_bounds__(kThreads) void wperm_kernel(const float* __restrict
   }
 }
 
+// Fragment-order weights (gemm.hip's packed layout: record (t, g) = [64 lanes][4], lane (li, lq)
+// holding output channel 16t + li, k = 16g + 4lq + e) of the input-gradient conv
+//   dX[q][c] = sum_{tap, o} dZ[q + off(tap)][o] Wd[c][tap * cout_pad + o],  Wd = W[o][c][26 - tap]
+// (the transposed conv is the forward conv of dZ with the taps flipped and the channel roles swapped).
+__global__ __launch_bounds__(kThreads) void pack_dx_kernel(const float* __restrict__ w, int cout, int cin,
+                                                           int cout_pad, int ntiles, int kgroups,
+                                                           float* __restrict__ wp) {
+  const int n_all = ntiles * kgroups * 256;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n_all; i += gridDim.x * kThreads) {
+    const int t = i / (kgroups * 256), r = i - t * kgroups * 256;
+    const int g = r >> 8, lane = (r >> 2) & 63, e = r & 3;
+    const int n = 16 * t + (lane & 15), k = 16 * g + 4 * (lane >> 4) + e;
+    const int tap = k / cout_pad, o = k - tap * cout_pad;
+    wp[i] = (n < cin && o < cout && tap < 27) ? w[((long long)o * cin + n) * 27 + (26 - tap)] : 0.f;
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void relu_kernel(float* __restrict__ y, int ld, int C, long long P) {
   const long long n = P * C;
   for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
@@ -293,6 +310,13 @@ hipError_t launch_col2im3d(const float* dcol, int C, int B, int F, int H, int W,
 
 hipError_t launch_wperm(const float* src, float* dst, int O, int C, int dir, hipStream_t s) {
   hipLaunchKernelGGL(wperm_kernel, dim3(grid_for((long long)O * C * 27)), dim3(kThreads), 0, s, src, dst, O, C, dir);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_dx(const float* w, int cout, int cin, float* wp, hipStream_t s) {
+  const int cout_pad = (cout + 15) / 16 * 16, ntiles = (cin + 15) / 16, kgroups = 27 * cout_pad / 16;
+  hipLaunchKernelGGL(pack_dx_kernel, dim3(grid_for((long long)ntiles * kgroups * 256)), dim3(kThreads), 0, s, w, cout,
+                     cin, cout_pad, ntiles, kgroups, wp);
   return hipGetLastError();
 }
 
