@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -48,6 +49,9 @@ constexpr size_t kPartialFloats = 16u << 20;  // split-K partials of the weight-
 #ifndef KDLAE_ST_DX_CONV
 #define KDLAE_ST_DX_CONV 1
 #endif
+#ifndef KDLAE_ST_DIRECT
+#define KDLAE_ST_DIRECT 1
+#endif
 constexpr int kColsumBlocks = 256;
 
 struct SPlanT {
@@ -66,11 +70,24 @@ long long npx(const kdlae_st_handle* h, int lvl, int B, int F, int H, int W) {
   return (long long)B * F * (H >> lvl) * (W >> lvl);
 }
 
+// A Conv3d whose channel counts are multiples of 16 on a level at least 16 wide runs "direct": the
+// forward on the inference conv kernels (conv3d_c16 for 16 -> 16, conv_lds for 2..16 output tiles) and
+// the weight gradient on the pixel-reduction GEMM with an implicit im2col B (bmode 4); no column
+// matrix.  The others (the 1-channel input conv, odd widths) go through Xcol.
+bool conv_direct(int cin, int cout, int Wl) {
+  if (!KDLAE_ST_DIRECT || cin % 16 || cout % 16 || Wl % 16) return false;
+  return (cin == 16 && cout == 16) || conv_lds_supported(3, cout / 16, cin);
+}
+// the input gradient of a Conv3d on the inference conv kernels (flipped taps, cout -> cin)
+bool dx_direct(int cin, int cout) {
+  return KDLAE_ST_DX_CONV && cout % 16 == 0 && cin % 16 == 0 &&
+         ((cin == 16 && cout == 16) || conv_lds_supported(3, cin / 16, cout));
+}
+
 SPlanT make_plan(const kdlae_st_handle* h, int B, int F, int H, int W) {
   SPlanT pl;
   const int L = h->L;
-  long long colmax = 0, gmax = 0;
-  int cin = 1;
+  long long colmax = 0, gmax = 0;  // colmax: set below
   for (int i = 0; i < L; ++i) {
     const long long P = npx(h, i, B, F, H, W);
     const int c = h->hc[i];
@@ -78,14 +95,11 @@ SPlanT make_plan(const kdlae_st_handle* h, int B, int F, int H, int W) {
     pl.e.push_back(pl.take(P * c));
     pl.pool.push_back(pl.take(P / 4 * c));
     pl.gskip.push_back(pl.take(P * c));
-    colmax = std::max(colmax, P * 27 * std::max(cin, c));
     gmax = std::max(gmax, P * c);
-    cin = c;
   }
   const long long PL = npx(h, L, B, F, H, W);
   pl.fa = pl.take(PL * h->hc[L]);
   pl.fo = pl.take(PL * h->hc[L]);
-  colmax = std::max(colmax, PL * 27 * std::max(cin, h->hc[L]));
   gmax = std::max(gmax, PL * h->hc[L]);
   for (int j = 0; j < L; ++j) {
     const int i = L - 1 - j;
@@ -95,26 +109,31 @@ SPlanT make_plan(const kdlae_st_handle* h, int B, int F, int H, int W) {
     pl.dd.push_back(pl.take(P * c));  // D = shuffle(U) + b + skip
     pl.da.push_back(pl.take(P * c));
     pl.dl.push_back(pl.take(P * c));
-    colmax = std::max(colmax, P * 27 * c);
   }
-  pl.col = pl.take(colmax);  // the input-gradient columns dZ . W' (and the ConvTranspose dU)
-  // every Conv3d's Xcol is kept from the forward for its weight gradient (about 4.4 GB at KDLAES.yml's
-  // B 4 x 7 x 128^2: one HBM write + read instead of a second im2col per conv)
+  // per Conv3d (name, input channels, output channels, level): its Xcol (only for the convs that are
+  // not direct) is kept from the forward for its weight gradient
+  std::vector<std::tuple<std::string, int, int, int>> convs;
   for (int i = 0; i < L; ++i) {
-    const long long P = npx(h, i, B, F, H, W);
     const std::string p = "encoders." + std::to_string(i);
-    pl.xcol[p + ".0"] = pl.take(P * 27 * (i ? h->hc[i - 1] : 1));
-    pl.xcol[p + ".2"] = pl.take(P * 27 * h->hc[i]);
+    convs.emplace_back(p + ".0", i ? h->hc[i - 1] : 1, h->hc[i], i);
+    convs.emplace_back(p + ".2", h->hc[i], h->hc[i], i);
   }
-  pl.xcol["st_fusion.0"] = pl.take(PL * 27 * h->hc[L - 1]);
-  pl.xcol["st_fusion.2"] = pl.take(PL * 27 * h->hc[L]);
+  convs.emplace_back("st_fusion.0", h->hc[L - 1], h->hc[L], L);
+  convs.emplace_back("st_fusion.2", h->hc[L], h->hc[L], L);
   for (int j = 0; j < L; ++j) {
     const int i = L - 1 - j;
-    const long long P = npx(h, i, B, F, H, W);
     const std::string d = "decoders." + std::to_string(j);
-    pl.xcol[d + ".0"] = pl.take(P * 27 * h->hc[i]);
-    pl.xcol[d + ".2"] = pl.take(P * 27 * h->hc[i]);
+    convs.emplace_back(d + ".0", h->hc[i], h->hc[i], i);
+    convs.emplace_back(d + ".2", h->hc[i], h->hc[i], i);
   }
+  // scratch: the dX columns of the convs whose dX is not direct, and the ConvTranspose dU
+  for (int i = 0; i < L; ++i) colmax = std::max(colmax, npx(h, i, B, F, H, W) * h->hc[i]);
+  for (auto& [name, ci, co, lvl] : convs) {
+    const long long P = npx(h, lvl, B, F, H, W);
+    if (!dx_direct(ci, co)) colmax = std::max(colmax, P * 27 * ci);
+    if (!conv_direct(ci, co, W >> lvl)) pl.xcol[name] = pl.take(P * 27 * ci);
+  }
+  pl.col = pl.take(colmax);
   long long wmax = 0;  // the largest Conv3d weight, for its tap-major copy and gradient
   for (int i = 0; i <= L; ++i) wmax = std::max(wmax, 27LL * h->hc[i] * std::max(i ? h->hc[i - 1] : 1, h->hc[i]));
   pl.wp = pl.take(wmax);
@@ -166,10 +185,34 @@ int colsum(Ctx& c, const float* x, int ld, int ncols, long long rows, float* out
   return KDLAE_OK;
 }
 
-// Y = relu(Xcol . W'^T + b) over P pixels at level lvl (W' = the weight in tap-major order)
+// Y = relu(conv(X, W) + b) on the inference kernels (conv_direct) or as Xcol . W'^T + b (W' = the weight
+// in the columns' tap-major order) over P pixels at level lvl
 int conv_fwd(Ctx& c, const std::string& p, const float* X, int cin, float* Y, int cout, int lvl) {
   const int Hl = c.H >> lvl, Wl = c.W >> lvl;
   const long long P = (long long)c.B * c.F * Hl * Wl;
+  if (conv_direct(cin, cout, Wl)) {
+    float* wpk = c.buf(c.pl.wpk);
+    HIPCHK(tr::launch_pack_conv(c.P(p + ".weight"), cout, cin, 0, wpk, c.s));
+    if (cin == 16 && cout == 16) {
+      Conv3dC16Params q{};
+      q.in = X; q.ldi = cin;
+      q.wp = wpk; q.bias = c.P(p + ".bias");
+      q.out = Y; q.ldo = cout;
+      q.Bn = c.B; q.F = c.F; q.H = Hl; q.W = Wl;
+      q.relu = 1; q.kt = 3;
+      HIPCHK(launch_conv3d_c16(q, c.s));
+    } else {
+      ConvLdsParams q{};
+      q.in = X; q.ldi = cin; q.cin_pad = cin;
+      q.wp = wpk; q.ntiles = cout / 16; q.kgroups = 27 * cin / 16;
+      q.bias = c.P(p + ".bias");
+      q.out = Y; q.ldo = cout;
+      q.Bn = c.B; q.F = c.F; q.H = Hl; q.W = Wl;
+      q.kt = 3; q.relu = 1;
+      HIPCHK(launch_conv_lds(q, c.s));
+    }
+    return KDLAE_OK;
+  }
   float* col = c.buf(c.pl.xcol.at(p));
   float* wp = c.buf(c.pl.wp);
   HIPCHK(tr::launch_wperm(c.P(p + ".weight"), wp, cout, cin, 0, c.s));
@@ -192,25 +235,29 @@ int conv_bwd(Ctx& c, const std::string& p, const float* X, int cin, const float*
   const long long P = (long long)c.B * c.F * Hl * Wl;
   HIPCHK(tr::launch_relu_mask(dY, cout, Y, cout, cout, P, c.s));
   TRY(colsum(c, dY, cout, cout, P, c.G(p + ".bias")));
-  (void)X;  // its columns are the forward's
-  const float* xcol = c.buf(c.pl.xcol.at(p));
   float* col = c.buf(c.pl.col);
   float* wp = c.buf(c.pl.wp);
   float* dwp = c.buf(c.pl.dwp);
   tr::TGemm g;  // dW'[o][k] = sum_p dZ[p][o] Xcol[p][k], then back to OIDHW order
   g.A = dY; g.sam = 1; g.sak = cout;
-  g.B = xcol; g.sbk = 27LL * cin; g.sbn = 1;
   g.C = dwp; g.scm = 27LL * cin; g.scn = 1;
   g.M = cout; g.N = 27 * cin; g.K = (int)P;
-  TRY(gemm(c, g, true));
+  if (conv_direct(cin, cout, Wl)) {  // Xcol implicit: the pixel-reduction kernel's bmode 4 reads X
+    g.B = X; g.sbk = cin; g.sbn = 1; g.bmode = 4;
+    g.Bn = c.B; g.F = c.F; g.H = Hl; g.W = Wl; g.Cg = cin;
+    g.partial = c.buf(c.pl.partial);
+    HIPCHK(tr::launch_tgemm_cols(g, kPartialFloats, c.s));
+  } else {  // the forward's columns
+    g.B = c.buf(c.pl.xcol.at(p)); g.sbk = 27LL * cin; g.sbn = 1;
+    TRY(gemm(c, g, true));
+  }
   HIPCHK(tr::launch_wperm(dwp, c.G(p + ".weight"), cout, cin, 1, c.s));
   if (!dX) return KDLAE_OK;
   // dX = the forward conv of dZ with flipped taps (cout -> cin channels) on the inference kernels:
   // conv3d_c16 for 16 -> 16, conv_lds for 2..16 output tiles; no column matrix, no col2im
-  if (KDLAE_ST_DX_CONV && cout % 16 == 0 && cin % 16 == 0 && ((cin == 16 && cout == 16) ||
-                                                               conv_lds_supported(3, cin / 16, cout))) {
+  if (dx_direct(cin, cout)) {
     float* wpk = c.buf(c.pl.wpk);
-    HIPCHK(tr::launch_pack_dx(c.P(p + ".weight"), cout, cin, wpk, c.s));
+    HIPCHK(tr::launch_pack_conv(c.P(p + ".weight"), cout, cin, 1, wpk, c.s));
     if (cin == 16 && cout == 16) {
       Conv3dC16Params q{};
       q.in = dY; q.ldi = cout;

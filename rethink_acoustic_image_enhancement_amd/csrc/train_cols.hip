@@ -46,7 +46,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, long l
 }
 constexpr unsigned kOOB = 0x80000000u;
 
-template <int TM, int TN>
+template <int TM, int TN, bool IMPB>
 __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
   const TGemm& g = a.g;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -61,7 +61,10 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
   const float* A = g.A + z1 * g.bA1 + z2 * g.bA2;
   const float* B = g.B + z1 * g.bB1 + z2 * g.bB2;
   const __amdgpu_buffer_rsrc_t ra = rsrc(A, (long long)(p1 - 1) * g.sak * 4 + 4LL * g.M);
-  const __amdgpu_buffer_rsrc_t rb = rsrc(B, (long long)(p1 - 1) * g.sbk * 4 + 4LL * g.N);
+  // (IMPB: a chunk's shifted rows reach past it, so the whole tensor; the chunks are whole 16-pixel
+  // stages there, K = Bn F H W with W % 16 == 0)
+  const __amdgpu_buffer_rsrc_t rb =
+      IMPB ? rsrc(B, (long long)g.K * g.sbk * 4) : rsrc(B, (long long)(p1 - 1) * g.sbk * 4 + 4LL * g.N);
   // this lane's byte offset of pixel lq, column 16 tile + li, per tile (kOOB past M / N); a k-step
   // adds a wave-uniform pixel offset.  Pixels >= p1 fall past the descriptor range by themselves
   // (row stride >= M, N), so no load carries a per-lane condition.
@@ -72,10 +75,21 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
     const int m = (wm * TM + i) * 16 + li;
     am[i] = m < g.M ? (unsigned)lq * sa + 4u * (unsigned)m : kOOB;
   }
+  // IMPB: tile t's 16 columns are channels c0..c0+15 of one tap (Cg % 16 == 0)
+  [[maybe_unused]] int tdf[TN], tdy[TN], tdx[TN], tdel[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
     const int n = (wn * TN + t) * 16 + li;
-    bn[t] = n < g.N ? (unsigned)lq * sb + 4u * (unsigned)n : kOOB;
+    if constexpr (IMPB) {
+      const int tap = ((wn * TN + t) * 16) / g.Cg;
+      tdf[t] = tap / 9 - 1;
+      tdy[t] = (tap / 3) % 3 - 1;
+      tdx[t] = tap % 3 - 1;
+      tdel[t] = (tdf[t] * g.H + tdy[t]) * g.W + tdx[t];
+      bn[t] = n < g.N ? 4u * (unsigned)(n - tap * g.Cg) : kOOB;
+    } else {
+      bn[t] = n < g.N ? (unsigned)lq * sb + 4u * (unsigned)n : kOOB;
+    }
   }
 
   f32x4 acc[TM][TN];
@@ -86,6 +100,18 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
 
   // stage = kU k-steps = 4 kU pixels: lane reads pixel q + 4u + lq for u < kU
   auto load = [&](int q, float (&av)[kU][TM], float (&bv)[kU][TN]) {
+    // IMPB: the stage's 16 pixels q .. q + 15 lie in one image row (q % 16 == 0, W % 16 == 0)
+    [[maybe_unused]] int x0 = 0, y = 0, f = 0;
+    [[maybe_unused]] bool rok[TN];
+    if constexpr (IMPB) {
+      const int row = q / g.W;
+      x0 = q - row * g.W;
+      y = row % g.H;
+      f = (row / g.H) % g.F;
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        rok[t] = (unsigned)(f + tdf[t]) < (unsigned)g.F && (unsigned)(y + tdy[t]) < (unsigned)g.H;
+    }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const unsigned pa = (unsigned)(q + 4 * u) * sa, pb = (unsigned)(q + 4 * u) * sb;
@@ -93,8 +119,17 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
       for (int i = 0; i < TM; ++i)
         av[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, (int)(am[i] + pa), 0, 0));
 #pragma unroll
-      for (int t = 0; t < TN; ++t)
-        bv[u][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (int)(bn[t] + pb), 0, 0));
+      for (int t = 0; t < TN; ++t) {
+        unsigned off;
+        if constexpr (IMPB) {
+          const int x = x0 + 4 * u + lq;
+          const bool ok = rok[t] && (unsigned)(x + tdx[t]) < (unsigned)g.W && bn[t] != kOOB;
+          off = ok ? (unsigned)(q + 4 * u + lq + tdel[t]) * sb + bn[t] : kOOB;
+        } else {
+          off = bn[t] + pb;
+        }
+        bv[u][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (int)off, 0, 0));
+      }
     }
   };
   auto compute = [&](const float (&av)[kU][TM], const float (&bv)[kU][TN]) {
@@ -135,12 +170,12 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
 }
 
 // blocks of this variant resident on the whole chip (hipOccupancy..., cached)
-template <int TM, int TN>
+template <int TM, int TN, bool IMPB>
 int slots() {
   static int n = 0;
   if (!n) {
     int b = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&tgemm_cols_kernel<TM, TN>),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&tgemm_cols_kernel<TM, TN, IMPB>),
                                                      kThreads, 0) != hipSuccess || b < 1)
       b = 1;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
@@ -157,9 +192,9 @@ int slots() {
 #ifndef KDLAE_COLS_MIN
 #define KDLAE_COLS_MIN 256
 #endif
-template <int TM, int TN>
+template <int TM, int TN, bool IMPB>
 hipError_t launch_tt(TGemm g, ColsArgs a, int gy, long long batch, size_t partial_cap, hipStream_t s) {
-  long long splits = ((long long)slots<TM, TN>() + gy * batch - 1) / (gy * batch);
+  long long splits = ((long long)slots<TM, TN, IMPB>() + gy * batch - 1) / (gy * batch);
   const long long maxs = (g.K + KDLAE_COLS_MIN - 1) / KDLAE_COLS_MIN;
   if (splits > maxs) splits = maxs;
   const long long cap = (long long)(partial_cap / ((size_t)g.M * g.N * batch));
@@ -172,7 +207,7 @@ hipError_t launch_tt(TGemm g, ColsArgs a, int gy, long long batch, size_t partia
   a.splits = (int)splits;
   g.splits = (int)splits;
   a.g = g;
-  hipLaunchKernelGGL((tgemm_cols_kernel<TM, TN>), dim3((unsigned)splits, (unsigned)gy, (unsigned)batch), dim3(kThreads),
+  hipLaunchKernelGGL((tgemm_cols_kernel<TM, TN, IMPB>), dim3((unsigned)splits, (unsigned)gy, (unsigned)batch), dim3(kThreads),
                      0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -182,8 +217,11 @@ hipError_t launch_tt(TGemm g, ColsArgs a, int gy, long long batch, size_t partia
 }  // namespace
 
 bool tgemm_cols_eligible(const TGemm& g) {
-  if (g.amode != 0 || g.bmode != 0 || g.alpha != 1.f || !g.partial) return false;
+  if (g.amode != 0 || (g.bmode != 0 && g.bmode != 4) || g.alpha != 1.f || !g.partial) return false;
   if (g.sam != 1 || g.sbn != 1 || g.M <= 0 || g.N <= 0 || g.K <= 0) return false;
+  if (g.bmode == 4 && (g.Cg <= 0 || g.Cg % 16 || g.W % 16 || g.N != 27 * g.Cg || g.nz1 * g.nz2 != 1 || g.F < 1 ||
+                       (long long)g.Bn * g.F * g.H * g.W != g.K || g.sbk < g.Cg))
+    return false;
   if ((long long)g.K * g.sak * 4 >= (1LL << 31) - 64 || (long long)g.K * g.sbk * 4 >= (1LL << 31) - 64) return false;
   return true;
 }
@@ -208,8 +246,10 @@ hipError_t launch_tgemm_cols(TGemm g, size_t partial_cap, hipStream_t s) {
   const int wtiles = a.wtm * a.wtn;
   const int gy = (wtiles + 3) / 4;
   const long long batch = (long long)g.nz1 * g.nz2;
-#define TT(m, n) \
-  if (TM == m && TN == n) return launch_tt<m, n>(g, a, gy, batch, partial_cap, s);
+#define TT(m, n)                                                                                     \
+  if (TM == m && TN == n)                                                                            \
+    return g.bmode == 4 ? launch_tt<m, n, true>(g, a, gy, batch, partial_cap, s)                      \
+                        : launch_tt<m, n, false>(g, a, gy, batch, partial_cap, s);
   TT(2, 2) TT(2, 3) TT(2, 4) TT(3, 2) TT(3, 3) TT(3, 4) TT(4, 2) TT(4, 3)
 #undef TT
   return hipErrorInvalidValue;

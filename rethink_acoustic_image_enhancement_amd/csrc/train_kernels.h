@@ -19,6 +19,9 @@ namespace train {
 //   bmode 1: B(k = pixel, n = c) = B[(pixel shifted by tap z2)*ldb + c] with zero padding (conv dW).
 //   bmode 2: 3x3 weight OIHW, k = tap*Cg + c: B = W[n][c][tap]      (conv forward)
 //   bmode 3: 3x3 weight OIHW, k = tap*Cg + c: B = W[c][n][8 - tap]  (conv dX, a transposed conv)
+//   bmode 4: implicit 3x3x3 im2col of an NDHWC view B ([Bn][F][H][W] pixels at stride sbk):
+//            B(k = pixel, n = tap*Cg + c) = B[(pixel shifted by tap) * sbk + c], zero padding 1
+//            (Conv3d weight gradient; pixel-reduction kernel only, Cg % 16 == 0, W % 16 == 0)
 // Batch: z = z1 * nz2 + z2, every operand offset by z1*b?1 + z2*b?2.
 // splits > 1: K is cut into `splits` chunks whose partial sums go to `partial`
 // ([batch][splits][M][N]) and a fixed-order reduce applies the epilogue (deterministic).
@@ -33,8 +36,8 @@ struct TGemm {
   int M = 0, N = 0, K = 0;
   int nz1 = 1, nz2 = 1;
   long long bA1 = 0, bA2 = 0, bB1 = 0, bB2 = 0, bC1 = 0, bC2 = 0, bR1 = 0, bR2 = 0, brs1 = 0, brs2 = 0;
-  // im2col geometry (amode 1 / bmode 1..3)
-  int Bn = 0, H = 0, W = 0, Cg = 0, dil = 1; long long lda = 0, ldb = 0;
+  // im2col geometry (amode 1 / bmode 1..4; F: frames of the 3x3x3 bmode 4)
+  int Bn = 0, H = 0, W = 0, Cg = 0, dil = 1, F = 1; long long lda = 0, ldb = 0;
   int splits = 1; float* partial = nullptr;
   // the C view's row pad [N, ld4(N)) belongs to nobody else (a ld-rounded private buffer): a
   // kernel may store whole float4 quads there (zeros: the weights past N are zero)

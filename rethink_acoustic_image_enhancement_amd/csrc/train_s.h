@@ -15,9 +15,10 @@ hipError_t launch_col2im3d(const float* dcol, int C, int B, int F, int H, int W,
                            hipStream_t s);
 // Conv3d weight order: dir 0 [O][C][27] (OIDHW) -> [O][27][C] (the column order); dir 1 back
 hipError_t launch_wperm(const float* src, float* dst, int O, int C, int dir, hipStream_t s);
-// packed (fragment-order, k = tap * cout_pad + o) weights of the input-gradient conv of a Conv3d 3x3x3
-// [cout][cin][27]: output channel c, taps flipped; ceil(cin/16) * 27 cout_pad/16 * 256 floats
-hipError_t launch_pack_dx(const float* w, int cout, int cin, float* wp, hipStream_t s);
+// packed (fragment-order, k = tap * in_pad + c) weights of a Conv3d 3x3x3 [cout][cin][27] for the inference
+// conv kernels: dx = 0 the forward conv (cout outputs), dx = 1 the input-gradient conv (cin outputs, taps
+// flipped); ceil(nout/16) * 27 in_pad/16 * 256 floats
+hipError_t launch_pack_conv(const float* w, int cout, int cin, int dx, float* wp, hipStream_t s);
 hipError_t launch_relu(float* y, int ld, int C, long long P, hipStream_t s);
 // dy *= (y > 0)
 hipError_t launch_relu_mask(float* dy, int ldd, const float* y, int ldy, int C, long long P, hipStream_t s);

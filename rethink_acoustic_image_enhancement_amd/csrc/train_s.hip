@@ -127,19 +127,24 @@ __global__ __launch_bounds__(kThreads) void wperm_kernel(const float* __restrict
 }
 
 // Fragment-order weights (gemm.hip's packed layout: record (t, g) = [64 lanes][4], lane (li, lq)
-// holding output channel 16t + li, k = 16g + 4lq + e) of the input-gradient conv
-//   dX[q][c] = sum_{tap, o} dZ[q + off(tap)][o] Wd[c][tap * cout_pad + o],  Wd = W[o][c][26 - tap]
-// (the transposed conv is the forward conv of dZ with the taps flipped and the channel roles swapped).
-__global__ __launch_bounds__(kThreads) void pack_dx_kernel(const float* __restrict__ w, int cout, int cin,
-                                                           int cout_pad, int ntiles, int kgroups,
-                                                           float* __restrict__ wp) {
+// holding output channel 16t + li, k = 16g + 4lq + e) of a Conv3d 3x3x3 weight W [cout][cin][27] for the
+// inference conv kernels (conv3d_c16 / conv_lds), k = tap * in_pad + c:
+//   dx = 0: the forward conv, out channel o, in channel c:  W[o][c][tap]
+//   dx = 1: the input-gradient conv dX[q][c] = sum_{tap, o} dZ[q + off(tap)][o] W[o][c][26 - tap]
+//           (the transposed conv is the forward conv of dZ with the taps flipped, channel roles swapped)
+__global__ __launch_bounds__(kThreads) void pack_conv_kernel(const float* __restrict__ w, int cout, int cin, int dx,
+                                                             int nout, int nin, int in_pad, int ntiles, int kgroups,
+                                                             float* __restrict__ wp) {
   const int n_all = ntiles * kgroups * 256;
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < n_all; i += gridDim.x * kThreads) {
     const int t = i / (kgroups * 256), r = i - t * kgroups * 256;
     const int g = r >> 8, lane = (r >> 2) & 63, e = r & 3;
     const int n = 16 * t + (lane & 15), k = 16 * g + 4 * (lane >> 4) + e;
-    const int tap = k / cout_pad, o = k - tap * cout_pad;
-    wp[i] = (n < cin && o < cout && tap < 27) ? w[((long long)o * cin + n) * 27 + (26 - tap)] : 0.f;
+    const int tap = k / in_pad, ci = k - tap * in_pad;
+    float v = 0.f;
+    if (n < nout && ci < nin && tap < 27)
+      v = dx ? w[((long long)ci * cin + n) * 27 + (26 - tap)] : w[((long long)n * cin + ci) * 27 + tap];
+    wp[i] = v;
   }
 }
 
@@ -313,10 +318,11 @@ hipError_t launch_wperm(const float* src, float* dst, int O, int C, int dir, hip
   return hipGetLastError();
 }
 
-hipError_t launch_pack_dx(const float* w, int cout, int cin, float* wp, hipStream_t s) {
-  const int cout_pad = (cout + 15) / 16 * 16, ntiles = (cin + 15) / 16, kgroups = 27 * cout_pad / 16;
-  hipLaunchKernelGGL(pack_dx_kernel, dim3(grid_for((long long)ntiles * kgroups * 256)), dim3(kThreads), 0, s, w, cout,
-                     cin, cout_pad, ntiles, kgroups, wp);
+hipError_t launch_pack_conv(const float* w, int cout, int cin, int dx, float* wp, hipStream_t s) {
+  const int nout = dx ? cin : cout, nin = dx ? cout : cin;
+  const int in_pad = (nin + 15) / 16 * 16, ntiles = (nout + 15) / 16, kgroups = 27 * in_pad / 16;
+  hipLaunchKernelGGL(pack_conv_kernel, dim3(grid_for((long long)ntiles * kgroups * 256)), dim3(kThreads), 0, s, w,
+                     cout, cin, dx, nout, nin, in_pad, ntiles, kgroups, wp);
   return hipGetLastError();
 }
 
