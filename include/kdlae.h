@@ -350,7 +350,8 @@ int kdlae_train_l1frames(const float* pred, const float* target, int N, int fram
  *   operand offset by z1 * b?1 + z2 * b?2 (floats); amode 1 = implicit 3x3 im2col of the NHWC view A
  *   (pixel stride lda, k = tap * Cg + c, dilation dil, zero padding), bmode 1 = the NHWC view B shifted
  *   by tap z2 (conv weight gradient), bmode 2 / 3 = a 3x3 OIHW weight as the forward / transposed
- *   conv operand (see train_kernels.h TGemm).  route: 0 = the engine's own dispatch, 1 = the
+ *   conv operand, bmode 4 = implicit 3x3x3 im2col of the NDHWC view B, n = tap * Cg + c (Conv3d weight
+ *   gradient; pixel-reduction kernel) (see train_kernels.h TGemm).  route: 0 = the engine's own dispatch, 1 = the
  *   row-streaming kernel, 2 = the pixel-reduction kernel (needs partial), 3 = the tiled kernels. */
 typedef struct kdlae_debug_tgemm_desc {
   const float* A; int64_t sam, sak; int amode;
@@ -366,6 +367,7 @@ typedef struct kdlae_debug_tgemm_desc {
   float* partial; int64_t partial_floats;
   int route;
   int c_pad_ok;
+  int F;  /* frames of the bmode 4 (implicit 3x3x3) B view; 0 = 1 */
 } kdlae_debug_tgemm_desc;
 int kdlae_debug_tgemm(const kdlae_debug_tgemm_desc* d, void* stream);
 

@@ -29,6 +29,7 @@ extern "C" int kdlae_debug_tgemm(const kdlae_debug_tgemm_desc* d, void* stream) 
   g.Bn = d->Bn; g.H = d->H; g.W = d->W; g.Cg = d->Cg; g.dil = d->dil; g.lda = d->lda; g.ldb = d->ldb;
   g.partial = d->partial;
   g.c_pad_ok = d->c_pad_ok != 0;
+  g.F = d->F > 0 ? d->F : 1;
   const size_t cap = d->partial ? (size_t)d->partial_floats : 0;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;

@@ -246,10 +246,15 @@ hipError_t launch_tgemm_cols(TGemm g, size_t partial_cap, hipStream_t s) {
   const int wtiles = a.wtm * a.wtn;
   const int gy = (wtiles + 3) / 4;
   const long long batch = (long long)g.nz1 * g.nz2;
+  // (bmode 4: N = 27 Cg is 27 * whole 16-tiles, so TN is 3 or 4, or 2 beside TM = 4; no other
+  // implicit instance is compiled)
 #define TT(m, n)                                                                                     \
-  if (TM == m && TN == n)                                                                            \
-    return g.bmode == 4 ? launch_tt<m, n, true>(g, a, gy, batch, partial_cap, s)                      \
-                        : launch_tt<m, n, false>(g, a, gy, batch, partial_cap, s);
+  if (TM == m && TN == n) {                                                                          \
+    if constexpr (n != 2 || m == 4)                                                                  \
+      if (g.bmode == 4) return launch_tt<m, n, true>(g, a, gy, batch, partial_cap, s);                \
+    if (g.bmode == 4) return hipErrorInvalidValue;                                                    \
+    return launch_tt<m, n, false>(g, a, gy, batch, partial_cap, s);                                   \
+  }
   TT(2, 2) TT(2, 3) TT(2, 4) TT(3, 2) TT(3, 3) TT(3, 4) TT(4, 2) TT(4, 3)
 #undef TT
   return hipErrorInvalidValue;

@@ -40,7 +40,7 @@ class TGemmDesc(ctypes.Structure):
                 ("Bn", c_int), ("H", c_int), ("W", c_int), ("Cg", c_int), ("dil", c_int),
                 ("lda", c_int64), ("ldb", c_int64),
                 ("partial", c_void_p), ("partial_floats", c_int64),
-                ("route", c_int), ("c_pad_ok", c_int)]
+                ("route", c_int), ("c_pad_ok", c_int), ("F", c_int)]
 
 
 def _ptr(t, off=0):
@@ -138,6 +138,31 @@ def test_cols_kernel_variant(tm, tn):
         a = dY[:, :, h * Ch_m:(h + 1) * Ch_m].double()
         b = X[:, :, h * Ch_n:(h + 1) * Ch_n].double()
         _close(C[:, h], torch.einsum("zpm,zpn->zmn", a, b), P)
+
+
+# (cout, cin) -> the implicit instances the dispatch can pick: TM = 2 / 3 / 4, TN = 3 (cin 16) or 4 (cin 64; 2 beside TM 4)
+COLS3D = [(16, 16), (48, 16), (64, 16), (32, 64), (48, 64), (64, 64)]
+
+
+@pytest.mark.parametrize("cout,cin", COLS3D)
+def test_cols_kernel_implicit_conv3d(cout, cin):
+    """Conv3d 3x3x3 weight gradient with the implicit-im2col B (bmode 4): dW'[o][tap * cin + c] =
+    sum_p dZ[p][o] X[p + off(tap)][c] with zero padding, against float64 unfold (B 2, F 3, 16 x 32, a
+    pixel stride wider than cin)."""
+    B_, F_, H_, W_ = 2, 3, 16, 32
+    P, ldx, ldz = B_ * F_ * H_ * W_, cin + 4, cout
+    X = _rand(B_, F_, H_, W_, ldx, seed=cin)
+    dZ = _rand(P, ldz, seed=cout + 7)
+    C = torch.zeros(cout, 27 * cin, device=DEV)
+    part = torch.empty(8 << 20, device=DEV)
+    _run(A=_ptr(dZ), sam=1, sak=ldz, B=_ptr(X), sbk=ldx, sbn=1, bmode=4, C=_ptr(C), scm=27 * cin, scn=1,
+         M=cout, N=27 * cin, K=P, Bn=B_, F=F_, H=H_, W=W_, Cg=cin, partial=_ptr(part),
+         partial_floats=part.numel(), route=2)
+    xp = torch.nn.functional.pad(X[..., :cin].double().cpu(), (0, 0, 1, 1, 1, 1, 1, 1))  # pad W, H, F
+    cols = torch.stack([xp[:, dt:dt + F_, dy:dy + H_, dx:dx + W_, :]
+                        for dt in range(3) for dy in range(3) for dx in range(3)], dim=4)  # [B,F,H,W,27,cin]
+    ref = dZ.double().cpu().t() @ cols.reshape(P, 27 * cin)
+    _close(C, ref.to(DEV), P)
 
 
 # ---------------------------------------------------------------------------------------------- tiled
