@@ -31,6 +31,12 @@
  * KDLAE_PROBE_DUMP.  It does not change results, but the synchronisation
  * removes the overlap of the bucketed all-reduce with the backward that the
  * gradient-ready marks exist for: diagnostics only, never in production.
+ * "train_serial" (read by kdlae_tt_backward / kdlae_tt_backward_marked) keeps
+ * every backward launch on the caller's stream; by default the weight-gradient
+ * GEMMs and bias column sums run on a library-owned non-blocking side stream
+ * that is forked from and joined back into the caller's stream inside the call
+ * (every gradient-ready mark and the call's end follow a join), with the same
+ * results either way.
  */
 #ifndef KDLAE_H_
 #define KDLAE_H_

@@ -41,6 +41,15 @@ struct kdlae_st_handle {
   int B = 0, F = 0, H = 0, W = 0;
   const void* ws = nullptr;
   const float* x = nullptr;
+  // backward side stream (non-blocking) for the Conv3d weight / bias gradients, and its fork / join
+  // events (KDLAE_DEBUG=train_serial: everything on the caller's stream)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  ~kdlae_st_handle() {
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
+  }
 };
 
 namespace {
@@ -155,6 +164,8 @@ struct Ctx {
   SPlanT pl;
   hipStream_t s;
   int B, F, H, W;
+  hipStream_t side = nullptr;    // set by the backward unless KDLAE_DEBUG=train_serial
+  hipStream_t main_s = nullptr;  // the caller's stream (c.s is the side stream inside a side segment)
   float* buf(size_t o) const { return reinterpret_cast<float*>(ws + o); }
   const float* P(const std::string& k) const { return th + h->off.at(k); }
   float* G(const std::string& k) const { return gr + h->off.at(k); }
@@ -228,12 +239,32 @@ int conv_fwd(Ctx& c, const std::string& p, const float* X, int cin, float* Y, in
   return KDLAE_OK;
 }
 
-// dY (grad of the ReLU output Y) -> weight / bias gradients and, when dX != null, the input gradient
-int conv_bwd(Ctx& c, const std::string& p, const float* X, int cin, const float* Y, float* dY, int cout, int lvl,
-             float* dX) {
+// the side stream waits for the main stream's current point; launches then go to the side stream
+int side_fork(Ctx& c, hipStream_t main_s) {
+  if (!c.side) return KDLAE_OK;
+  HIPCHK(hipEventRecord(c.h->ev_fork, main_s));
+  HIPCHK(hipStreamWaitEvent(c.side, c.h->ev_fork, 0));
+  c.s = c.side;
+  return KDLAE_OK;
+}
+// back to the main stream, which waits for the side stream's launches
+int side_join(Ctx& c, hipStream_t main_s) {
+  c.s = main_s;
+  if (!c.side) return KDLAE_OK;
+  HIPCHK(hipEventRecord(c.h->ev_join, c.side));
+  HIPCHK(hipStreamWaitEvent(main_s, c.h->ev_join, 0));
+  return KDLAE_OK;
+}
+
+// dY (grad of the ReLU output Y) -> weight / bias gradients and, when dX != null, the input gradient.
+// The weight / bias gradients (which use the partial buffers, dwp and the gradient keys) run on the
+// side stream beside the input gradient (which uses wpk / wp / col only); conv_bwd joins before returning.
+int conv_bwd_body(Ctx& c, const std::string& p, const float* X, int cin, const float* Y, float* dY, int cout,
+                  int lvl, float* dX) {
   const int Hl = c.H >> lvl, Wl = c.W >> lvl;
   const long long P = (long long)c.B * c.F * Hl * Wl;
   HIPCHK(tr::launch_relu_mask(dY, cout, Y, cout, cout, P, c.s));
+  TRY(side_fork(c, c.main_s));
   TRY(colsum(c, dY, cout, cout, P, c.G(p + ".bias")));
   float* col = c.buf(c.pl.col);
   float* wp = c.buf(c.pl.wp);
@@ -252,6 +283,7 @@ int conv_bwd(Ctx& c, const std::string& p, const float* X, int cin, const float*
     TRY(gemm(c, g, true));
   }
   HIPCHK(tr::launch_wperm(dwp, c.G(p + ".weight"), cout, cin, 1, c.s));
+  c.s = c.main_s;
   if (!dX) return KDLAE_OK;
   // dX = the forward conv of dZ with flipped taps (cout -> cin channels) on the inference kernels:
   // conv3d_c16 for 16 -> 16, conv_lds for 2..16 output tiles; no column matrix, no col2im
@@ -287,6 +319,13 @@ int conv_bwd(Ctx& c, const std::string& p, const float* X, int cin, const float*
   TRY(gemm(c, d, false));
   HIPCHK(tr::launch_col2im3d(col, cin, c.B, c.F, Hl, Wl, dX, cin, 0, c.s));
   return KDLAE_OK;
+}
+
+int conv_bwd(Ctx& c, const std::string& p, const float* X, int cin, const float* Y, float* dY, int cout, int lvl,
+             float* dX) {
+  const int r = conv_bwd_body(c, p, X, cin, Y, dY, cout, lvl, dX);
+  const int j = side_join(c, c.main_s);  // also on an error path: no side launch left unjoined
+  return r ? r : j;
 }
 
 int net_fwd(Ctx& c, const float* x, float* out) {
@@ -520,6 +559,15 @@ int kdlae_st_backward(kdlae_st_handle* h, const float* theta, const float* dout,
         (hipStream_t)stream, h->B, h->F, h->H, h->W};
   if ((int64_t)c.pl.total > workspace_bytes) return fail(KDLAE_ESTATE, "training workspace too small");
   DeviceGuard dg(h->device);
+  c.main_s = c.s;
+  if (!debug_flag("train_serial")) {
+    if (!h->side) {
+      HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+    }
+    c.side = h->side;
+  }
   HIPCHK(hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), c.s));  // the pad floats stay zero
   HIPCHK(hipMemsetAsync(c.buf(c.pl.zb), 0, 64 * sizeof(float), c.s));
   return net_bwd(c, h->x, dout);

@@ -82,8 +82,15 @@ struct kdlae_tt_handle {
     hipEvent_t a, b;
   };
   std::vector<TraceRec> trace;
+  // backward side stream (non-blocking) and its fork / join events: the weight-gradient GEMMs and
+  // bias column sums run there, beside the input-gradient chain on the caller's stream
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   ~kdlae_tt_handle() {
     for (hipEvent_t e : mark_ev) (void)hipEventDestroy(e);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
   }
 };
 
@@ -183,9 +190,20 @@ struct Ctx {
   char* base = nullptr;
   size_t off = 0, cap = 0, peak = 0;
   bool dry = true;
-  hipStream_t s = nullptr;
-  float* splitk = nullptr;
+  hipStream_t s = nullptr;  // the stream launches go to: main_s, or side_s inside a side segment
+  float* splitk = nullptr;   // split-K partials of the current stream (splitk_main / splitk_side)
   float* red = nullptr;
+  // backward side stream (kdlae_tt_backward*): a side segment (side_begin .. side_end) holds
+  // launches that only READ buffers the main stream does not write until the next join.  Every
+  // segment starts with a fork (the side stream waits for the main stream's current point), so side
+  // work is ordered after all earlier main work, including reduction flushes; the main stream waits
+  // for the side stream (join) at every flush, mark and block end, before a write to a buffer a
+  // pending side launch reads, and before scratch is released.  side_s == nullptr: one stream.
+  hipStream_t main_s = nullptr, side_s = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  float* splitk_main = nullptr;
+  float* splitk_side = nullptr;
+  bool in_side = false, side_pending = false;
   // gradient-ready marks (kdlae_tt_backward_marked): the dry run records, per key offset, the first
   // and last mark index at which its gradient was written; the real run records an event per mark
   std::map<int64_t, std::pair<int, int>>* touch = nullptr;
@@ -226,6 +244,43 @@ struct Ctx {
 
 int flush_reduce(Ctx& c);
 
+int hip_fail(hipError_t e, const char* what) {
+  return fail(KDLAE_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// enter a side segment: the side stream waits for everything enqueued on the main stream so far
+int side_begin(Ctx& c) {
+  if (c.in_side) return KDLAE_OK;
+  c.splitk = c.splitk_side;
+  c.in_side = true;
+  if (c.dry || !c.side_s) {
+    c.splitk = c.splitk_main;  // one stream: the main stream's partials
+    return KDLAE_OK;
+  }
+  hipError_t e = hipEventRecord(c.ev_fork, c.main_s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(c.side_s, c.ev_fork, 0);
+  if (e != hipSuccess) return hip_fail(e, "side stream fork");
+  c.s = c.side_s;
+  c.side_pending = true;
+  return KDLAE_OK;
+}
+
+void side_end(Ctx& c) {
+  c.in_side = false;
+  c.s = c.main_s;
+  c.splitk = c.splitk_main;
+}
+
+// the main stream waits for every side launch enqueued so far
+int join(Ctx& c) {
+  if (c.in_side) side_end(c);
+  if (!c.side_pending) return KDLAE_OK;
+  c.side_pending = false;
+  hipError_t e = hipEventRecord(c.ev_join, c.side_s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(c.main_s, c.ev_join, 0);
+  return e == hipSuccess ? KDLAE_OK : hip_fail(e, "side stream join");
+}
+
 // a region of the reduction buffer for a queued reduction's partials (flushes when full)
 // Returns nullptr with c.red_err set (and the message in kdlae_last_error) when the flush fails
 // (a HIP error) or when one request alone exceeds the buffer (a sizing bug: KDLAE_ESTATE).
@@ -253,7 +308,7 @@ float* red_take(Ctx& c, size_t n) {
 // one head conv, ...).  kdlae_tt_backward_marked records an event at the marks that close a suffix
 // of the flat buffer, so the caller can all-reduce that suffix while the backward continues.
 int mark(Ctx& c) {
-  int rc = flush_reduce(c);  // the gradients this mark declares final
+  int rc = flush_reduce(c);  // the gradients this mark declares final (joins the side stream)
   if (rc) return rc;
   if (c.record_marks && !c.dry && c.cur_mark < (int)c.h->mark_slot.size()) {
     const int j = c.h->mark_slot[c.cur_mark];
@@ -300,10 +355,15 @@ void trace_end(Ctx& c, hipEvent_t a, const char* what) {
 
 inline int ld4(int n) { return (n + 3) / 4 * 4; }
 
+// on the main stream after a join (queued partials may come from either stream); inside a side
+// segment the segment is re-entered afterwards, so later side writes to `red` follow the flush
 int flush_reduce(Ctx& c) {
+  const bool was_side = c.in_side;
+  TRY(join(c));
   if (!c.pend.empty()) LAUNCH(tr::launch_part_reduce_multi(c.pend.data(), (int)c.pend.size(), c.s));
   c.pend.clear();
   c.red_off = 0;
+  if (was_side) TRY(side_begin(c));
   return KDLAE_OK;
 }
 
@@ -400,9 +460,11 @@ int conv1_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, long l
   g.B = x.p; g.sbk = x.ld; g.sbn = 1;
   g.C = c.G(n + ".weight"); g.scm = Cin; g.scn = 1;
   g.M = Cout; g.N = Cin; g.K = (int)P;
+  TRY(side_begin(c));  // dW and db only read x and dy
   g.partial = c.splitk;
   TRY(gemm(c, g, kSplitCap, n + " dW"));
   TRY(bias_grad(c, dy, Cout, P, c.G(n + ".bias")));
+  side_end(c);
   if (dx.p) {
     tr::TGemm d;
     d.A = dy.p; d.sam = dy.ld; d.sak = 1;
@@ -499,6 +561,7 @@ int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn
               const float* R = nullptr, int ldr = 0) {
   const long long P = (long long)Bn * H * W;
   float* gw = c.G(n + ".weight");
+  TRY(side_begin(c));  // dW and db only read x and dy (dx may alias R, never x or dy)
   if (tr::dw3_small_ok(Cin, Cout) && gw) {
     // narrow side: per-block [Cout][Cin][9] partials on the VALU (train_small.hip)
     const int ncols = Cin * Cout * 9;
@@ -519,6 +582,7 @@ int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn
     TRY(gemm(c, g, kSplitCap, n + " dW3"));
   }
   TRY(bias_grad(c, dy, Cout, P, c.G(n + ".bias")));
+  side_end(c);
   if (dx.p) {
     // the transposed conv: Cout -> Cin channels (flipped taps), narrow-side kernels where they apply
     int done = 0;
@@ -718,8 +782,9 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   }
   float* dxn1 = c.alloc(P * C);
   TRY(conv1_bwd(c, p + ".attn.qkv", {r.xn1, C}, {dqkv, C3}, C, C3, P, {dxn1, C}));
+  TRY(join(c));  // ln_bwd overwrites d, which the project_out weight gradient reads
   TRY(ln_bwd(c, dxn1, r.x, r.st1, C, P, p + ".norm1.body", dx1, d));
-  TRY(flush_reduce(c));  // before the block's scratch (dtp) is released
+  TRY(flush_reduce(c));  // before the block's scratch (dtp) is released (joins the side stream)
   c.off = mark;
   return KDLAE_OK;
 }
@@ -966,9 +1031,27 @@ void ctx_init(Ctx& c, const kdlae_tt_handle* h, void* ws, size_t ws_bytes, bool 
   c.base = dry ? nullptr : static_cast<char*>(ws);
   c.cap = ws_bytes;
   c.off = 0;
-  c.splitk = c.alloc(kSplitCap);
+  c.main_s = s;
+  c.splitk_main = c.splitk = c.alloc(kSplitCap);
+  c.splitk_side = c.alloc(kSplitCap);
   c.red_cap = red_floats(h->cfg, B, H, W);
   c.red = c.alloc(c.red_cap);
+}
+
+// the backward's side stream (created once per handle, on its device); KDLAE_DEBUG=train_serial
+// keeps every launch on the caller's stream (A/B and diagnostics: same results either way)
+int use_side_stream(Ctx& c, kdlae_tt_handle* h) {
+  if (kdlae::debug_flag("train_serial")) return KDLAE_OK;
+  if (!h->side) {
+    hipError_t e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(e, "backward side stream");
+  }
+  c.side_s = h->side;
+  c.ev_fork = h->ev_fork;
+  c.ev_join = h->ev_join;
+  return KDLAE_OK;
 }
 
 // KDLAE_DEBUG=train_trace: wait for the call's launches and append "phase,layer,kernel,ms" rows to
@@ -1097,10 +1180,13 @@ int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, 
   c.gr = grad;
   c.off = h->sv.fwd_end;
   if (kdlae::debug_flag("train_trace")) c.trace = &h->trace;
+  int rc = use_side_stream(c, h);
+  if (rc) return rc;
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
-  int rc = net_bwd(c, dhq, dsr, has_dsr);
+  rc = net_bwd(c, dhq, dsr, has_dsr);
   if (rc == KDLAE_OK) rc = flush_reduce(c);
+  if (rc != KDLAE_OK) (void)join(c);  // leave no side launch unjoined, even on an error path
   trace_dump(h, c.s, "bwd");
   return rc;
 }
@@ -1172,10 +1258,13 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
   std::map<int64_t, std::pair<int, int>> written;  // what the real run writes, checked against the marks
   c.touch = &written;
   if (kdlae::debug_flag("train_trace")) c.trace = &h->trace;
+  int rc = use_side_stream(c, h);
+  if (rc) return rc;
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
-  int rc = net_bwd(c, dhq, dsr, has_dsr);
+  rc = net_bwd(c, dhq, dsr, has_dsr);
   if (rc == KDLAE_OK) rc = flush_reduce(c);
+  if (rc != KDLAE_OK) (void)join(c);
   trace_dump(h, c.s, "bwd");
   if (rc) return rc;
   // every gradient the launches wrote must have been written by the dry run the marks came from, at

@@ -12,6 +12,7 @@
 #             per-launch probe of class $PROBE (default 1) and a short T16 bench; CHECK=1 runs
 #             tests/test_kdlae_gpu.py against each variant first
 #   train_ab  like ab for the training step: launch trace (tools/train_trace.py) + training bench
+#   trains_ab the KDLAE-S training bench for each variant
 #   taps      tools/config1_taps.py gpu leg for each "name=path" in $VARIANTS
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -88,6 +89,13 @@ train_ab)
     echo "$n: $(head -1 $O/$n.txt)"
     timeout -k 10 300 python -u bench.py --workload train --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_$n.json 2> $O/bench_$n.err || { tail -20 $O/bench_$n.err; exit 1; }
     echo "$n bench: $(head -c 200 $O/bench_$n.json)"
+  done
+  ;;
+trains_ab)  # KDLAE-S training bench per variant
+  for nv in ${VARIANTS:-default=default}; do
+    use_variant "$nv"; n=$VNAME
+    timeout -k 10 300 python -u bench.py --workload train_s --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_s_$n.json 2> $O/bench_s_$n.err || { tail -20 $O/bench_s_$n.err; exit 1; }
+    echo "$n train_s bench: $(head -c 200 $O/bench_s_$n.json)"
   done
   ;;
 taps)
