@@ -339,6 +339,36 @@ def test_full_size_step_properties():
     assert float((o["sr"] - tr.output["sr"]).abs().max()) <= 1e-3
 
 
+def test_side_stream_backward_equals_serial_backward():
+    """The backward runs its weight-gradient GEMMs and bias column sums on a forked side stream; the
+    gradient must equal, bit for bit, the one-stream backward (KDLAE_DEBUG=train_serial), for both
+    the plain and the marked backward, at the KDLAET.yml patch setting where the two streams overlap."""
+    m = _model(dict(LayerNorm_type="BiasFree"))
+    B, H, W = 6, 128, 128
+    img = torch.from_numpy(hash_images("img:side", (B, 3, H, W))).to(DEV)
+    rate = torch.full((B, 1, H, W), 0.6, device=DEV)
+    gt = {"hq": img.clamp(0.2, 0.8), "sr": torch.nn.functional.interpolate(img, scale_factor=2).clamp(0.2, 0.8)}
+    tr = KDLAETrainer(m)
+    inp = {"img": img, "denoise_rate": rate}
+    old = os.environ.get("KDLAE_DEBUG")
+    try:
+        os.environ["KDLAE_DEBUG"] = "train_serial"
+        tr.forward_backward(inp, gt)
+        torch.cuda.synchronize()
+        g_serial = tr.grad.clone()
+        os.environ.pop("KDLAE_DEBUG")
+        for marked in (False, True, False):
+            tr.grad.fill_(float("nan"))
+            tr.forward_backward(inp, gt, marked=marked)
+            torch.cuda.synchronize()
+            assert torch.equal(g_serial, tr.grad), f"side-stream backward (marked={marked}) differs"
+    finally:
+        if old is None:
+            os.environ.pop("KDLAE_DEBUG", None)
+        else:
+            os.environ["KDLAE_DEBUG"] = old
+
+
 def test_engine_rejects_bad_shapes():
     m = _model(dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1))
     eng = TrainEngine(m, torch.device(DEV))

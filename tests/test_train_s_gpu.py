@@ -119,6 +119,34 @@ def test_backward_is_deterministic():
     assert torch.equal(grads[0], grads[1])
 
 
+def test_side_stream_backward_equals_serial_backward():
+    """Conv3d weight / bias gradients run on a forked side stream beside the input gradient; the result
+    must equal the one-stream backward (KDLAE_DEBUG=train_serial) bit for bit, at the KDLAES.yml batch
+    shape (4 x 7 x 128^2) where the streams overlap."""
+    m = _model(dict(residual=True, hidden_channels=[16, 32, 64]))
+    x = torch.from_numpy(hash_images("side_s_x", (4, 7, 128, 128))).to(DEV)
+    tgt = torch.from_numpy(hash_images("side_s_t", (4, 7, 128, 128))).to(DEV)
+    old = os.environ.get("KDLAE_DEBUG")
+    grads = []
+    try:
+        for flag in ("train_serial", None, None):
+            if flag:
+                os.environ["KDLAE_DEBUG"] = flag
+            else:
+                os.environ.pop("KDLAE_DEBUG", None)
+            m.zero_grad()
+            L1LossForVideoFrames()(m(x), tgt).backward()
+            torch.cuda.synchronize()
+            grads.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone())
+    finally:
+        if old is None:
+            os.environ.pop("KDLAE_DEBUG", None)
+        else:
+            os.environ["KDLAE_DEBUG"] = old
+    assert torch.isfinite(grads[0]).all()
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+
+
 def test_unsupported_reduction_raises():
     with pytest.raises(NotImplementedError):
         L1LossForVideoFrames(reduction="max")(torch.zeros(1, 2, 4, 4, device=DEV), torch.zeros(1, 2, 4, 4, device=DEV))
