@@ -139,6 +139,58 @@ __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t r, f32x4* lds_wav
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)lds_wave_base, 16, (int)voff, soff, 0, 0);
 }
 
+// gate of one 16-hidden-channel chunk for RPW tile rows (the GDFN stencil): depthwise 3x3 of x1 and x2
+// (rows of the wave, column cx, channels 4q..4q+3 of each half) + exact-erf gate -> the float4 that IS
+// the lane's MFMA B operand.  sl: the chunk's halo image (lane-linear [pixel][slot], slot = quad ^
+// (column & 7), kHalo columns per row); dw: the chunk's dw block ([9][8] weights, [8] bias at +72);
+// lo[h][j]: the lane's read offset of half h, column tap j in the wave's first halo row.  Shared by
+// gdfn_out_kernel and ffn48_kernel, so the two compute the same bits.
+// LOWREG: a scheduling fence between the column taps, so at most one tap's halo reads are in flight
+// (for callers with little register room left; the values are the same)
+template <int RPW, bool PACKED, bool LOWREG = false>
+__device__ __forceinline__ void gate_rows(const f32x4* sl, const f32x4* dw, const int (&lo)[2][3], int q,
+                                          f32x4 (&gb)[RPW]) {
+  f32x4 d[2][RPW];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x4 bb = dw[72 + 4 * h + q];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) d[h][r] = bb;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      f32x4 wv[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) wv[i] = dw[(3 * i + j) * 8 + 4 * h + q];
+#pragma unroll
+      for (int rr = 0; rr < RPW + 2; ++rr) {
+        const f32x4 v = (sl + lo[h][j])[rr * kHalo * 8];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int r = rr - i;
+          if (r >= 0 && r < RPW) d[h][r] = v * wv[i] + d[h][r];
+        }
+      }
+      if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    if constexpr (PACKED) {
+      const f32x2 lo2 = gelu_gate2(f32x2{d[0][r].x, d[0][r].y}, f32x2{d[1][r].x, d[1][r].y});
+      const f32x2 hi2 = gelu_gate2(f32x2{d[0][r].z, d[0][r].w}, f32x2{d[1][r].z, d[1][r].w});
+      gb[r] = f32x4{lo2.x, lo2.y, hi2.x, hi2.y};
+    } else {
+      gb[r].x = gelu_erf_g(d[0][r].x) * d[1][r].x;
+      gb[r].y = gelu_erf_g(d[0][r].y) * d[1][r].y;
+      gb[r].z = gelu_erf_g(d[0][r].z) * d[1][r].z;
+      gb[r].w = gelu_erf_g(d[0][r].w) * d[1][r].w;
+    }
+  }
+}
+
 }  // namespace
 
 // W2: the project_out W fragments travel one chunk ahead of their MFMAs in a 2-slot ring of their
@@ -282,45 +334,7 @@ __global__ __launch_bounds__(64 * WAVES, W2 ? 2 : 1) void gdfn_out_kernel(GdfnPa
   // gate(g): depthwise 3x3 (rows 4w..4w+3, column cx, channels 16g+4q..+3 of x1 and x2) + gate
   auto gate = [&](int g, f32x4 (&gb)[RPW]) {
     const f32x4* sl = lds + (g % kNStage) * kStageSlot;
-    const f32x4* dw = sl + kStageF4;               // [9][8] then bias [8]
-    f32x4 d[2][RPW];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4 bb = dw[72 + 4 * h + q];
-#pragma unroll
-      for (int r = 0; r < RPW; ++r) d[h][r] = bb;
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        f32x4 wv[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) wv[i] = dw[(3 * i + j) * 8 + 4 * h + q];
-#pragma unroll
-        for (int rr = 0; rr < RPW + 2; ++rr) {
-          const f32x4 v = (sl + lo[h][j])[rr * kHalo * 8];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const int r = rr - i;
-            if (r >= 0 && r < RPW) d[h][r] = v * wv[i] + d[h][r];
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      if constexpr (kGeluPacked && NT <= 6) {
-        const f32x2 lo = gelu_gate2(f32x2{d[0][r].x, d[0][r].y}, f32x2{d[1][r].x, d[1][r].y});
-        const f32x2 hi = gelu_gate2(f32x2{d[0][r].z, d[0][r].w}, f32x2{d[1][r].z, d[1][r].w});
-        gb[r] = f32x4{lo.x, lo.y, hi.x, hi.y};
-      } else {
-        gb[r].x = gelu_erf_g(d[0][r].x) * d[1][r].x;
-        gb[r].y = gelu_erf_g(d[0][r].y) * d[1][r].y;
-        gb[r].z = gelu_erf_g(d[0][r].z) * d[1][r].z;
-        gb[r].w = gelu_erf_g(d[0][r].w) * d[1][r].w;
-      }
-    }
+    gate_rows<RPW, kGeluPacked && NT <= 6>(sl, sl + kStageF4, lo, q, gb);  // [9][8] then bias [8]
   };
   auto mfma_chunk = [&](int g, const f32x4 (&gb)[RPW]) {
     const f32x4* wl = wring + (g % kNW) * (64 * NT);
@@ -485,5 +499,312 @@ static hipError_t launch_gdfn_out_small(const GdfnParams& p, int C, hipStream_t 
   // C48@1024^2 5.68 -> 5.42 ms, @512^2 1.46 -> 1.42 ms (profiles/r02_gdfn_c48_tile12_probe.txt).
   return launch_gdfn1<3, 4, 12, 2>(p, s);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Fused C = 48 FFN (r04, KDLAE_model.py:140-144, :160-161, :101-106): one kernel from the attention's
+// v and the block input x to the block output, replacing gemm_attn_in_kernel<8,3,2> (x1 = x + M v,
+// LN, project_in -> 2 hid-wide rows in HBM) + gdfn_out_kernel<3,4,12,2> (those rows back with a halo,
+// dwconv + gate + project_out + residual).  The C = 48 blocks run at 512^2 and 1024^2 and were
+// HBM-bound: 3008 B of traffic per pixel for the pair, ~600 B here.  The price is project_in (and
+// M v, LN) recomputed on the tile's halo ring: 252 halo pixels per 192 outputs.
+//  * block = 4 waves (one per SIMD, up to 512 VGPRs each: the LN'd halo rows, both accumulator sets
+//    and the gate fit without spills; 8-wave 16 x 24 tiles at 256 VGPRs spilled ~180), a 16 x 12 pixel
+//    tile (wave w owns tile rows 3w..3w+2, as gdfn_out's lanes do), persistent over the tiles of its
+//    XCD; all weights (project_in 48 KiB, project_out 24 KiB, dw 16 KiB, biases) resident in LDS, M
+//    restaged when the image changes;
+//  * phase A: the 18 x 14 halo = 14 row tiles of 16 pixels + 2 column tiles; wave w takes halo rows
+//    3w+1..3w+3 (its output rows: x1 is parked in `out` as the residual) and one of the 4 remaining
+//    tiles.  x1 = (M v + bias_m) + x, LayerNorm, in registers (lane: pixel, channel quad);
+//  * per 16-channel hidden chunk g: project_in of tiles 2g, 2g+1 (x1 and x2 halves) for the wave's
+//    halo pixels -> the chunk's halo image in LDS (gdfn_out's layout; out-of-image pixels 0), barrier,
+//    gate_rows (the gdfn_out stencil) -> project_out MFMAs; project_in of chunk g+1 is issued beside
+//    the gate of chunk g.
+//  Every value is computed by the same operation sequence as the kernel pair (same fragments, same
+//  MFMA k order per accumulator, the same LN and gate code), so the output is bit-identical.
+namespace {
+constexpr int kF48RPW = 3, kF48Waves = 4, kF48TH = kF48RPW * kF48Waves;  // 12 tile rows
+constexpr int kF48HR = kF48TH + 2;                                     // 14 halo rows
+constexpr int kF48Px = kF48HR * kHalo;                                 // 252 halo pixels
+constexpr int kF48Kch = 8;                                             // hidden chunks (hidS = 128)
+constexpr int kF48Tin = 2 * kF48Kch;                                   // project_in output tiles
+// LDS carve, f32x4 units
+constexpr int kF48Hb = 0;                                // [468 px][8 slots] chunk halo image
+constexpr int kF48Win = kF48Hb + kF48Px * 8;             // [16 tiles][3 k-groups][64]
+constexpr int kF48Wout = kF48Win + kF48Tin * 3 * 64;     // [3 tiles][8 chunks][64]
+constexpr int kF48Dw = kF48Wout + 3 * kF48Kch * 64;      // [8 chunks][128]
+constexpr int kF48M = kF48Dw + kF48Kch * kDwF4;          // [3][3][64] folded projection of the image
+constexpr int kF48Bm = kF48M + 9 * 64;                   // [12] bias_m
+constexpr int kF48Bin = kF48Bm + 12;                     // [64] bias_in
+constexpr int kF48Bout = kF48Bin + kF48Tin * 4;          // [12] bias_out
+constexpr int kF48Lds = (kF48Bout + 12) * 16;            // 132,992 bytes: one block per CU
+static_assert(kF48Lds <= 160 * 1024, "ffn48 LDS");
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+}  // namespace
+
+__global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lq = lane >> 4;
+  const int tx_n = p.W / kTile, ty_n = (p.H + kF48TH - 1) / kF48TH;
+  const int per_img = tx_n * ty_n;
+  const int ntiles = p.Bn * per_img;
+  const long long HW = (long long)p.H * p.W;
+  // persistent and XCD-aware: XCD k (blockIdx & 7) walks logical tiles [k T / 8, (k+1) T / 8), its
+  // blocks interleaved, so tiles that share halo rows run together on one L2
+  const int xcd = (int)(blockIdx.x & 7), nxb = (int)(gridDim.x >> 3), xb = (int)(blockIdx.x >> 3);
+  const int t_lo = (int)((long long)ntiles * xcd / 8), t_hi = (int)((long long)ntiles * (xcd + 1) / 8);
+  if (t_lo + xb >= t_hi) return;
+
+  // resident weights
+  {
+    const f32x4* win = reinterpret_cast<const f32x4*>(p.Win);
+    for (int i = tid; i < kF48Tin * 3 * 64; i += 64 * kF48Waves) lds[kF48Win + i] = win[i];
+    const f32x4* wout = reinterpret_cast<const f32x4*>(p.Wout);
+    for (int i = tid; i < 3 * kF48Kch * 64; i += 64 * kF48Waves) lds[kF48Wout + i] = wout[i];
+    const f32x4* dwg = reinterpret_cast<const f32x4*>(p.dw);
+    for (int i = tid; i < kF48Kch * kDwF4; i += 64 * kF48Waves) lds[kF48Dw + i] = dwg[i];
+    for (int i = tid; i < kF48Tin * 4; i += 64 * kF48Waves)
+      lds[kF48Bin + i] = p.bias_in ? reinterpret_cast<const f32x4*>(p.bias_in)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = tid; i < 12; i += 64 * kF48Waves)
+      lds[kF48Bout + i] = p.bias_out ? reinterpret_cast<const f32x4*>(p.bias_out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float wb = (p.ln == 2) ? 1.f : 0.f;
+  // stencil read offsets (gdfn_out's, for the wave's first halo row)
+  int lo[2][3];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int hx = li + j;
+      lo[h][j] = (kF48RPW * wave * kHalo + hx) * 8 + ((4 * h + lq) ^ (hx & 7));
+    }
+  // phase-A pixel tiles of this wave: pt 0..2 = halo rows 3w+1..3w+3 (the wave's output rows, interior
+  // columns), pt 3 = the top halo row (w 0), the bottom one (w 1), the left (w 2) or right (w 3) halo
+  // column (14 pixels)
+  int hy[4], hx[4];
+  bool tv[4];
+#pragma unroll
+  for (int pt = 0; pt < 3; ++pt) {
+    hy[pt] = kF48RPW * wave + 1 + pt;
+    hx[pt] = li + 1;
+    tv[pt] = true;
+  }
+  hy[3] = wave == 0 ? 0 : wave == 1 ? kF48HR - 1 : li;
+  hx[3] = wave <= 1 ? li + 1 : (wave == 2 ? 0 : kHalo - 1);
+  tv[3] = wave <= 1 || li < kF48HR;
+
+  int staged = -1;
+  for (int t = t_lo + xb; t < t_hi; t += nxb) {
+    const int b = t / per_img;
+    const int rem = t - b * per_img;
+    const int ty = rem / tx_n;
+    const int x0 = (rem - ty * tx_n) * kTile, y0 = ty * kF48TH;
+    if (b != staged) {  // block-uniform
+      __syncthreads();
+      const f32x4* mb = reinterpret_cast<const f32x4*>(p.Wm + (long long)b * p.wm_img_stride);
+      for (int i = tid; i < 9 * 64; i += 64 * kF48Waves) lds[kF48M + i] = mb[i];
+      for (int i = tid; i < 12; i += 64 * kF48Waves)
+        lds[kF48Bm + i] = p.bias_m ? reinterpret_cast<const f32x4*>(p.bias_m)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+      __syncthreads();
+      staged = b;
+    }
+    const unsigned obytes = (unsigned)HW * (unsigned)p.ldo * 4u;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        p.out + (long long)b * HW * p.ldo, 0, (int)obytes, 0x00020000);
+    // ---- phase A: x1 and LN(x1) of the wave's halo pixels (the next tile's rows are loaded while one
+    // is computed).  x1 of the wave's output rows goes to `out` (it is the residual the epilogue adds;
+    // the same lane reads it back), so it holds no registers across the chunk loop.
+    bool in[4];
+    f32x4 xn[4][3];
+    {
+      const f32x4* ml = lds + kF48M;
+      f32x4 va[2][3], xa[2][3];
+      // raw buffer loads through per-image descriptors: 32-bit offsets, zeros past the range (the
+      // offset of an out-of-image pixel), no branches
+      const unsigned vbytes = (unsigned)HW * (unsigned)p.ldv * 4u, xbytes = (unsigned)HW * (unsigned)p.ldx * 4u;
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(p.v + (long long)b * HW * p.ldv), 0, (int)vbytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rxx = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(p.x + (long long)b * HW * p.ldx), 0, (int)xbytes, 0x00020000);
+      auto load = [&](int pt, f32x4 (&vv)[3], f32x4 (&xx3)[3]) {
+        const int yy = y0 - 1 + hy[pt], xx = x0 - 1 + hx[pt];
+        in[pt] = tv[pt] && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+        const unsigned px = (unsigned)(yy * p.W + xx);
+        const unsigned ov = in[pt] ? px * (unsigned)p.ldv * 4u + 16u * lq : kOOB2;
+        const unsigned ox = in[pt] ? px * (unsigned)p.ldx * 4u + 16u * lq : kOOB2;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          vv[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(ov + 64u * g), 0, 0));
+          xx3[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rxx, (int)(ox + 64u * g), 0, 0));
+        }
+      };
+      load(0, va[0], xa[0]);
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) {
+        const int cb = pt & 1;
+        if (pt + 1 < 4) load(pt + 1, va[cb ^ 1], xa[cb ^ 1]);
+        // M v: per accumulator, k-group-major and k-step-minor (gemm_attn_in's mfma_chunk order)
+        f32x4 a1[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          f32x4 wm[3];
+#pragma unroll
+          for (int tt = 0; tt < 3; ++tt) wm[tt] = ml[(tt * 3 + g) * 64 + lane];
+#pragma unroll
+          for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+            for (int tt = 0; tt < 3; ++tt) a1[tt] = mfma4(wm[tt][ss], va[cb][g][ss], a1[tt]);
+        }
+        f32x4 a[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          f32x4 v = a1[g] + lds[kF48Bm + 4 * g + lq];
+          v += xa[cb][g];
+          a[g] = v;
+          // an output row (pt < 3: interior columns; the row may be past the image bottom: in[] = 0)
+          if (pt < 3)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4g, v), ro,
+                                                   (int)((in[pt] ? (unsigned)((y0 + kF48RPW * wave + pt) * p.W + x0 + li) *
+                                                                       (unsigned)p.ldo * 4u + 16u * lq
+                                                                 : kOOB2) + 64u * g), 0, 0);
+        }
+        // LayerNorm over the 48 channels (gemm.hip apply_ln, row in registers)
+        float sm = 0.f;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) sm += (a[g].x + a[g].y) + (a[g].z + a[g].w);
+        sm += __shfl_xor(sm, 16);
+        sm += __shfl_xor(sm, 32);
+        const float mean = sm / 48.0f;
+        float v2 = 0.f;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const f32x4 d = a[g] - mean;
+          const float dd = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+          v2 += dd;
+        }
+        v2 += __shfl_xor(v2, 16);
+        v2 += __shfl_xor(v2, 32);
+        const float rstd = 1.0f / sqrtf(v2 / 48.0f + 1e-5f);
+        const float sh = mean * wb;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) xn[pt][g] = (a[g] - sh) * rstd;
+      }
+    }
+    // ---- project_in of one chunk for the wave's halo pixels (tiles 2c, 2c+1), + bias
+    auto project_in = [&](int c, f32x4 (&o)[4][2]) {
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) o[pt][hh] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const f32x4 w0 = lds[kF48Win + ((2 * c) * 3 + g) * 64 + lane];
+        const f32x4 w1 = lds[kF48Win + ((2 * c + 1) * 3 + g) * 64 + lane];
+#pragma unroll
+        for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+          for (int pt = 0; pt < 4; ++pt) {
+            o[pt][0] = mfma4(w0[ss], xn[pt][g][ss], o[pt][0]);
+            o[pt][1] = mfma4(w1[ss], xn[pt][g][ss], o[pt][1]);
+          }
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const f32x4 bias = lds[kF48Bin + 4 * (2 * c + hh) + lq];
+#pragma unroll
+        for (int pt = 0; pt < 4; ++pt) o[pt][hh] = o[pt][hh] + bias;
+      }
+    };
+    auto store_chunk = [&](const f32x4 (&o)[4][2]) {
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) {
+        if (!tv[pt]) continue;
+        const int base = (hy[pt] * kHalo + hx[pt]) * 8;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+          lds[kF48Hb + base + ((4 * hh + lq) ^ (hx[pt] & 7))] = in[pt] ? o[pt][hh] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    f32x4 acc[kF48RPW][3];
+#pragma unroll
+    for (int r = 0; r < kF48RPW; ++r)
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 pin[4][2];
+    project_in(0, pin);
+    lds_barrier();  // the previous tile's last gate has read the halo image
+    store_chunk(pin);
+    lds_barrier();
+#pragma unroll 1
+    for (int c = 0; c < kF48Kch; ++c) {
+      f32x4 gb[kF48RPW];
+      gate_rows<kF48RPW, kGeluPacked, true>(lds + kF48Hb, lds + kF48Dw + c * kDwF4, lo, lq, gb);
+      __builtin_amdgcn_sched_barrier(0);  // the gate's 30 halo reads and project_in's operands would
+                                          // not fit the 256 VGPRs together (the SIMD's other wave overlaps them)
+      if (c + 1 < kF48Kch) project_in(c + 1, pin);
+      f32x4 w[3];
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) w[tt] = lds[kF48Wout + (tt * kF48Kch + c) * 64 + lane];
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+        for (int r = 0; r < kF48RPW; ++r) {
+          acc[r][tt] = mfma4(w[tt].x, gb[r].x, acc[r][tt]);
+          acc[r][tt] = mfma4(w[tt].y, gb[r].y, acc[r][tt]);
+          acc[r][tt] = mfma4(w[tt].z, gb[r].z, acc[r][tt]);
+          acc[r][tt] = mfma4(w[tt].w, gb[r].w, acc[r][tt]);
+        }
+      if (c + 1 < kF48Kch) {
+        lds_barrier();  // every wave has read chunk c's halo image
+        store_chunk(pin);
+        lds_barrier();
+      }
+    }
+    // ---- epilogue: out = acc + x1 + bias (gdfn_out's order); x1 is read back from `out`, where this
+    // lane stored it (rows past the image: out-of-range offsets, dropped)
+#pragma unroll
+    for (int r = 0; r < kF48RPW; ++r) {
+      const int yo = y0 + kF48RPW * wave + r;
+      const unsigned off = yo < p.H ? (unsigned)(yo * p.W + x0 + li) * (unsigned)p.ldo * 4u + 16u * lq : kOOB2;
+      f32x4 x1v[3];
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt)
+        x1v[tt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ro, (int)(off + 64u * tt), 0, 0));
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4g, acc[r][tt] + x1v[tt] + lds[kF48Bout + 4 * tt + lq]), ro, (int)(off + 64u * tt), 0, 0);
+    }
+  }
+}
+
+bool ffn48_supported(int C, int hidS, int W) { return C == 48 && hidS == 16 * kF48Kch && W % kTile == 0; }
+
+hipError_t launch_ffn48(const Ffn48Params& p, hipStream_t s) {
+  if (p.W % kTile || p.ldv % 4 || p.ldx % 4 || p.ldo % 4 || p.Bn <= 0 || p.H <= 0) return hipErrorInvalidValue;
+  static bool attr[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!attr[dev]) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ffn48_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kF48Lds);
+    if (e != hipSuccess) return e;
+    attr[dev] = true;
+  }
+  const long long tiles = (long long)p.Bn * ((p.H + kF48TH - 1) / kF48TH) * (p.W / kTile);
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  long long grid = std::min<long long>(tiles, cus);  // one resident block per CU
+  grid = (grid + 7) / 8 * 8;
+  hipLaunchKernelGGL(ffn48_kernel, dim3((unsigned)grid), dim3(64 * kF48Waves), kF48Lds, s, p);
+  return hipGetLastError();
+}
+
 
 }  // namespace kdlae

@@ -36,6 +36,10 @@ struct BlockW {
   // forms x1), a plain LN GEMM on x1 runs group 1
   bool attn_in_split = false;
   Gemm pin_g0, pin_g1;
+  // C = 48 (r04): the whole FFN half (x1 = x + M v, LN, project_in, dwconv + gate, project_out,
+  // residual) in one kernel (gdfn.hip ffn48_kernel) writing the block output to another buffer; the
+  // stage alternates buffers.  Debug flag no_ffn48 keeps gemm_attn_in + gdfn_out (bit-identity test)
+  bool ffn48 = false;
 };
 
 }  // namespace kdlae
@@ -367,6 +371,8 @@ struct Packer {
       b.pin_g1.group_tiles = b.pin_g1.ntiles;
       b.fused_attn_in = b.attn_in_split = true;
     }
+    b.ffn48 = b.fused_attn_in && !b.attn_in_split && b.fused_gdfn && ffn48_supported(C, hidS, 16) &&
+              b.pin.ntiles == 2 * hidS / 16 && !debug_flag("no_ffn48");
     return b;
   }
 
@@ -536,8 +542,9 @@ struct Fwd {
     return probe_end(1, probeC, bytes, 2.0 * P * g.n_true * g.k_true);
   }
 
-  // One TransformerBlock (:159-163) in place on x.
-  int block(const BlockW& b, View x, int Hh, int Ww) {
+  // One TransformerBlock (:159-163) in place on x, or, with f48 (b.ffn48 and a width ffn48_kernel
+  // takes), from x into *f48 (which must not overlap x).
+  int block(const BlockW& b, View x, int Hh, int Ww, const View* f48 = nullptr) {
     const int HW = Hh * Ww;
     const int ln = h->cfg.layernorm_biasfree ? 1 : 2;
     const long long P = (long long)B * HW;
@@ -570,6 +577,34 @@ struct Fwd {
     if ((rc = probe_end(2, b.C, 4.0 * P * 4 * b.C, 2.0 * P * (27.0 * b.C + (double)b.C * b.Ch)))) return rc;
     HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
     HIPCHK(launch_attn_fold(buf(pl.red), gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
+    if (f48) {
+      Ffn48Params q{};
+      q.v = buf(pl.vbuf);
+      q.ldv = b.C;
+      q.x = x.p;
+      q.ldx = x.ld;
+      q.Wm = buf(pl.Mp);
+      q.wm_img_stride = (long long)b.C * b.C;
+      q.bias_m = h->P(b.proj_b);
+      q.ln = ln;
+      q.Win = h->P(b.pin.w);
+      q.bias_in = h->P(b.pin.bias);
+      q.dw = h->P(b.dwffn);
+      q.Wout = h->P(b.pout.w);
+      q.bias_out = h->P(b.pout.bias);
+      q.out = f48->p;
+      q.ldo = f48->ld;
+      q.Bn = B;
+      q.H = Hh;
+      q.W = Ww;
+      if ((rc = probe_begin(3, b.C))) return rc;
+      tag = "ffn48 C" + std::to_string(b.C) + " hid" + std::to_string(b.hid) + " HW" + std::to_string(HW);
+      HIPCHK(launch_ffn48(q, s));
+      // algorithmic: read v and x, write the block output; M v, project_in, dwconv + gate, project_out
+      const double Pd = (double)P;
+      return probe_end(3, b.C, 4.0 * Pd * 3.0 * b.C,
+                       2.0 * Pd * ((double)b.C * b.C + 2.0 * b.C * b.hid + 18.0 * b.hid + (double)b.hid * b.C));
+    }
     View fpre{buf(pl.fpre), 2 * b.hidS};
     const bool fuse_in = b.fused_attn_in;
     if (fuse_in) {
@@ -678,8 +713,22 @@ struct Fwd {
     if (st.empty()) return KDLAE_OK;
     int rc = tap(x, st[0].C, Hh, Ww);
     if (rc) return rc;
-    for (const BlockW& b : st) {
-      if ((rc = block(b, x, Hh, Ww))) return rc;
+    // ffn48 blocks write their output to the other buffer of (x, T), T = the project_in scratch they
+    // do not use; an even count of them keeps the stage's output in x (an odd last one runs unfused).
+    // Off while diagnostics taps are armed (they read x1, which ffn48 never materialises).
+    const bool f48 = st[0].ffn48 && h->taps.empty() && ffn48_supported(st[0].C, st[0].hidS, Ww);
+    const int nf = f48 ? (int)st.size() / 2 * 2 : 0;
+    const View T{buf(pl.fpre), st[0].C};
+    View cur = x;
+    for (int i = 0; i < (int)st.size(); ++i) {
+      const BlockW& b = st[i];
+      if (i < nf) {
+        const View nxt = (i % 2 == 0) ? T : x;
+        if ((rc = block(b, cur, Hh, Ww, &nxt))) return rc;
+        cur = nxt;
+      } else {
+        if ((rc = block(b, x, Hh, Ww))) return rc;
+      }
       if ((rc = tap(x, b.C, Hh, Ww))) return rc;
     }
     return KDLAE_OK;

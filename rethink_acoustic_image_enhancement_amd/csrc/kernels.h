@@ -133,6 +133,26 @@ struct GdfnParams {
 bool gdfn_supported(int C, int hidS);
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s);
 
+// Fused C = 48 feed-forward half of a TransformerBlock (gdfn.hip, ffn48_kernel): from the attention's
+// v and the block input x, out = x1 + project_out(gate(dwconv(project_in(LN(x1))))) with
+// x1 = x + M v (+ bias_m) — the gemm_attn_in_kernel + gdfn_out_kernel pair in one pass, bit for bit,
+// without the 2 hid-wide project_in rows (or x1) ever reaching HBM.  `out` must not overlap x or v
+// (neighbouring tiles read them as halo).
+struct Ffn48Params {
+  const float* v; int ldv;                          // attention v, [P][ldv] (48 channels)
+  const float* x; int ldx;                          // block input
+  const float* Wm; long long wm_img_stride;         // folded projection fragments per image (attn_fold)
+  const float* bias_m;                              // [48] or null
+  int ln;                                           // 1 BiasFree, 2 WithBias
+  const float* Win; const float* bias_in;           // project_in fragments [16][3][64][4], bias [256] or null
+  const float* dw;                                  // GDFN dw blocks, [8 chunks][512]
+  const float* Wout; const float* bias_out;         // project_out fragments [3][8][64][4], bias [48] or null
+  float* out; int ldo;
+  int Bn, H, W;
+};
+bool ffn48_supported(int C, int hidS, int W);
+hipError_t launch_ffn48(const Ffn48Params& p, hipStream_t s);
+
 // Pre/post-processing around the forward (pipeline.hip)
 struct PreParams {
   const uint8_t* in; int B, h, w, cin, cout, bgr;  // u8 [B][h][w][cin]

@@ -7,6 +7,8 @@
 #   bench     bench.py with the given args (default: the driver's default run)
 #   prof      rocprofv3 --kernel-trace --stats of the T16 bench and of the training bench
 #   profb     rocprofv3 --kernel-trace --stats of one bench.py run with the given args
+#   pmc_lds   one PMC pass of wave-state + LDS counters over one T16 step
+#   split     tools/stream_split_probe.py (two half-batches on two streams vs one)
 #   pmc       PMC passes over one T16 step: FETCH_SIZE, WRITE_SIZE, busy counters (one group per run)
 #   ab        library A/B: for each "name=path[,ENV=V...]" in $VARIANTS ("default" = in-tree build), the
 #             per-launch probe of class $PROBE (default 1) and a short T16 bench; CHECK=1 runs
@@ -67,6 +69,15 @@ pmc)
   timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- $B > $O/pmc_fetch.log 2>&1 || exit $?
   timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- $B > $O/pmc_write.log 2>&1 || exit $?
   timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_busy -o run -- $B > $O/pmc_busy.log 2>&1 || exit $?
+  ;;
+pmc_lds)  # one T16 step: wave-state and LDS counters per kernel (one pass)
+  cd /tmp && export TMPDIR=/tmp
+  B="python3 $R/bench.py --steps 1 --warmup 0 --probe 0 --no-cpu-baseline --no-bs1 --no-secondary"
+  timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --output-format csv -d $O/pmc_lds -o run -- $B > $O/pmc_lds.log 2>&1 || exit $?
+  ;;
+split)  # two half-batches on two streams vs one stream (tools/stream_split_probe.py)
+  timeout -k 10 300 python -u tools/stream_split_probe.py ${STEPS:-5} > $O/split.json 2> $O/split.err || { tail -20 $O/split.err; exit 1; }
+  cat $O/split.json
   ;;
 ab)
   for nv in ${VARIANTS:-default=default}; do
