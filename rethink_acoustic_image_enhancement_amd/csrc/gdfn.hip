@@ -513,7 +513,7 @@ static hipError_t launch_gdfn_out_small(const GdfnParams& p, int C, hipStream_t 
 //    XCD; all weights (project_in 48 KiB, project_out 24 KiB, dw 16 KiB, biases) resident in LDS, M
 //    restaged when the image changes;
 //  * phase A: the 18 x 14 halo = 14 row tiles of 16 pixels + 2 column tiles; wave w takes halo rows
-//    3w+1..3w+3 (its output rows: x1 is parked in `out` as the residual) and one of the 4 remaining
+//    3w+1..3w+3 (its output rows: their x1 is kept as the residual) and one of the 4 remaining
 //    tiles.  x1 = (M v + bias_m) + x, LayerNorm, in registers (lane: pixel, channel quad);
 //  * per 16-channel hidden chunk g: project_in of tiles 2g, 2g+1 (x1 and x2 halves) for the wave's
 //    halo pixels -> the chunk's halo image in LDS (gdfn_out's layout; out-of-image pixels 0), barrier,
@@ -617,11 +617,11 @@ __global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p)
     const unsigned obytes = (unsigned)HW * (unsigned)p.ldo * 4u;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
         p.out + (long long)b * HW * p.ldo, 0, (int)obytes, 0x00020000);
-    // ---- phase A: x1 and LN(x1) of the wave's halo pixels (the next tile's rows are loaded while one
-    // is computed).  x1 of the wave's output rows goes to `out` (it is the residual the epilogue adds;
-    // the same lane reads it back), so it holds no registers across the chunk loop.
+    // ---- phase A: x1 and LN(x1) of the wave's halo pixels (the next pixel tile's rows are loaded while
+    // one is computed); x1 of the wave's output rows stays in registers as the epilogue's residual
     bool in[4];
     f32x4 xn[4][3];
+    f32x4 x1r[3][3];
     {
       const f32x4* ml = lds + kF48M;
       f32x4 va[2][3], xa[2][3];
@@ -667,12 +667,7 @@ __global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p)
           f32x4 v = a1[g] + lds[kF48Bm + 4 * g + lq];
           v += xa[cb][g];
           a[g] = v;
-          // an output row (pt < 3: interior columns; the row may be past the image bottom: in[] = 0)
-          if (pt < 3)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4g, v), ro,
-                                                   (int)((in[pt] ? (unsigned)((y0 + kF48RPW * wave + pt) * p.W + x0 + li) *
-                                                                       (unsigned)p.ldo * 4u + 16u * lq
-                                                                 : kOOB2) + 64u * g), 0, 0);
+          if (pt < 3) x1r[pt][g] = v;
         }
         // LayerNorm over the 48 channels (gemm.hip apply_ln, row in registers)
         float sm = 0.f;
@@ -744,9 +739,7 @@ __global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p)
 #pragma unroll 1
     for (int c = 0; c < kF48Kch; ++c) {
       f32x4 gb[kF48RPW];
-      gate_rows<kF48RPW, kGeluPacked, true>(lds + kF48Hb, lds + kF48Dw + c * kDwF4, lo, lq, gb);
-      __builtin_amdgcn_sched_barrier(0);  // the gate's 30 halo reads and project_in's operands would
-                                          // not fit the 256 VGPRs together (the SIMD's other wave overlaps them)
+      gate_rows<kF48RPW, kGeluPacked>(lds + kF48Hb, lds + kF48Dw + c * kDwF4, lo, lq, gb);
       if (c + 1 < kF48Kch) project_in(c + 1, pin);
       f32x4 w[3];
 #pragma unroll
@@ -766,20 +759,16 @@ __global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p)
         lds_barrier();
       }
     }
-    // ---- epilogue: out = acc + x1 + bias (gdfn_out's order); x1 is read back from `out`, where this
-    // lane stored it (rows past the image: out-of-range offsets, dropped)
+    // ---- epilogue: out = acc + x1 + bias (gdfn_out's order); rows past the image get out-of-range
+    // offsets (dropped)
 #pragma unroll
     for (int r = 0; r < kF48RPW; ++r) {
       const int yo = y0 + kF48RPW * wave + r;
       const unsigned off = yo < p.H ? (unsigned)(yo * p.W + x0 + li) * (unsigned)p.ldo * 4u + 16u * lq : kOOB2;
-      f32x4 x1v[3];
-#pragma unroll
-      for (int tt = 0; tt < 3; ++tt)
-        x1v[tt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ro, (int)(off + 64u * tt), 0, 0));
 #pragma unroll
       for (int tt = 0; tt < 3; ++tt)
         __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4g, acc[r][tt] + x1v[tt] + lds[kF48Bout + 4 * tt + lq]), ro, (int)(off + 64u * tt), 0, 0);
+            __builtin_bit_cast(u32x4g, acc[r][tt] + x1r[r][tt] + lds[kF48Bout + 4 * tt + lq]), ro, (int)(off + 64u * tt), 0, 0);
     }
   }
 }
