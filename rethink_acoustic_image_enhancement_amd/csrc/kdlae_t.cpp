@@ -38,7 +38,8 @@ struct BlockW {
   Gemm pin_g0, pin_g1;
   // C = 48 (r04): the whole FFN half (x1 = x + M v, LN, project_in, dwconv + gate, project_out,
   // residual) in one kernel (gdfn.hip ffn48_kernel) writing the block output to another buffer; the
-  // stage alternates buffers.  Debug flag no_ffn48 keeps gemm_attn_in + gdfn_out (bit-identity test)
+  // stage alternates buffers.  Opt-in (debug flag ffn48): bit-identical, but measured slower than
+  // gemm_attn_in + gdfn_out (12.46 vs 11.2 ms per 1024^2 block, profiles/r04_ffn48_ab_probe.txt)
   bool ffn48 = false;
 };
 
@@ -372,7 +373,7 @@ struct Packer {
       b.fused_attn_in = b.attn_in_split = true;
     }
     b.ffn48 = b.fused_attn_in && !b.attn_in_split && b.fused_gdfn && ffn48_supported(C, hidS, 16) &&
-              b.pin.ntiles == 2 * hidS / 16 && !debug_flag("no_ffn48");
+              b.pin.ntiles == 2 * hidS / 16 && debug_flag("ffn48");
     return b;
   }
 

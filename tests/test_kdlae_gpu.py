@@ -176,13 +176,13 @@ def test_fused_attention_input_equals_unfused_bit_for_bit(ln, split, monkeypatch
 def test_ffn48_equals_unfused_bit_for_bit(ln, bias, nb0, nref, shape, monkeypatch):
     """ffn48_kernel (the C = 48 blocks' whole FFN half: x1 = x + M v, LN, project_in on the tile's halo,
     dwconv + gate, project_out, residual; output to the other buffer of a ping-pong pair) gives the same
-    bits as gemm_attn_in_kernel + gdfn_out_kernel (KDLAE_DEBUG=no_ffn48)."""
+    bits as gemm_attn_in_kernel + gdfn_out_kernel (the default path; ffn48 is opt-in: KDLAE_DEBUG=ffn48)."""
     kw = dict(dim=48, LayerNorm_type=ln, num_blocks=[nb0, 1, 1, 1], num_refinement_blocks=nref, bias=bias)
     img = torch.from_numpy(hash_images("f48", shape))
     rate = torch.from_numpy(hash_images("f48r", (shape[0], 1) + shape[2:]))
-    fused = _run(_model(kw), img, rate)
-    monkeypatch.setenv("KDLAE_DEBUG", "no_ffn48")  # read when a new handle builds its blocks
     unfused = _run(_model(kw), img, rate)
+    monkeypatch.setenv("KDLAE_DEBUG", "ffn48")  # read when a new handle builds its blocks
+    fused = _run(_model(kw), img, rate)
     assert torch.equal(fused["hq"], unfused["hq"]) and torch.equal(fused["sr"], unfused["sr"])
 
 
