@@ -51,11 +51,16 @@ torch.cuda.synchronize()
 print(f"untraced step: {e0.elapsed_time(e1) / 5:.2f} ms")
 if os.path.exists(out):
     os.remove(out)
-os.environ["KDLAE_DEBUG"] = "train_trace"
+# one stream for the traced step (the backward's side stream would overlap the launches being timed)
+keep = os.environ.get("KDLAE_DEBUG")
+os.environ["KDLAE_DEBUG"] = "train_trace,train_serial"
 os.environ["KDLAE_PROBE_DUMP"] = out
 step()
 torch.cuda.synchronize()
-del os.environ["KDLAE_DEBUG"]
+if keep is None:
+    del os.environ["KDLAE_DEBUG"]
+else:
+    os.environ["KDLAE_DEBUG"] = keep
 ROLES = {"fwd", "dW", "dX", "fwd3", "dW3", "dX3", "gram", "av", "dA", "dv", "dq", "dk"}
 rows = []
 for line in open(out):
