@@ -522,21 +522,21 @@ static hipError_t launch_gdfn_out_small(const GdfnParams& p, int C, hipStream_t 
 //  Every value is computed by the same operation sequence as the kernel pair (same fragments, same
 //  MFMA k order per accumulator, the same LN and gate code), so the output is bit-identical.
 namespace {
-constexpr int kF48RPW = 3, kF48Waves = 4, kF48TH = kF48RPW * kF48Waves;  // 12 tile rows
+constexpr int kF48RPW = 3, kF48Main = 4, kF48TH = kF48RPW * kF48Main;   // 12 tile rows
+constexpr int kF48Waves = 2 * kF48Main;                                  // + 4 project_in waves
 constexpr int kF48HR = kF48TH + 2;                                     // 14 halo rows
 constexpr int kF48Px = kF48HR * kHalo;                                 // 252 halo pixels
 constexpr int kF48Kch = 8;                                             // hidden chunks (hidS = 128)
 constexpr int kF48Tin = 2 * kF48Kch;                                   // project_in output tiles
 // LDS carve, f32x4 units
-constexpr int kF48Hb = 0;                                // [468 px][8 slots] chunk halo image
-constexpr int kF48Win = kF48Hb + kF48Px * 8;             // [16 tiles][3 k-groups][64]
-constexpr int kF48Wout = kF48Win + kF48Tin * 3 * 64;     // [3 tiles][8 chunks][64]
-constexpr int kF48Dw = kF48Wout + 3 * kF48Kch * 64;      // [8 chunks][128]
+constexpr int kF48Hb = 0;                                // [2][252 px][8 slots] chunk halo images
+constexpr int kF48Win = kF48Hb + 2 * kF48Px * 8;         // [16 tiles][3 k-groups][64]
+constexpr int kF48Dw = kF48Win + kF48Tin * 3 * 64;       // [8 chunks][128]
 constexpr int kF48M = kF48Dw + kF48Kch * kDwF4;          // [3][3][64] folded projection of the image
 constexpr int kF48Bm = kF48M + 9 * 64;                   // [12] bias_m
 constexpr int kF48Bin = kF48Bm + 12;                     // [64] bias_in
 constexpr int kF48Bout = kF48Bin + kF48Tin * 4;          // [12] bias_out
-constexpr int kF48Lds = (kF48Bout + 12) * 16;            // 132,992 bytes: one block per CU
+constexpr int kF48Lds = (kF48Bout + 12) * 16;            // 140,672 bytes: one block per CU
 static_assert(kF48Lds <= 160 * 1024, "ffn48 LDS");
 
 __device__ __forceinline__ void lds_barrier() {
@@ -544,12 +544,37 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
+
+// x1 = (M v + bias_m) + x for one 16-pixel tile (lane: pixel li, channel quad lq), the M GEMM in
+// gemm_attn_in's per-accumulator order (k-group major, k-step minor)
+__device__ __forceinline__ void f48_x1(const f32x4* ml, const f32x4* bm, int lane, int lq, const f32x4 (&va)[3],
+                                       const f32x4 (&xa)[3], f32x4 (&x1)[3]) {
+  f32x4 a1[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    f32x4 wm[3];
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt) wm[tt] = ml[(tt * 3 + g) * 64 + lane];
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) a1[tt] = mfma4(wm[tt][ss], va[g][ss], a1[tt]);
+  }
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    f32x4 v = a1[g] + bm[4 * g + lq];
+    v += xa[g];
+    x1[g] = v;
+  }
+}
 }  // namespace
 
 __global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p) {
   extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool main_w = wave < kF48Main;                    // gate + project_out of tile rows 3w..3w+2
+  const int hw = main_w ? wave : wave - kF48Main;         // helper index / row group of the wave
   const int li = lane & 15, lq = lane >> 4;
   const int tx_n = p.W / kTile, ty_n = (p.H + kF48TH - 1) / kF48TH;
   const int per_img = tx_n * ty_n;
@@ -561,12 +586,10 @@ __global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p)
   const int t_lo = (int)((long long)ntiles * xcd / 8), t_hi = (int)((long long)ntiles * (xcd + 1) / 8);
   if (t_lo + xb >= t_hi) return;
 
-  // resident weights
+  // resident weights (project_out's stream from L2 into the main waves' registers, a chunk ahead)
   {
     const f32x4* win = reinterpret_cast<const f32x4*>(p.Win);
     for (int i = tid; i < kF48Tin * 3 * 64; i += 64 * kF48Waves) lds[kF48Win + i] = win[i];
-    const f32x4* wout = reinterpret_cast<const f32x4*>(p.Wout);
-    for (int i = tid; i < 3 * kF48Kch * 64; i += 64 * kF48Waves) lds[kF48Wout + i] = wout[i];
     const f32x4* dwg = reinterpret_cast<const f32x4*>(p.dw);
     for (int i = tid; i < kF48Kch * kDwF4; i += 64 * kF48Waves) lds[kF48Dw + i] = dwg[i];
     for (int i = tid; i < kF48Tin * 4; i += 64 * kF48Waves)
@@ -575,29 +598,30 @@ __global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p)
       lds[kF48Bout + i] = p.bias_out ? reinterpret_cast<const f32x4*>(p.bias_out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const float wb = (p.ln == 2) ? 1.f : 0.f;
-  // stencil read offsets (gdfn_out's, for the wave's first halo row)
+  const f32x4* wout = reinterpret_cast<const f32x4*>(p.Wout);
+  // stencil read offsets (gdfn_out's, for the main wave's first halo row)
   int lo[2][3];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int hx = li + j;
-      lo[h][j] = (kF48RPW * wave * kHalo + hx) * 8 + ((4 * h + lq) ^ (hx & 7));
+      lo[h][j] = (kF48RPW * hw * kHalo + hx) * 8 + ((4 * h + lq) ^ (hx & 7));
     }
-  // phase-A pixel tiles of this wave: pt 0..2 = halo rows 3w+1..3w+3 (the wave's output rows, interior
-  // columns), pt 3 = the top halo row (w 0), the bottom one (w 1), the left (w 2) or right (w 3) halo
-  // column (14 pixels)
+  // pixel tiles of helper hw (and, pt 0..2, of main wave hw): pt 0..2 = halo rows 3hw+1..3hw+3 (the
+  // main wave's output rows, interior columns), pt 3 = the top halo row (0), the bottom one (1), the
+  // left (2) or right (3) halo column (14 pixels)
   int hy[4], hx[4];
   bool tv[4];
 #pragma unroll
   for (int pt = 0; pt < 3; ++pt) {
-    hy[pt] = kF48RPW * wave + 1 + pt;
+    hy[pt] = kF48RPW * hw + 1 + pt;
     hx[pt] = li + 1;
     tv[pt] = true;
   }
-  hy[3] = wave == 0 ? 0 : wave == 1 ? kF48HR - 1 : li;
-  hx[3] = wave <= 1 ? li + 1 : (wave == 2 ? 0 : kHalo - 1);
-  tv[3] = wave <= 1 || li < kF48HR;
+  hy[3] = hw == 0 ? 0 : hw == 1 ? kF48HR - 1 : li;
+  hx[3] = hw <= 1 ? li + 1 : (hw == 2 ? 0 : kHalo - 1);
+  tv[3] = hw <= 1 || li < kF48HR;
 
   int staged = -1;
   for (int t = t_lo + xb; t < t_hi; t += nxb) {
@@ -614,161 +638,172 @@ __global__ __launch_bounds__(64 * kF48Waves, 1) void ffn48_kernel(Ffn48Params p)
       __syncthreads();
       staged = b;
     }
-    const unsigned obytes = (unsigned)HW * (unsigned)p.ldo * 4u;
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        p.out + (long long)b * HW * p.ldo, 0, (int)obytes, 0x00020000);
-    // ---- phase A: x1 and LN(x1) of the wave's halo pixels (the next pixel tile's rows are loaded while
-    // one is computed); x1 of the wave's output rows stays in registers as the epilogue's residual
+    const unsigned vbytes = (unsigned)HW * (unsigned)p.ldv * 4u, xbytes = (unsigned)HW * (unsigned)p.ldx * 4u;
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(p.v + (long long)b * HW * p.ldv), 0, (int)vbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rxx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(p.x + (long long)b * HW * p.ldx), 0, (int)xbytes, 0x00020000);
     bool in[4];
-    f32x4 xn[4][3];
-    f32x4 x1r[3][3];
-    {
-      const f32x4* ml = lds + kF48M;
-      f32x4 va[2][3], xa[2][3];
-      // raw buffer loads through per-image descriptors: 32-bit offsets, zeros past the range (the
-      // offset of an out-of-image pixel), no branches
-      const unsigned vbytes = (unsigned)HW * (unsigned)p.ldv * 4u, xbytes = (unsigned)HW * (unsigned)p.ldx * 4u;
-      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(p.v + (long long)b * HW * p.ldv), 0, (int)vbytes, 0x00020000);
-      const __amdgpu_buffer_rsrc_t rxx = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(p.x + (long long)b * HW * p.ldx), 0, (int)xbytes, 0x00020000);
-      auto load = [&](int pt, f32x4 (&vv)[3], f32x4 (&xx3)[3]) {
-        const int yy = y0 - 1 + hy[pt], xx = x0 - 1 + hx[pt];
-        in[pt] = tv[pt] && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-        const unsigned px = (unsigned)(yy * p.W + xx);
-        const unsigned ov = in[pt] ? px * (unsigned)p.ldv * 4u + 16u * lq : kOOB2;
-        const unsigned ox = in[pt] ? px * (unsigned)p.ldx * 4u + 16u * lq : kOOB2;
+    // raw buffer loads: 32-bit offsets, zeros past the range (out-of-image pixels), no branches
+    auto load = [&](int pt, f32x4 (&vv)[3], f32x4 (&xx3)[3]) {
+      const int yy = y0 - 1 + hy[pt], xx = x0 - 1 + hx[pt];
+      in[pt] = tv[pt] && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      const unsigned px = (unsigned)(yy * p.W + xx);
+      const unsigned ov = in[pt] ? px * (unsigned)p.ldv * 4u + 16u * lq : kOOB2;
+      const unsigned ox = in[pt] ? px * (unsigned)p.ldx * 4u + 16u * lq : kOOB2;
 #pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          vv[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(ov + 64u * g), 0, 0));
-          xx3[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rxx, (int)(ox + 64u * g), 0, 0));
+      for (int g = 0; g < 3; ++g) {
+        vv[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(ov + 64u * g), 0, 0));
+        xx3[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rxx, (int)(ox + 64u * g), 0, 0));
+      }
+    };
+    const f32x4* ml = lds + kF48M;
+    const f32x4* bm = lds + kF48Bm;
+    if (main_w) {
+      // ---- main wave: x1 of its output rows (the residual; the helper of the same rows forms the same
+      // values for LN), then per chunk the gate and project_out
+      // x1 is parked in `out` at the lane's own addresses (the epilogue reads it back: same thread, so
+      // program order holds) instead of holding 36 registers across the chunk loop
+      const unsigned obytes = (unsigned)HW * (unsigned)p.ldo * 4u;
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          p.out + (long long)b * HW * p.ldo, 0, (int)obytes, 0x00020000);
+      unsigned oo[kF48RPW];
+#pragma unroll
+      for (int r = 0; r < kF48RPW; ++r) {
+        const int yo = y0 + kF48RPW * hw + r;
+        oo[r] = yo < p.H ? (unsigned)(yo * p.W + x0 + li) * (unsigned)p.ldo * 4u + 16u * lq : kOOB2;
+      }
+      {
+        f32x4 va[3][3], xa[3][3];
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt) load(pt, va[pt], xa[pt]);
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt) {
+          f32x4 x1[3];
+          f48_x1(ml, bm, lane, lq, va[pt], xa[pt], x1);
+#pragma unroll
+          for (int tt = 0; tt < 3; ++tt)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4g, x1[tt]), ro, (int)(oo[pt] + 64u * tt), 0, 0);
         }
-      };
-      load(0, va[0], xa[0]);
+      }
+      f32x4 acc[kF48RPW][3];
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        const int cb = pt & 1;
-        if (pt + 1 < 4) load(pt + 1, va[cb ^ 1], xa[cb ^ 1]);
-        // M v: per accumulator, k-group-major and k-step-minor (gemm_attn_in's mfma_chunk order)
-        f32x4 a1[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      for (int r = 0; r < kF48RPW; ++r)
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt) acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 w[3];
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) w[tt] = wout[(tt * kF48Kch + 0) * 64 + lane];
+      lds_barrier();  // chunk 0's halo image
+#pragma unroll 1
+      for (int c = 0; c < kF48Kch; ++c) {
+        f32x4 wn[3];
+        if (c + 1 < kF48Kch) {
+#pragma unroll
+          for (int tt = 0; tt < 3; ++tt) wn[tt] = wout[(tt * kF48Kch + c + 1) * 64 + lane];
+        }
+        f32x4 gb[kF48RPW];
+        gate_rows<kF48RPW, kGeluPacked>(lds + kF48Hb + (c & 1) * kF48Px * 8, lds + kF48Dw + c * kDwF4, lo, lq, gb);
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+          for (int r = 0; r < kF48RPW; ++r) {
+            acc[r][tt] = mfma4(w[tt].x, gb[r].x, acc[r][tt]);
+            acc[r][tt] = mfma4(w[tt].y, gb[r].y, acc[r][tt]);
+            acc[r][tt] = mfma4(w[tt].z, gb[r].z, acc[r][tt]);
+            acc[r][tt] = mfma4(w[tt].w, gb[r].w, acc[r][tt]);
+          }
+        if (c + 1 < kF48Kch) {
+#pragma unroll
+          for (int tt = 0; tt < 3; ++tt) w[tt] = wn[tt];
+        }
+        lds_barrier();  // chunk c's image read; chunk c+1's written
+      }
+      // ---- epilogue: out = acc + x1 + bias (gdfn_out's order); rows past the image dropped
+#pragma unroll
+      for (int r = 0; r < kF48RPW; ++r) {
+        f32x4 x1v[3];
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt)
+          x1v[tt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ro, (int)(oo[r] + 64u * tt), 0, 0));
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4g, acc[r][tt] + x1v[tt] + lds[kF48Bout + 4 * tt + lq]), ro, (int)(oo[r] + 64u * tt), 0,
+              0);
+      }
+    } else {
+      // ---- helper wave: x1 and LN(x1) of its 4 halo pixel tiles, then project_in chunk by chunk into
+      // the double-buffered halo image (chunk c+1 is written while the main waves gate chunk c)
+      f32x4 xn[4][3];
+      {
+        f32x4 va[2][3], xa[2][3];
+        load(0, va[0], xa[0]);
+#pragma unroll
+        for (int pt = 0; pt < 4; ++pt) {
+          const int cb = pt & 1;
+          if (pt + 1 < 4) load(pt + 1, va[cb ^ 1], xa[cb ^ 1]);
+          f32x4 a[3];
+          f48_x1(ml, bm, lane, lq, va[cb], xa[cb], a);
+          // LayerNorm over the 48 channels (gemm.hip apply_ln, row in registers)
+          float sm = 0.f;
+#pragma unroll
+          for (int g = 0; g < 3; ++g) sm += (a[g].x + a[g].y) + (a[g].z + a[g].w);
+          sm += __shfl_xor(sm, 16);
+          sm += __shfl_xor(sm, 32);
+          const float mean = sm / 48.0f;
+          float v2 = 0.f;
+#pragma unroll
+          for (int g = 0; g < 3; ++g) {
+            const f32x4 d = a[g] - mean;
+            const float dd = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+            v2 += dd;
+          }
+          v2 += __shfl_xor(v2, 16);
+          v2 += __shfl_xor(v2, 32);
+          const float rstd = 1.0f / sqrtf(v2 / 48.0f + 1e-5f);
+          const float sh = mean * wb;
+#pragma unroll
+          for (int g = 0; g < 3; ++g) xn[pt][g] = (a[g] - sh) * rstd;
+        }
+      }
+      // project_in of chunk c (tiles 2c, 2c+1) + bias -> halo image buffer c & 1 (out-of-image pixels 0)
+      auto project_in = [&](int c) {
+        f32x4 o[4][2];
+#pragma unroll
+        for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) o[pt][hh] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
-          f32x4 wm[3];
-#pragma unroll
-          for (int tt = 0; tt < 3; ++tt) wm[tt] = ml[(tt * 3 + g) * 64 + lane];
+          const f32x4 w0 = lds[kF48Win + ((2 * c) * 3 + g) * 64 + lane];
+          const f32x4 w1 = lds[kF48Win + ((2 * c + 1) * 3 + g) * 64 + lane];
 #pragma unroll
           for (int ss = 0; ss < 4; ++ss)
 #pragma unroll
-            for (int tt = 0; tt < 3; ++tt) a1[tt] = mfma4(wm[tt][ss], va[cb][g][ss], a1[tt]);
+            for (int pt = 0; pt < 4; ++pt) {
+              o[pt][0] = mfma4(w0[ss], xn[pt][g][ss], o[pt][0]);
+              o[pt][1] = mfma4(w1[ss], xn[pt][g][ss], o[pt][1]);
+            }
         }
-        f32x4 a[3];
+        f32x4* hb = lds + kF48Hb + (c & 1) * kF48Px * 8;
 #pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          f32x4 v = a1[g] + lds[kF48Bm + 4 * g + lq];
-          v += xa[cb][g];
-          a[g] = v;
-          if (pt < 3) x1r[pt][g] = v;
-        }
-        // LayerNorm over the 48 channels (gemm.hip apply_ln, row in registers)
-        float sm = 0.f;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) sm += (a[g].x + a[g].y) + (a[g].z + a[g].w);
-        sm += __shfl_xor(sm, 16);
-        sm += __shfl_xor(sm, 32);
-        const float mean = sm / 48.0f;
-        float v2 = 0.f;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const f32x4 d = a[g] - mean;
-          const float dd = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
-          v2 += dd;
-        }
-        v2 += __shfl_xor(v2, 16);
-        v2 += __shfl_xor(v2, 32);
-        const float rstd = 1.0f / sqrtf(v2 / 48.0f + 1e-5f);
-        const float sh = mean * wb;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) xn[pt][g] = (a[g] - sh) * rstd;
-      }
-    }
-    // ---- project_in of one chunk for the wave's halo pixels (tiles 2c, 2c+1), + bias
-    auto project_in = [&](int c, f32x4 (&o)[4][2]) {
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) o[pt][hh] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const f32x4 w0 = lds[kF48Win + ((2 * c) * 3 + g) * 64 + lane];
-        const f32x4 w1 = lds[kF48Win + ((2 * c + 1) * 3 + g) * 64 + lane];
-#pragma unroll
-        for (int ss = 0; ss < 4; ++ss)
+        for (int hh = 0; hh < 2; ++hh) {
+          const f32x4 bias = lds[kF48Bin + 4 * (2 * c + hh) + lq];
 #pragma unroll
           for (int pt = 0; pt < 4; ++pt) {
-            o[pt][0] = mfma4(w0[ss], xn[pt][g][ss], o[pt][0]);
-            o[pt][1] = mfma4(w1[ss], xn[pt][g][ss], o[pt][1]);
+            const f32x4 v = o[pt][hh] + bias;
+            if (tv[pt]) hb[(hy[pt] * kHalo + hx[pt]) * 8 + ((4 * hh + lq) ^ (hx[pt] & 7))] = in[pt] ? v : f32x4{0.f, 0.f, 0.f, 0.f};
           }
-      }
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const f32x4 bias = lds[kF48Bin + 4 * (2 * c + hh) + lq];
-#pragma unroll
-        for (int pt = 0; pt < 4; ++pt) o[pt][hh] = o[pt][hh] + bias;
-      }
-    };
-    auto store_chunk = [&](const f32x4 (&o)[4][2]) {
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        if (!tv[pt]) continue;
-        const int base = (hy[pt] * kHalo + hx[pt]) * 8;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-          lds[kF48Hb + base + ((4 * hh + lq) ^ (hx[pt] & 7))] = in[pt] ? o[pt][hh] : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    };
-    f32x4 acc[kF48RPW][3];
-#pragma unroll
-    for (int r = 0; r < kF48RPW; ++r)
-#pragma unroll
-      for (int tt = 0; tt < 3; ++tt) acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 pin[4][2];
-    project_in(0, pin);
-    lds_barrier();  // the previous tile's last gate has read the halo image
-    store_chunk(pin);
-    lds_barrier();
-#pragma unroll 1
-    for (int c = 0; c < kF48Kch; ++c) {
-      f32x4 gb[kF48RPW];
-      gate_rows<kF48RPW, kGeluPacked>(lds + kF48Hb, lds + kF48Dw + c * kDwF4, lo, lq, gb);
-      if (c + 1 < kF48Kch) project_in(c + 1, pin);
-      f32x4 w[3];
-#pragma unroll
-      for (int tt = 0; tt < 3; ++tt) w[tt] = lds[kF48Wout + (tt * kF48Kch + c) * 64 + lane];
-#pragma unroll
-      for (int tt = 0; tt < 3; ++tt)
-#pragma unroll
-        for (int r = 0; r < kF48RPW; ++r) {
-          acc[r][tt] = mfma4(w[tt].x, gb[r].x, acc[r][tt]);
-          acc[r][tt] = mfma4(w[tt].y, gb[r].y, acc[r][tt]);
-          acc[r][tt] = mfma4(w[tt].z, gb[r].z, acc[r][tt]);
-          acc[r][tt] = mfma4(w[tt].w, gb[r].w, acc[r][tt]);
         }
-      if (c + 1 < kF48Kch) {
-        lds_barrier();  // every wave has read chunk c's halo image
-        store_chunk(pin);
+      };
+      project_in(0);
+      lds_barrier();  // chunk 0's halo image
+#pragma unroll 1
+      for (int c = 0; c < kF48Kch; ++c) {
+        if (c + 1 < kF48Kch) project_in(c + 1);
         lds_barrier();
       }
-    }
-    // ---- epilogue: out = acc + x1 + bias (gdfn_out's order); rows past the image get out-of-range
-    // offsets (dropped)
-#pragma unroll
-    for (int r = 0; r < kF48RPW; ++r) {
-      const int yo = y0 + kF48RPW * wave + r;
-      const unsigned off = yo < p.H ? (unsigned)(yo * p.W + x0 + li) * (unsigned)p.ldo * 4u + 16u * lq : kOOB2;
-#pragma unroll
-      for (int tt = 0; tt < 3; ++tt)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4g, acc[r][tt] + x1r[r][tt] + lds[kF48Bout + 4 * tt + lq]), ro, (int)(off + 64u * tt), 0, 0);
     }
   }
 }
