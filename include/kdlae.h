@@ -40,7 +40,10 @@
  * GEMMs and bias column sums run on a library-owned non-blocking side stream
  * that is forked from and joined back into the caller's stream inside the call
  * (every gradient-ready mark and the call's end follow a join), with the same
- * results either way.
+ * results either way.  "train_keep_yd" (read by kdlae_tt_forward; the backward
+ * follows what the forward kept) stores the GDFN dwconv output for the
+ * backward instead of having the backward recompute it from its input (A/B
+ * only: same gradients bit for bit, 1 KiB per pixel more traffic each way).
  */
 #ifndef KDLAE_H_
 #define KDLAE_H_

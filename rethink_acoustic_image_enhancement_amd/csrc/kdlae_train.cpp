@@ -657,9 +657,12 @@ int block_fwd(Ctx& c, BlockRec& r) {
   const int L2 = ld4(2 * hid), L1 = ld4(hid);
   r.y = c.alloc(P * L2);
   TRY(conv1(c, p + ".ffn.project_in", {r.xn2, C}, C, 2 * hid, P, {r.y, L2}, nullptr, 0, {nullptr, 0}, true));
-  r.yd = c.alloc(P * L2);
+  // yd (the dwconv output) is not kept: the backward recomputes it from y, which its weight gradient
+  // reads anyway (1 KiB per pixel less written here and read there); KDLAE_DEBUG=train_keep_yd stores
+  // it for the stored-yd backward (A/B; same bits)
+  r.yd = kdlae::debug_flag("train_keep_yd") ? c.alloc(P * L2) : nullptr;
   r.g = c.alloc(P * L1);
-  // dwconv + GELU gate in one pass (train_dwg.hip): yd for the backward, g for project_out
+  // dwconv + GELU gate in one pass (train_dwg.hip): g for project_out
   LAUNCH(tr::launch_dwgate_fwd(r.y, L2, c.W(p + ".ffn.dwconv.weight"), c.W(p + ".ffn.dwconv.bias"), hid, Bn, r.H,
                                r.W, r.yd, L2, r.g, L1, c.s));
   r.out = c.alloc(P * C);
@@ -717,8 +720,13 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
     const int nb = tr::dwg_blocks(Bn, r.H, r.W);
     float* part = red_take(c, (size_t)nb * 10 * 2 * hid);
     if (!part) return c.red_err;
-    LAUNCH(tr::launch_dwgate_bwd(dg, L1, r.yd, L2, r.y, L2, c.W(p + ".ffn.dwconv.weight"), hid, Bn, r.H, r.W, dy, L2,
-                                 part, c.s));
+    if (r.yd) {
+      LAUNCH(tr::launch_dwgate_bwd(dg, L1, r.yd, L2, r.y, L2, c.W(p + ".ffn.dwconv.weight"), hid, Bn, r.H, r.W, dy,
+                                   L2, part, c.s));
+    } else {
+      LAUNCH(tr::launch_dwgate_bwd_rc(dg, L1, r.y, L2, c.W(p + ".ffn.dwconv.weight"), c.W(p + ".ffn.dwconv.bias"), hid,
+                                      Bn, r.H, r.W, dy, L2, part, c.s));
+    }
     TRY(dw_reduce(c, part, nb, 2 * hid, p + ".ffn.dwconv"));
   }
   float* dxn2 = c.alloc(P * C);

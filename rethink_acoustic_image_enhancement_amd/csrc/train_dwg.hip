@@ -2,9 +2,10 @@
 // (KDLAE_model.py:101-105: x1, x2 = dwconv(project_in(x)).chunk(2); gelu(x1) * x2) and the MDTA qkv
 // dwconv (:127), forward and backward, each in one pass over HBM.
 //
-//   dwgate_fwd : yd = dw(y) (+ bias) for both halves, g = gelu_erf(yd1) * yd2 — y read once, yd
-//                (the backward's gate input) and g written; the separate dwconv + gate kernels read
-//                yd a second time.
+//   dwgate_fwd : yd = dw(y) (+ bias) for both halves, g = gelu_erf(yd1) * yd2 — y read once, g
+//                written (and yd, the stored-yd backward's gate input, under KDLAE_DEBUG=train_keep_yd);
+//                the separate dwconv + gate kernels read yd a second time.
+//   dwgate_bwd_rc: the GDFN backward recomputing yd from y (below).
 //   dw_bwd     : from dyd (GATE: dyd = gate_bwd(dg, yd) computed on the fly), dy = dw^T(dyd) (the
 //                flipped-tap conv) and the weight / bias gradient partials sum dyd * y_in(shifted),
 //                sum dyd — dyd is never written; the unfused chain wrote it and read it twice.
@@ -15,7 +16,8 @@
 // columns (16 columns) x TY rows of one image x 64 channels; a thread walks its 4 columns down the
 // rows with a 3-row x 6-column register window per tensor (each input row is loaded once per walk;
 // the 2 halo columns are the neighbouring wave's, L1 hits).  Accumulation order per output: bias,
-// then taps row-major (as dw_tile_fwd_kernel).  Weight gradient partials: the block's 4 waves in
+// then taps row-major (as dw_tile_fwd_kernel), every multiply-add an explicit fma (so the recomputing
+// backward reproduces the forward's yd and the stored-yd backward's arithmetic exactly).  Weight gradient partials: the block's 4 waves in
 // fixed order -> part[spatial block][c * 9 + t] and part[..][9 C + c] (C = all channels), summed
 // over spatial blocks in fixed order by part_reduce: deterministic.
 #include <math.h>
@@ -64,7 +66,7 @@ __device__ __forceinline__ float erf_half(float x, float& ex) {
   poly = fmaf(poly, t, 0.254829592f);
   poly *= t;
   ex = __expf(-z * z);
-  return copysignf(1.0f - poly * ex, x);
+  return copysignf(fmaf(-poly, ex, 1.0f), x);
 }
 
 // forward GELU with libm's erff (measured 5% faster here than the A&S form, which pays off only
@@ -145,14 +147,16 @@ __global__ __launch_bounds__(256) void dwgate_fwd_kernel(const float* __restrict
       for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
         for (int tx = 0; tx < 3; ++tx) {
-          s1 += w1[ty * 3 + tx] * a[ty][u + tx];
-          s2 += w2[ty * 3 + tx] * v[ty][u + tx];
+          s1 = fmaf(w1[ty * 3 + tx], a[ty][u + tx], s1);
+          s2 = fmaf(w2[ty * 3 + tx], v[ty][u + tx], s2);
         }
       const int xx = o.x0 + u;
       if (o.live && xx < W) {
         const long long p = o.img0 + (long long)yy * W + xx;
-        yd[p * ldyd + c] = s1;
-        yd[p * ldyd + hid + c] = s2;
+        if (yd) {  // (null: the backward recomputes yd, dwgate_bwd_rc_kernel)
+          yd[p * ldyd + c] = s1;
+          yd[p * ldyd + hid + c] = s2;
+        }
         g[p * ldg + c] = gelu_erf(s1) * s2;
       }
     }
@@ -221,7 +225,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
         float ex;
         const float cdf = 0.5f * (1.f + erf_half(r1[j], ex));
         const float pdf = 0.39894228040143268f * ex;
-        dd[j] = pack(rg[j] * r2[j] * (cdf + r1[j] * pdf), rg[j] * r1[j] * cdf);
+        dd[j] = pack((rg[j] * r2[j]) * fmaf(r1[j], pdf, cdf), (rg[j] * r1[j]) * cdf);
       } else {
         dd[j] = r1[j];
       }
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
 #pragma unroll
       for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-        for (int tx = 0; tx < 3; ++tx) s += wf[ty * 3 + tx] * d[ty][u + tx];
+        for (int tx = 0; tx < 3; ++tx) s = __builtin_elementwise_fma(wf[ty * 3 + tx], d[ty][u + tx], s);
       if (o.live && xx < W) {
         float* dst = dy + (o.img0 + (long long)yy * W + xx) * lddy + c;
 #pragma unroll
@@ -261,7 +265,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
 #pragma unroll
       for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-        for (int tx = 0; tx < 3; ++tx) acc[ty * 3 + tx] += dc * x[ty][u + tx];
+        for (int tx = 0; tx < 3; ++tx) acc[ty * 3 + tx] = __builtin_elementwise_fma(dc, x[ty][u + tx], acc[ty * 3 + tx]);
       acc[9] += dc;
     }
 #pragma unroll
@@ -293,6 +297,142 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
     }
 }
 
+// The GDFN backward without a stored yd: yd = dw(y) (+ bias) is recomputed from the layer input y,
+// which the weight gradient reads anyway, so the forward writes only g (1.5 instead of 2.5 KiB per
+// pixel at hid = 127) and the backward reads dg and y (2.5 instead of 3.5 KiB).  The recomputation
+// is the forward's arithmetic (bias, then taps row-major, fused multiply-adds), so yd, and with it
+// every gradient, has the same bits as the stored-yd kernel's.
+// A thread walks its kU columns down the rows with a 4-row x (kU + 4)-column window of y (both
+// halves packed as one float2) and a 3-row x (kU + 2)-column window of dyd: output row yy needs dyd
+// rows yy - 1 .. yy + 1, dyd row r needs yd row r, and yd row r needs y rows r - 1 .. r + 1.
+__global__ __launch_bounds__(256) void dwgate_bwd_rc_kernel(const float* __restrict__ dg, int ldg,
+                                                            const float* __restrict__ yin, int ldi,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ bias, int hid, int H, int W,
+                                                            int tiles_x, int ty, float* __restrict__ dy, int lddy,
+                                                            float* __restrict__ part) {
+  constexpr int NY = kU + 4, ND = kU + 2;
+  __shared__ float red[4][64][20];
+  const Geo o = geo(hid, H, W, tiles_x, ty);
+  const int c = o.c;
+  f2 wv[9];  // forward taps; the transposed conv reads them flipped
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wv[t] = o.live ? f2{w[c * 9 + t], w[(hid + c) * 9 + t]} : f2{0.f, 0.f};
+  const f2 bv = (o.live && bias) ? f2{bias[c], bias[hid + c]} : f2{0.f, 0.f};
+  f2 acc[10];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) acc[t] = f2{0.f, 0.f};
+  // y row yy, columns x0 - 2 .. x0 + kU + 1 (zero outside the image / past the channels)
+  auto load_y = [&](int yy, f2 (&r)[NY]) {
+    const bool oky = o.live && yy >= 0 && yy < H;
+#pragma unroll
+    for (int j = 0; j < NY; ++j) {
+      const int xx = o.x0 - 2 + j;
+      if (oky && xx >= 0 && xx < W) {
+        const float* q = yin + (o.img0 + (long long)yy * W + xx) * ldi + c;
+        r[j] = f2{q[0], q[hid]};
+      } else {
+        r[j] = f2{0.f, 0.f};
+      }
+    }
+  };
+  // dyd row from dg (columns x0 - 1 .. x0 + kU) and the y rows r - 1, r, r + 1: yd as the forward
+  // computed it, then the gate backward (dg = 0 outside the image, so dyd is the transposed conv's
+  // zero padding there)
+  auto row_d = [&](const float (&rg)[ND], const f2 (&ya)[NY], const f2 (&yb)[NY], const f2 (&yc)[NY], f2 (&dd)[ND]) {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      f2 s = bv;
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx) s = __builtin_elementwise_fma(wv[tx], ya[j + tx], s);
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx) s = __builtin_elementwise_fma(wv[3 + tx], yb[j + tx], s);
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx) s = __builtin_elementwise_fma(wv[6 + tx], yc[j + tx], s);
+      float ex;
+      const float cdf = 0.5f * (1.f + erf_half(s.x, ex));
+      const float pdf = 0.39894228040143268f * ex;
+      dd[j] = f2{(rg[j] * s.y) * fmaf(s.x, pdf, cdf), (rg[j] * s.x) * cdf};
+    }
+  };
+  f2 Y[4][NY], D[3][ND];
+  f2 y4[NY];
+  float rg[ND];
+  load_y(o.y0 - 2, y4);
+  load_y(o.y0 - 1, Y[0]);
+  load_y(o.y0, Y[1]);
+  load_y(o.y0 + 1, Y[2]);
+  load_y(o.y0 + 2, Y[3]);
+  load_row(dg, ldg, o, H, W, o.y0 - 1, c, rg);
+  row_d(rg, y4, Y[0], Y[1], D[0]);
+  load_row(dg, ldg, o, H, W, o.y0, c, rg);
+  row_d(rg, Y[0], Y[1], Y[2], D[1]);
+  load_row(dg, ldg, o, H, W, o.y0 + 1, c, rg);
+  row_d(rg, Y[1], Y[2], Y[3], D[2]);
+  // rows yy + 3 (y) and yy + 2 (dg) are in flight during row yy
+  load_y(o.y0 + 3, y4);
+  load_row(dg, ldg, o, H, W, o.y0 + 2, c, rg);
+  for (int yy = o.y0; yy < o.y1; ++yy) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int xx = o.x0 + u;
+      f2 s = f2{0.f, 0.f};
+#pragma unroll
+      for (int ty2 = 0; ty2 < 3; ++ty2)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) s = __builtin_elementwise_fma(wv[8 - (ty2 * 3 + tx)], D[ty2][u + tx], s);
+      if (o.live && xx < W) {
+        float* dst = dy + (o.img0 + (long long)yy * W + xx) * lddy + c;
+        dst[0] = s.x;
+        dst[hid] = s.y;
+      }
+      // weight / bias gradient: centre dyd times the input at each tap (y at column x0 + u + tx - 1)
+      const f2 dc = D[1][u + 1];
+#pragma unroll
+      for (int ty2 = 0; ty2 < 3; ++ty2)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) acc[ty2 * 3 + tx] = __builtin_elementwise_fma(dc, Y[ty2][u + tx + 1], acc[ty2 * 3 + tx]);
+      acc[9] += dc;
+    }
+    if (yy + 1 >= o.y1) break;
+#pragma unroll
+    for (int j = 0; j < NY; ++j) {
+      Y[0][j] = Y[1][j];
+      Y[1][j] = Y[2][j];
+      Y[2][j] = Y[3][j];
+      Y[3][j] = y4[j];
+    }
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      D[0][j] = D[1][j];
+      D[1][j] = D[2][j];
+    }
+    row_d(rg, Y[1], Y[2], Y[3], D[2]);  // dyd row yy + 2
+    load_y(yy + 4, y4);
+    load_row(dg, ldg, o, H, W, yy + 3, c, rg);
+  }
+  const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6;
+#pragma unroll
+  for (int t = 0; t < 10; ++t) {
+    red[wv_][lane][t] = acc[t].x;
+    red[wv_][lane][10 + t] = acc[t].y;
+  }
+  __syncthreads();
+  if (wv_ != 0 || !o.live) return;
+  const int Ctot = 2 * hid;
+  float* pr = part + ((long long)o.b * gridDim.x + blockIdx.x) * 10 * Ctot;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      const float s = ((red[0][lane][h * 10 + t] + red[1][lane][h * 10 + t]) + red[2][lane][h * 10 + t]) +
+                      red[3][lane][h * 10 + t];
+      const int ch = h * hid + c;
+      if (t < 9) pr[ch * 9 + t] = s;
+      else pr[9 * Ctot + ch] = s;
+    }
+}
+
 }  // namespace
 
 int dwg_blocks(int Bn, int H, int W) {
@@ -314,6 +454,14 @@ hipError_t launch_dwgate_bwd(const float* dg, int ldg, const float* yd, int ldyd
   const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
   hipLaunchKernelGGL(dw_bwd_kernel<true>, dim3(tx * nty, (hid + 63) / 64, Bn), dim3(256), 0, s, dg, ldg, yd, ldyd,
                      yin, ldi, w, hid, H, W, tx, ty, dy, lddy, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_dwgate_bwd_rc(const float* dg, int ldg, const float* yin, int ldi, const float* w, const float* b,
+                                int hid, int Bn, int H, int W, float* dy, int lddy, float* part, hipStream_t s) {
+  const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
+  hipLaunchKernelGGL(dwgate_bwd_rc_kernel, dim3(tx * nty, (hid + 63) / 64, Bn), dim3(256), 0, s, dg, ldg, yin, ldi, w, b,
+                     hid, H, W, tx, ty, dy, lddy, part);
   return hipGetLastError();
 }
 

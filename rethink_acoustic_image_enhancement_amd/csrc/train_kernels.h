@@ -75,7 +75,7 @@ hipError_t launch_ln_bwd(const float* dy, int ldd, const float* x, int ldx, cons
 hipError_t launch_dw_fwd(const float* in, int ldi, const float* w, const float* b, int flip, int C, int Bn, int H,
                          int W, float* out, int ldo, hipStream_t s);
 // Fused depthwise kernels (train_dwg.hip).  GDFN forward: yd = dw(y) (+b) over both halves
-// (x1 at [0, hid), x2 at [hid, 2 hid)) and g = gelu_erf(yd1) * yd2.  Backward: dy = dw^T(dyd) and the
+// (x1 at [0, hid), x2 at [hid, 2 hid)) and g = gelu_erf(yd1) * yd2 (yd may be null: not stored).  Backward: dy = dw^T(dyd) and the
 // weight / bias gradient partials part[dwg_blocks][10 C] (C = 2 hid; columns [9 C weights | C biases]),
 // with dyd = gate_bwd(dg, yd) computed on the fly (dwgate) or given (dw_bwd, C channels).
 int dwg_blocks(int Bn, int H, int W);
@@ -84,6 +84,10 @@ hipError_t launch_dwgate_fwd(const float* y, int ldi, const float* w, const floa
 hipError_t launch_dwgate_bwd(const float* dg, int ldg, const float* yd, int ldyd, const float* yin, int ldi,
                              const float* w, int hid, int Bn, int H, int W, float* dy, int lddy, float* part,
                              hipStream_t s);
+// GDFN backward from (dg, y) alone: yd recomputed from y with the forward's arithmetic (same bits as
+// launch_dwgate_bwd given the stored yd); the forward then passes yd = null to launch_dwgate_fwd.
+hipError_t launch_dwgate_bwd_rc(const float* dg, int ldg, const float* yin, int ldi, const float* w, const float* b,
+                                int hid, int Bn, int H, int W, float* dy, int lddy, float* part, hipStream_t s);
 hipError_t launch_dw_bwd(const float* dyd, int ldd, const float* yin, int ldi, const float* w, int C, int Bn, int H,
                          int W, float* dy, int lddy, float* part, hipStream_t s);
 

@@ -369,6 +369,41 @@ def test_side_stream_backward_equals_serial_backward():
             os.environ["KDLAE_DEBUG"] = old
 
 
+@pytest.mark.parametrize("kw,shape", [
+    (dict(LayerNorm_type="BiasFree"), (6, 3, 128, 128)),
+    (dict(dim=16, bias=True, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1), (2, 3, 48, 40)),
+])
+def test_recomputed_yd_backward_equals_stored_yd_backward(kw, shape):
+    """The GDFN backward recomputes the dwconv output yd from its input (dwgate_bwd_rc_kernel) instead
+    of reading the copy the forward stored; the gradient must equal the stored-yd path's
+    (KDLAE_DEBUG=train_keep_yd) bit for bit — with and without the dwconv bias, and on a width that is
+    not a multiple of the kernel's 16-column tile."""
+    m = _model(kw)
+    B, _, H, W = shape
+    img = torch.from_numpy(hash_images("img:rcyd", shape)).to(DEV)
+    rate = torch.full((B, 1, H, W), 0.6, device=DEV)
+    gt = {"hq": img.clamp(0.2, 0.8), "sr": torch.nn.functional.interpolate(img, scale_factor=2).clamp(0.2, 0.8)}
+    tr = KDLAETrainer(m)
+    inp = {"img": img, "denoise_rate": rate}
+    old = os.environ.get("KDLAE_DEBUG")
+    try:
+        os.environ["KDLAE_DEBUG"] = "train_keep_yd"
+        tr.forward_backward(inp, gt)
+        torch.cuda.synchronize()
+        g_keep = tr.grad.clone()
+        os.environ.pop("KDLAE_DEBUG")
+        tr.grad.fill_(float("nan"))
+        tr.forward_backward(inp, gt)
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("KDLAE_DEBUG", None)
+        else:
+            os.environ["KDLAE_DEBUG"] = old
+    assert torch.isfinite(g_keep).all()
+    assert torch.equal(g_keep, tr.grad), float((g_keep - tr.grad).abs().max())
+
+
 def test_engine_rejects_bad_shapes():
     m = _model(dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1))
     eng = TrainEngine(m, torch.device(DEV))

@@ -7,6 +7,7 @@
 #   bench     bench.py with the given args (default: the driver's default run)
 #   prof      rocprofv3 --kernel-trace --stats of the T16 bench and of the training bench
 #   profb     rocprofv3 --kernel-trace --stats of one bench.py run with the given args
+#   probe     a tools/ probe script with args, then the same under rocprofv3 --kernel-trace --stats
 #   pmc_lds   one PMC pass of wave-state + LDS counters over one T16 step
 #   split     tools/stream_split_probe.py (two half-batches on two streams vs one)
 #   pmc       PMC passes over one T16 step: FETCH_SIZE, WRITE_SIZE, busy counters (one group per run)
@@ -62,6 +63,13 @@ profb)  # rocprofv3 kernel trace + stats of one bench.py invocation (args)
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py "$@" > $O/prof_bench.log 2>&1 || exit $?
   tail -2 $O/prof_bench.log
+  ;;
+probe)  # a tools/ probe script (args: script [script args]), then the same under rocprofv3 --kernel-trace --stats
+  timeout -k 10 300 python -u "$@" > $O/probe.txt 2> $O/probe.err || { tail -30 $O/probe.err; exit 1; }
+  cat $O/probe.txt
+  s=$R/$1; shift
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $s "$@" > $O/prof_probe.log 2>&1 || exit $?
   ;;
 pmc)
   cd /tmp && export TMPDIR=/tmp
