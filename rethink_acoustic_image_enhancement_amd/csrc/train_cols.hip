@@ -25,7 +25,7 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kThreads = 256;  // 4 waves
+constexpr int kThreads = 256;  // at most 4 waves
 constexpr int kU = 4;          // k-steps (4 pixels each) per pipeline stage
 
 struct ColsArgs {
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
   const TGemm& g = a.g;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lq = lane >> 4;
-  const int wt = blockIdx.y * 4 + wave;
+  const int wt = blockIdx.y * (int)(blockDim.x >> 6) + wave;
   if (wt >= a.wtm * a.wtn) return;  // wave-uniform; no block barrier below
   const int wm = wt / a.wtn, wn = wt - wm * a.wtn;
   const int z = blockIdx.z, z1 = z / g.nz2, z2 = z - z1 * g.nz2;
@@ -169,21 +169,21 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
     }
 }
 
-// blocks of this variant resident on the whole chip (hipOccupancy..., cached)
+// blocks of this variant and block size (nw waves) resident on the whole chip (hipOccupancy..., cached)
 template <int TM, int TN, bool IMPB>
-int slots() {
-  static int n = 0;
-  if (!n) {
+int slots(int nw) {
+  static int n[5] = {0, 0, 0, 0, 0};
+  if (!n[nw]) {
     int b = 0, dev = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&tgemm_cols_kernel<TM, TN, IMPB>),
-                                                     kThreads, 0) != hipSuccess || b < 1)
+                                                     64 * nw, 0) != hipSuccess || b < 1)
       b = 1;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                  hipSuccess || cus < 1)
       cus = 256;
-    n = b * cus;
+    n[nw] = b * cus;
   }
-  return n;
+  return n[nw];
 }
 
 // split count: whole rounds of resident blocks (r03 sweep: a fixed wave target was up to 40% off
@@ -192,9 +192,12 @@ int slots() {
 #ifndef KDLAE_COLS_MIN
 #define KDLAE_COLS_MIN 256
 #endif
+#ifndef KDLAE_COLS_NARROW
+#define KDLAE_COLS_NARROW 1
+#endif
 template <int TM, int TN, bool IMPB>
-hipError_t launch_tt(TGemm g, ColsArgs a, int gy, long long batch, size_t partial_cap, hipStream_t s) {
-  long long splits = ((long long)slots<TM, TN, IMPB>() + gy * batch - 1) / (gy * batch);
+hipError_t launch_tt(TGemm g, ColsArgs a, int nw, int gy, long long batch, size_t partial_cap, hipStream_t s) {
+  long long splits = ((long long)slots<TM, TN, IMPB>(nw) + gy * batch - 1) / (gy * batch);
   const long long maxs = (g.K + KDLAE_COLS_MIN - 1) / KDLAE_COLS_MIN;
   if (splits > maxs) splits = maxs;
   const long long cap = (long long)(partial_cap / ((size_t)g.M * g.N * batch));
@@ -207,8 +210,8 @@ hipError_t launch_tt(TGemm g, ColsArgs a, int gy, long long batch, size_t partia
   a.splits = (int)splits;
   g.splits = (int)splits;
   a.g = g;
-  hipLaunchKernelGGL((tgemm_cols_kernel<TM, TN, IMPB>), dim3((unsigned)splits, (unsigned)gy, (unsigned)batch), dim3(kThreads),
-                     0, s, a);
+  hipLaunchKernelGGL((tgemm_cols_kernel<TM, TN, IMPB>), dim3((unsigned)splits, (unsigned)gy, (unsigned)batch),
+                     dim3(64 * nw), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_tgemm_reduce(g, s);
@@ -244,16 +247,19 @@ hipError_t launch_tgemm_cols(TGemm g, size_t partial_cap, hipStream_t s) {
   a.wtm = (a.mt + TM - 1) / TM;
   a.wtn = (a.nt + TN - 1) / TN;
   const int wtiles = a.wtm * a.wtn;
-  const int gy = (wtiles + 3) / 4;
+  // waves per block: up to 4 wave tiles of one pixel chunk; fewer wave tiles take smaller blocks
+  // (a 4-wave block with one live wave puts every live wave of the CU on the same SIMD)
+  const int nw = KDLAE_COLS_NARROW ? (wtiles < 4 ? wtiles : 4) : 4;
+  const int gy = (wtiles + nw - 1) / nw;
   const long long batch = (long long)g.nz1 * g.nz2;
   // (bmode 4: N = 27 Cg is 27 * whole 16-tiles, so TN is 3 or 4, or 2 beside TM = 4; no other
   // implicit instance is compiled)
 #define TT(m, n)                                                                                     \
   if (TM == m && TN == n) {                                                                          \
     if constexpr (n != 2 || m == 4)                                                                  \
-      if (g.bmode == 4) return launch_tt<m, n, true>(g, a, gy, batch, partial_cap, s);                \
+      if (g.bmode == 4) return launch_tt<m, n, true>(g, a, nw, gy, batch, partial_cap, s);            \
     if (g.bmode == 4) return hipErrorInvalidValue;                                                    \
-    return launch_tt<m, n, false>(g, a, gy, batch, partial_cap, s);                                   \
+    return launch_tt<m, n, false>(g, a, nw, gy, batch, partial_cap, s);                               \
   }
   TT(2, 2) TT(2, 3) TT(2, 4) TT(3, 2) TT(3, 3) TT(3, 4) TT(4, 2) TT(4, 3)
 #undef TT
