@@ -397,6 +397,31 @@ __device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t r, unsigned of
 }
 constexpr unsigned kOOB = 0x80000000u;  // a byte offset past every descriptor's range
 
+// Block -> (tile block bx, weight group / n-chunk by) of the resident and chunked kernels.  A tile
+// block's A rows are read once per group, so the gy blocks of one tile block are launched as
+// consecutive dispatches on one XCD: 1-D grid, id = s * 8 gy + j * 8 + k -> bx = 8 s + k, by = j
+// (the hardware deals consecutive ids round-robin over the 8 XCDs, so k is the XCD).  They run side
+// by side over the same tiles, and all but the first read of each A tile hit that XCD's L2 instead
+// of HBM (with x-fastest 2-D grids the first ceil(gx / CUs) rounds were all group 0: every group
+// re-read A from HBM).  gy = 1 keeps bx = id.  Ids past gx (the round-up to 8) exit.
+#ifndef KDLAE_GEMM_XCD_PAIR
+#define KDLAE_GEMM_XCD_PAIR 1
+#endif
+__device__ __forceinline__ void block_tile_group(int gy, int& bx, int& by) {
+  if (!KDLAE_GEMM_XCD_PAIR) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    return;
+  }
+  const int id = blockIdx.x, sgrp = id / (8 * gy), r = id - sgrp * 8 * gy;
+  by = r >> 3;
+  bx = sgrp * 8 + (r & 7);
+}
+static dim3 gemm_grid(int grid_x, int grid_y) {
+  if (!KDLAE_GEMM_XCD_PAIR) return dim3(grid_x, grid_y);
+  return dim3((unsigned)(((grid_x + 7) / 8) * 8 * grid_y));
+}
+
 template <int NT, int KG, int NCH, int WPE, bool HASR, bool PF>
 __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
@@ -404,10 +429,12 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lq = lane >> 4;
   const int HW = p.F * p.H * p.W;
-  const int t_begin = blockIdx.x * p.tiles_per_block;
+  int bx, by;
+  block_tile_group((p.ntiles + p.group_tiles - 1) / p.group_tiles, bx, by);
+  const int t_begin = bx * p.tiles_per_block;
   const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
   if (t_begin >= t_end) return;
-  const int g0 = blockIdx.y * p.group_tiles;
+  const int g0 = by * p.group_tiles;
   const int gtiles = min(p.group_tiles, p.ntiles - g0);
   constexpr int TP = NT * NCH;  // tiles staged per group (zero weights past gtiles)
   // weights are per image when w_img_stride != 0 (the MDTA-folded projection M = W_proj blockdiag(A))
@@ -780,10 +807,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lq = lane >> 4;
   const int HW = p.F * p.H * p.W;
-  const int t_begin = blockIdx.x * p.tiles_per_block;
+  int bx, nc;
+  block_tile_group((p.ntiles + NT - 1) / NT, bx, nc);
+  const int t_begin = bx * p.tiles_per_block;
   const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
   if (t_begin >= t_end) return;
-  const int nc = blockIdx.y;
   const int KC = p.kchunks;
   f32x4* bias_l = wlds + 2 * SLOT;
   for (int idx = tid; idx < NT * 4; idx += kGemmThreads) {
@@ -1028,12 +1056,14 @@ static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_
   }
   if constexpr (RK) {
     if (p.R) {
-      hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, true, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+      hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, true, PF>), gemm_grid(grid_x, grid_y), dim3(kGemmThreads), lds, s,
+                         p);
       return hipGetLastError();
     }
   }
   if (p.R) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, false, PF>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+  hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, false, PF>), gemm_grid(grid_x, grid_y), dim3(kGemmThreads), lds, s,
+                     p);
   return hipGetLastError();
 }
 
@@ -1084,11 +1114,12 @@ static hipError_t launch_chunk2(const GemmParams& p, int grid_x, int grid_y, hip
     attr_lds[dev] = lds;
   }
   if (R0 && p.R)
-    hipLaunchKernelGGL((gemm_chunk_kernel<NT, KG, C3, OUT, R0>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+    hipLaunchKernelGGL((gemm_chunk_kernel<NT, KG, C3, OUT, R0>), gemm_grid(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
   else if (OUT == 0 && p.R)
     return hipErrorInvalidValue;  // (no residual variant: the host picks another NT x KG)
   else
-    hipLaunchKernelGGL((gemm_chunk_kernel<NT, KG, C3, OUT, false>), dim3(grid_x, grid_y), dim3(kGemmThreads), lds, s, p);
+    hipLaunchKernelGGL((gemm_chunk_kernel<NT, KG, C3, OUT, false>), gemm_grid(grid_x, grid_y), dim3(kGemmThreads), lds, s,
+                       p);
   return hipGetLastError();
 }
 
