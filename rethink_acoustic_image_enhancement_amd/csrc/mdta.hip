@@ -413,6 +413,9 @@ struct GramRing {
   static constexpr int PPD = (Pieces + NDW - 1) / NDW;  // pieces per DMA wave per row
 };
 
+#ifndef KDLAE_RING_XCD
+#define KDLAE_RING_XCD 1
+#endif
 template <int CT>
 __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_kernel(GramParams p, int seg_rows) {
   using R = GramRing<CT>;
@@ -432,7 +435,11 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, lq = lane >> 4;
   const int strips = p.W >> 4;
-  const int slot = blockIdx.x;
+  // XCD-aware slot order: XCD k (blockIdx.x & 7; nslots % 8 == 0 keeps the 3-D grid's linear ids
+  // congruent) walks the slot range [k n / 8, (k+1) n / 8), so neighbouring strips, whose 2 halo
+  // columns overlap, are read on the same L2 at about the same time
+  const int slot = (KDLAE_RING_XCD && p.nslots % 8 == 0)
+                       ? (int)(blockIdx.x & 7) * (p.nslots >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   const int strip = slot % strips, seg = slot / strips;
   const int h = blockIdx.y, b = blockIdx.z;
   const int HW = p.H * p.W;
