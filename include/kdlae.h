@@ -21,8 +21,9 @@
  * results.  KDLAE_DEBUG (comma-separated flags, read when a KDLAE-T handle
  * builds its pack program: kdlae_t_prepare or the first pack) selects between kernel schedules that produce
  * the same bits: "no_attn_in_fusion" keeps the attention-output GEMM and the
- * LN + ffn.project_in GEMM separate for C = 48 blocks; "attn_in_split" fuses
- * the C = 96 blocks' first project_in weight group as well; "ffn48" runs the
+ * LN + ffn.project_in GEMM separate (every block); "no_attn_in_split" keeps
+ * them separate for the C = 96 blocks only (by default their first
+ * project_in weight group is fused as well); "ffn48" runs the
  * C = 48 blocks' FFN half as one kernel (x1, LN, project_in on the tile halo,
  * dwconv + gate, project_out) writing each block's output to a ping-pong
  * buffer, instead of gemm_attn_in + gdfn_out (measured slower at 512^2 and

@@ -352,10 +352,11 @@ struct Packer {
     const bool no_ai = debug_flag("no_attn_in_fusion");
     b.fused_attn_in = b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 && b.pin.WPE == 2 &&
                       gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.ntiles + b.pin.NT - 1) / b.pin.NT) && !no_ai;
-    // C = 96 (two weight groups): the fused kernel on group 0 + a plain LN GEMM on group 1 measured a
-    // wash (profiles/r02_attn_in_probe.txt: 4637 vs 4598 us at 512^2), so it stays behind the
-    // attn_in_split debug flag (bit-identity test)
-    if (!b.fused_attn_in && !no_ai && debug_flag("attn_in_split") && b.pin.group_tiles > 0 &&
+    // C = 96 (two weight groups): the fused kernel on group 0 + a plain LN GEMM on group 1.  A wash in
+    // r02 (profiles/r02_attn_in_probe.txt); since r04's fused-kernel waitcnt fix and XCD-paired GEMM
+    // order -4.2% at 512^2 and -2.7% at 256^2 per block (profiles/r04k_attn_in_split_ab_probe.txt), so on
+    // by default; debug flag no_attn_in_split keeps the unfused pair (bit-identity test)
+    if (!b.fused_attn_in && !no_ai && !debug_flag("no_attn_in_split") && b.pin.group_tiles > 0 &&
         b.pin.group_tiles < b.pin.ntiles && 2 * b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 &&
         b.pin.WPE == 2 && gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.group_tiles + b.pin.NT - 1) / b.pin.NT)) {
       const int gt = b.pin.group_tiles;

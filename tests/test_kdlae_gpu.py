@@ -152,16 +152,17 @@ def test_batch_invariance_and_determinism():
     assert torch.equal(full["hq"][1:2], one["hq"]) and torch.equal(full["sr"][1:2], one["sr"])
 
 
-@pytest.mark.parametrize("ln,split", [("BiasFree", False), ("WithBias", False), ("BiasFree", True)])
+@pytest.mark.parametrize("ln,split", [("BiasFree", False), ("WithBias", False), ("BiasFree", True), ("WithBias", True)])
 def test_fused_attention_input_equals_unfused_bit_for_bit(ln, split, monkeypatch):
-    """gemm_attn_in_kernel (x1 = x + M v, LN, project_in in one pass: the C = 48 blocks; with
-    KDLAE_DEBUG=attn_in_split also the C = 96 blocks' first project_in weight group) gives the same bits as
-    the separate attention-output GEMM + LN/project_in GEMM it replaces."""
+    """gemm_attn_in_kernel (x1 = x + M v, LN, project_in in one pass: the C = 48 blocks, and by default
+    the C = 96 blocks' first project_in weight group) gives the same bits as the separate
+    attention-output GEMM + LN/project_in GEMM it replaces (split=False: the C = 96 blocks unfused,
+    KDLAE_DEBUG=no_attn_in_split)."""
     kw = dict(dim=48, LayerNorm_type=ln, num_blocks=[2, 1, 1, 1], num_refinement_blocks=1, bias=ln == "WithBias")
     img = torch.from_numpy(hash_images("fai", (2, 3, 64, 80)))
     rate = torch.from_numpy(hash_images("fair", (2, 1, 64, 80)))
-    if split:
-        monkeypatch.setenv("KDLAE_DEBUG", "attn_in_split")
+    if not split:
+        monkeypatch.setenv("KDLAE_DEBUG", "no_attn_in_split")
     fused = _run(_model(kw), img, rate)
     monkeypatch.setenv("KDLAE_DEBUG", "no_attn_in_fusion")  # read when a new handle builds its blocks
     unfused = _run(_model(kw), img, rate)
