@@ -93,7 +93,10 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
 #ifndef KDLAE_NPEN_1X1
 #define KDLAE_NPEN_1X1 0.06
 #endif
-      const double npen = g.ksize == 3 ? 0.12 : KDLAE_NPEN_1X1;
+#ifndef KDLAE_NPEN_3X3
+#define KDLAE_NPEN_3X3 0.12
+#endif
+      const double npen = g.ksize == 3 ? KDLAE_NPEN_3X3 : KDLAE_NPEN_1X1;
 #ifndef KDLAE_KPEN_1X1
 #define KDLAE_KPEN_1X1 0.02
 #endif
