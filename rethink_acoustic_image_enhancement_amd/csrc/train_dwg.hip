@@ -22,6 +22,8 @@
 // over spatial blocks in fixed order by part_reduce: deterministic.
 #include <math.h>
 
+#include <algorithm>
+
 #include "train_kernels.h"
 
 namespace kdlae {
@@ -92,15 +94,37 @@ __device__ __forceinline__ Geo geo(int C, int H, int W, int tiles_x, int ty) {
   return o;
 }
 
+// Image-relative buffer accesses: a descriptor per (tensor, image) (uniform), a row offset per row
+// (uniform) plus a loop-invariant column offset per lane, instead of a 64-bit address per element
+// (the flat form spent ~4 VALU address instructions per load).  Out-of-image rows / columns and
+// channels past C take kOOBU, one "out of range" unit: a row and a column unit together stay below
+// 2^32 and past every image's byte count (< kOOBU, checked by the launchers), so the hardware
+// returns the conv's zero padding on loads and drops stores.
+constexpr unsigned kOOBU = 0x40000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const float* p, int ld, const Geo& o, int H, int W) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p + o.img0 * ld), 0, H * W * ld * 4, 0x00020000);
+}
+__device__ __forceinline__ unsigned row_off(int yy, int H, int W, int ld) {
+  return (yy >= 0 && yy < H) ? (unsigned)(yy * W) * (unsigned)ld * 4u : kOOBU;
+}
+__device__ __forceinline__ unsigned col_off(const Geo& o, int xx, int W, int ld, int off) {
+  return (o.live && xx >= 0 && xx < W) ? ((unsigned)xx * (unsigned)ld + (unsigned)off) * 4u : kOOBU;
+}
+__device__ __forceinline__ float ld_img(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void st_img(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
+}
+bool img_bytes_ok(int H, int W, int ld) { return (long long)H * W * ld * 4 < (long long)kOOBU; }
+
 // row yy, columns x0 - 1 .. x0 + kU of channel off (zero outside the image / past the channels)
 __device__ __forceinline__ void load_row(const float* __restrict__ p, int ld, const Geo& o, int H, int W, int yy,
                                          int off, float (&r)[kU + 2]) {
-  const bool oky = o.live && yy >= 0 && yy < H;
+  const __amdgpu_buffer_rsrc_t rs = img_rsrc(p, ld, o, H, W);
+  const unsigned ro = row_off(yy, H, W, ld);
 #pragma unroll
-  for (int j = 0; j < kU + 2; ++j) {
-    const int xx = o.x0 - 1 + j;
-    r[j] = (oky && xx >= 0 && xx < W) ? p[(o.img0 + (long long)yy * W + xx) * ld + off] : 0.f;
-  }
+  for (int j = 0; j < kU + 2; ++j) r[j] = ld_img(rs, col_off(o, o.x0 - 1 + j, W, ld, off) + ro);
 }
 
 __global__ __launch_bounds__(256) void dwgate_fwd_kernel(const float* __restrict__ y, int ldi,
@@ -117,6 +141,8 @@ __global__ __launch_bounds__(256) void dwgate_fwd_kernel(const float* __restrict
     w2[t] = o.live ? w[(hid + c) * 9 + t] : 0.f;
   }
   const float b1 = (o.live && bias) ? bias[c] : 0.f, b2 = (o.live && bias) ? bias[hid + c] : 0.f;
+  const __amdgpu_buffer_rsrc_t rg = img_rsrc(g, ldg, o, H, W);
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t ryd = img_rsrc(yd ? yd : g, yd ? ldyd : ldg, o, H, W);
   float a[3][kU + 2], v[3][kU + 2];  // rows y-1, y, y+1 of halves 1 and 2
   load_row(y, ldi, o, H, W, o.y0 - 1, c, a[0]);
   load_row(y, ldi, o, H, W, o.y0, c, a[1]);
@@ -151,14 +177,12 @@ __global__ __launch_bounds__(256) void dwgate_fwd_kernel(const float* __restrict
           s2 = fmaf(w2[ty * 3 + tx], v[ty][u + tx], s2);
         }
       const int xx = o.x0 + u;
-      if (o.live && xx < W) {
-        const long long p = o.img0 + (long long)yy * W + xx;
-        if (yd) {  // (null: the backward recomputes yd, dwgate_bwd_rc_kernel)
-          yd[p * ldyd + c] = s1;
-          yd[p * ldyd + hid + c] = s2;
-        }
-        g[p * ldg + c] = gelu_erf(s1) * s2;
+      if (yd) {  // (null: the backward recomputes yd, dwgate_bwd_rc_kernel)
+        const unsigned ro = row_off(yy, H, W, ldyd);
+        st_img(ryd, col_off(o, xx, W, ldyd, c) + ro, s1);
+        st_img(ryd, col_off(o, xx, W, ldyd, hid + c) + ro, s2);
       }
+      st_img(rg, col_off(o, xx, W, ldg, c) + row_off(yy, H, W, ldg), gelu_erf(s1) * s2);
     }
 #pragma unroll
     for (int j = 0; j < kU + 2; ++j) {
@@ -198,6 +222,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
     if constexpr (GATE) return f2{a, b};
     else return a;
   };
+  const __amdgpu_buffer_rsrc_t rdy = img_rsrc(dy, lddy, o, H, W);
   T wf[9];  // flipped taps (the transposed conv)
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -255,10 +280,10 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(const float* __restrict__ d
       for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
         for (int tx = 0; tx < 3; ++tx) s = __builtin_elementwise_fma(wf[ty * 3 + tx], d[ty][u + tx], s);
-      if (o.live && xx < W) {
-        float* dst = dy + (o.img0 + (long long)yy * W + xx) * lddy + c;
+      {
+        const unsigned ro = row_off(yy, H, W, lddy);
 #pragma unroll
-        for (int h = 0; h < NH; ++h) dst[h * hid] = comp(s, h);
+        for (int h = 0; h < NH; ++h) st_img(rdy, col_off(o, xx, W, lddy, h * hid + c) + ro, comp(s, h));
       }
       // weight / bias gradient: centre dyd times the input at each tap (zero past the image)
       const T dc = d[1][u + 1];
@@ -323,17 +348,13 @@ __global__ __launch_bounds__(256) void dwgate_bwd_rc_kernel(const float* __restr
 #pragma unroll
   for (int t = 0; t < 10; ++t) acc[t] = f2{0.f, 0.f};
   // y row yy, columns x0 - 2 .. x0 + kU + 1 (zero outside the image / past the channels)
+  const __amdgpu_buffer_rsrc_t ryin = img_rsrc(yin, ldi, o, H, W), rdy = img_rsrc(dy, lddy, o, H, W);
   auto load_y = [&](int yy, f2 (&r)[NY]) {
-    const bool oky = o.live && yy >= 0 && yy < H;
+    const unsigned ro = row_off(yy, H, W, ldi);
 #pragma unroll
     for (int j = 0; j < NY; ++j) {
       const int xx = o.x0 - 2 + j;
-      if (oky && xx >= 0 && xx < W) {
-        const float* q = yin + (o.img0 + (long long)yy * W + xx) * ldi + c;
-        r[j] = f2{q[0], q[hid]};
-      } else {
-        r[j] = f2{0.f, 0.f};
-      }
+      r[j] = f2{ld_img(ryin, col_off(o, xx, W, ldi, c) + ro), ld_img(ryin, col_off(o, xx, W, ldi, hid + c) + ro)};
     }
   };
   // dyd row from dg (columns x0 - 1 .. x0 + kU) and the y rows r - 1, r, r + 1: yd as the forward
@@ -381,10 +402,10 @@ __global__ __launch_bounds__(256) void dwgate_bwd_rc_kernel(const float* __restr
       for (int ty2 = 0; ty2 < 3; ++ty2)
 #pragma unroll
         for (int tx = 0; tx < 3; ++tx) s = __builtin_elementwise_fma(wv[8 - (ty2 * 3 + tx)], D[ty2][u + tx], s);
-      if (o.live && xx < W) {
-        float* dst = dy + (o.img0 + (long long)yy * W + xx) * lddy + c;
-        dst[0] = s.x;
-        dst[hid] = s.y;
+      {
+        const unsigned ro = row_off(yy, H, W, lddy);
+        st_img(rdy, col_off(o, xx, W, lddy, c) + ro, s.x);
+        st_img(rdy, col_off(o, xx, W, lddy, hid + c) + ro, s.y);
       }
       // weight / bias gradient: centre dyd times the input at each tap (y at column x0 + u + tx - 1)
       const f2 dc = D[1][u + 1];
@@ -442,6 +463,7 @@ int dwg_blocks(int Bn, int H, int W) {
 
 hipError_t launch_dwgate_fwd(const float* y, int ldi, const float* w, const float* b, int hid, int Bn, int H, int W,
                              float* yd, int ldyd, float* g, int ldg, hipStream_t s) {
+  if (!img_bytes_ok(H, W, std::max(ldi, std::max(ldyd, ldg)))) return hipErrorInvalidValue;
   const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
   hipLaunchKernelGGL(dwgate_fwd_kernel, dim3(tx * nty, (hid + 63) / 64, Bn), dim3(256), 0, s, y, ldi, w, b, hid, H, W,
                      tx, ty, yd, ldyd, g, ldg);
@@ -451,6 +473,7 @@ hipError_t launch_dwgate_fwd(const float* y, int ldi, const float* w, const floa
 hipError_t launch_dwgate_bwd(const float* dg, int ldg, const float* yd, int ldyd, const float* yin, int ldi,
                              const float* w, int hid, int Bn, int H, int W, float* dy, int lddy, float* part,
                              hipStream_t s) {
+  if (!img_bytes_ok(H, W, std::max(std::max(ldg, ldyd), std::max(ldi, lddy)))) return hipErrorInvalidValue;
   const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
   hipLaunchKernelGGL(dw_bwd_kernel<true>, dim3(tx * nty, (hid + 63) / 64, Bn), dim3(256), 0, s, dg, ldg, yd, ldyd,
                      yin, ldi, w, hid, H, W, tx, ty, dy, lddy, part);
@@ -459,6 +482,7 @@ hipError_t launch_dwgate_bwd(const float* dg, int ldg, const float* yd, int ldyd
 
 hipError_t launch_dwgate_bwd_rc(const float* dg, int ldg, const float* yin, int ldi, const float* w, const float* b,
                                 int hid, int Bn, int H, int W, float* dy, int lddy, float* part, hipStream_t s) {
+  if (!img_bytes_ok(H, W, std::max(ldg, std::max(ldi, lddy)))) return hipErrorInvalidValue;
   const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
   hipLaunchKernelGGL(dwgate_bwd_rc_kernel, dim3(tx * nty, (hid + 63) / 64, Bn), dim3(256), 0, s, dg, ldg, yin, ldi, w, b,
                      hid, H, W, tx, ty, dy, lddy, part);
@@ -467,6 +491,7 @@ hipError_t launch_dwgate_bwd_rc(const float* dg, int ldg, const float* yin, int 
 
 hipError_t launch_dw_bwd(const float* dyd, int ldd, const float* yin, int ldi, const float* w, int C, int Bn, int H,
                          int W, float* dy, int lddy, float* part, hipStream_t s) {
+  if (!img_bytes_ok(H, W, std::max(ldd, std::max(ldi, lddy)))) return hipErrorInvalidValue;
   const int ty = rows_per_block(Bn, H, W), tx = (W + kTX - 1) / kTX, nty = (H + ty - 1) / ty;
   hipLaunchKernelGGL(dw_bwd_kernel<false>, dim3(tx * nty, (C + 63) / 64, Bn), dim3(256), 0, s, nullptr, 0, dyd, ldd,
                      yin, ldi, w, C, H, W, tx, ty, dy, lddy, part);
