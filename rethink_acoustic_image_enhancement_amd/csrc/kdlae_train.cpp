@@ -412,8 +412,14 @@ int gemm(Ctx& c, const tr::TGemm& g0, size_t cap, const std::string& what) {
   return KDLAE_OK;
 }
 
-int nblk_for(long long rows, long long ncols, int maxb = 1024) {
-  long long nb = rows / 128;
+#ifndef KDLAE_LN_BWD_MAXB
+#define KDLAE_LN_BWD_MAXB 4096
+#endif
+#ifndef KDLAE_LN_BWD_ROWS
+#define KDLAE_LN_BWD_ROWS 32
+#endif
+int nblk_for(long long rows, long long ncols, int maxb = 1024, int rows_per_blk = 128) {
+  long long nb = rows / rows_per_blk;
   if (nb > maxb) nb = maxb;
   const long long cap = (long long)(kRedCap / (size_t)(ncols > 0 ? ncols : 1));
   if (nb > cap) nb = cap;
@@ -691,7 +697,9 @@ int ln_bwd(Ctx& c, const float* dy, const float* x, const float* st, int C, long
            const float* R, float* dx) {
   const int bf = c.h->cfg.layernorm_biasfree;
   const int ncol = bf ? C : 2 * C;
-  const int nb = nblk_for(P, ncol);
+  // 32 pixels per block (8 per wave: one or two steps of the lane-group loop, whose loads are used
+  // right away, so the kernel is latency-bound and wants many waves in flight), up to 4096 blocks
+  const int nb = nblk_for(P, ncol, KDLAE_LN_BWD_MAXB, KDLAE_LN_BWD_ROWS);
   float* part = red_take(c, (size_t)nb * ncol);
   if (!part) return c.red_err;
   LAUNCH(tr::launch_ln_bwd(dy, C, x, C, c.W(n + ".weight"), st, C, P, bf, R, C, dx, C, part, nb, c.s));
