@@ -413,7 +413,7 @@ int gemm(Ctx& c, const tr::TGemm& g0, size_t cap, const std::string& what) {
 }
 
 #ifndef KDLAE_LN_BWD_MAXB
-#define KDLAE_LN_BWD_MAXB 4096
+#define KDLAE_LN_BWD_MAXB 2048
 #endif
 #ifndef KDLAE_LN_BWD_ROWS
 #define KDLAE_LN_BWD_ROWS 32
@@ -698,7 +698,7 @@ int ln_bwd(Ctx& c, const float* dy, const float* x, const float* st, int C, long
   const int bf = c.h->cfg.layernorm_biasfree;
   const int ncol = bf ? C : 2 * C;
   // 32 pixels per block (8 per wave: one or two steps of the lane-group loop, whose loads are used
-  // right away, so the kernel is latency-bound and wants many waves in flight), up to 4096 blocks
+  // right away, so the kernel is latency-bound and wants many waves in flight), up to 2048 blocks
   const int nb = nblk_for(P, ncol, KDLAE_LN_BWD_MAXB, KDLAE_LN_BWD_ROWS);
   float* part = red_take(c, (size_t)nb * ncol);
   if (!part) return c.red_err;
