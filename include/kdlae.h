@@ -44,7 +44,10 @@
  * results either way.  "train_keep_yd" (read by kdlae_tt_forward; the backward
  * follows what the forward kept) stores the GDFN dwconv output for the
  * backward instead of having the backward recompute it from its input (A/B
- * only: same gradients bit for bit, 1 KiB per pixel more traffic each way).
+ * only: same gradients bit for bit, 1 KiB per pixel more traffic each way);
+ * "train_w3_raw" (read on every training call) has the 3x3 convs' implicit
+ * GEMMs read the OIHW weights directly instead of a per-call [9 Cin][Cout]
+ * repack (A/B only: same bits).
  */
 #ifndef KDLAE_H_
 #define KDLAE_H_

@@ -543,6 +543,20 @@ int conv3_narrow(Ctx& c, const float* w, const float* bias, V in, int Cin, int C
   return KDLAE_OK;
 }
 
+// the implicit-GEMM 3x3 conv's B operand repacked from the OIHW weights into a [9 Cg][N] matrix in the
+// workspace (bmode 2 / 3 -> 0): float4 B loads in the tiled kernel instead of per-element index math
+// (KDLAE_DEBUG=train_w3_raw keeps the OIHW operand; same bits)
+int pack_w3(Ctx& c, tr::TGemm& g, int N) {
+  if (kdlae::debug_flag("train_w3_raw") || N % 4) return KDLAE_OK;
+  float* wp = c.alloc((size_t)9 * g.Cg * N);
+  LAUNCH(tr::launch_pack_w3(g.B, g.Cg, N, g.bmode, wp, c.s));
+  g.B = wp;
+  g.bmode = 0;
+  g.sbk = N;
+  g.sbn = 1;
+  return KDLAE_OK;
+}
+
 int conv3(Ctx& c, const std::string& n, V x, int Cin, int Cout, int Bn, int H, int W, int dil, V out,
           const float* R = nullptr, int ldr = 0) {
   int done = 0;
@@ -551,6 +565,7 @@ int conv3(Ctx& c, const std::string& n, V x, int Cin, int Cout, int Bn, int H, i
   tr::TGemm g;
   g.A = x.p; g.amode = 1; g.lda = x.ld; g.Cg = Cin;
   g.B = c.W(n + ".weight"); g.bmode = 2;
+  TRY(pack_w3(c, g, Cout));
   g.C = out.p; g.scm = out.ld; g.scn = 1;
   g.bias = c.W(n + ".bias");
   g.R = R; g.srm = ldr; g.srn = 1;
@@ -597,6 +612,7 @@ int conv3_bwd(Ctx& c, const std::string& n, V x, V dy, int Cin, int Cout, int Bn
     tr::TGemm d;  // transposed conv: flipped taps, channels swapped
     d.A = dy.p; d.amode = 1; d.lda = dy.ld; d.Cg = Cout;
     d.B = c.W(n + ".weight"); d.bmode = 3;
+    TRY(pack_w3(c, d, Cin));
     d.C = dx.p; d.scm = dx.ld; d.scn = 1;
     d.R = R; d.srm = ldr; d.srn = 1;
     d.M = (int)P; d.N = Cin; d.K = 9 * Cout;

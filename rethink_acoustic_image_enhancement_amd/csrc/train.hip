@@ -618,6 +618,7 @@ hipError_t launch_tgemm_tiled(TGemm g, size_t partial_cap, hipStream_t s) {
   }
   // (the conv weight gradient's M = C_out never reaches 512 tiles of 128 rows: 64-row tiles only)
   else if (g.amode == 0 && g.bmode == 1) hipLaunchKernelGGL((tgemm_kernel<0, 1, 1>), grid, dim3(256), 0, s, g, kchunk, flags);
+  else if (g.amode == 1 && g.bmode == 0) launch_t<1, 0>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 2) launch_t<1, 2>(g, kchunk, flags, rm, grid, s);
   else if (g.amode == 1 && g.bmode == 3) launch_t<1, 3>(g, kchunk, flags, rm, grid, s);
   else return hipErrorInvalidValue;
@@ -1475,6 +1476,26 @@ hipError_t launch_shuffle(const float* in, int ldi, float* out, int ldo, int C, 
   const long long total = (long long)Bn * h * w * C * 4;
   hipLaunchKernelGGL(shuffle_kernel, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, in, ldi, out, ldo, C, Bn, h, w,
                      dir);
+  return hipGetLastError();
+}
+
+// 3x3 conv weights (OIHW) -> the implicit-GEMM B operand as a plain [K = 9 Cg][N] row-major matrix
+// (mode 2: B(k = t Cg + c, n) = W[n][c][t], the conv; mode 3: W[c][n][8 - t], the transposed conv):
+// the tiled kernel then reads B as float4 runs instead of one index computation (k / Cg) and one
+// stride-9 load per element.  Same values, so the same sums.
+__global__ __launch_bounds__(256) void pack_w3_kernel(const float* __restrict__ W, int Cg, int N, int mode,
+                                                      float* __restrict__ out) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x, tot = 9LL * Cg * N;
+  if (idx >= tot) return;
+  const int k = (int)(idx / N), n = (int)(idx - (long long)k * N);
+  const int t = k / Cg, c = k - t * Cg;
+  out[idx] = mode == 2 ? W[((long long)n * Cg + c) * 9 + t] : W[((long long)c * N + n) * 9 + (8 - t)];
+}
+
+hipError_t launch_pack_w3(const float* W, int Cg, int N, int mode, float* out, hipStream_t s) {
+  if ((mode != 2 && mode != 3) || Cg <= 0 || N <= 0) return hipErrorInvalidValue;
+  const long long tot = 9LL * Cg * N;
+  hipLaunchKernelGGL(pack_w3_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, W, Cg, N, mode, out);
   return hipGetLastError();
 }
 

@@ -135,6 +135,9 @@ hipError_t launch_attn_bwd(const float* G, const float* sumsq, const float* temp
 // h, w are the low-resolution sizes, C the low-channel count.
 hipError_t launch_shuffle(const float* in, int ldi, float* out, int ldo, int C, int Bn, int h, int w, int dir,
                           hipStream_t s);
+// 3x3 weights OIHW -> [9 Cg][N] row-major implicit-GEMM B operand (mode 2: conv, B(t Cg + c, n) =
+// W[n][c][t]; mode 3: transposed conv, W[c][n][8 - t]); then TGemm bmode 0 with sbk = N, sbn = 1
+hipError_t launch_pack_w3(const float* W, int Cg, int N, int mode, float* out, hipStream_t s);
 // out[p, 0:C] (= or +=) in[p, 0:C]; zero_to > C also zeroes out[p, C:zero_to] (a padded copy)
 hipError_t launch_copy_cols(const float* in, int ldi, float* out, int ldo, int C, long long P, int accumulate,
                             hipStream_t s, int zero_to = 0);
