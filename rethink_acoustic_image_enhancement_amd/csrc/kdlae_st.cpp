@@ -68,6 +68,7 @@ struct SPlanT {
   std::vector<size_t> ea, e, pool, ua, da, dd, dl, gskip;  // per level / decoder
   std::unordered_map<std::string, size_t> xcol;            // each Conv3d's forward column matrix
   size_t fa = 0, fo = 0, col = 0, gA = 0, gB = 0, partial = 0, part = 0, wp = 0, dwp = 0, wpk = 0, zb = 0;
+  long long col2im_max = 0;  // the largest P * cin a col2im gathers (its element index is 32-bit)
   size_t take(long long floats) {
     const size_t o = total;
     total += ((size_t)floats * 4 + 255) / 256 * 256;
@@ -139,7 +140,10 @@ SPlanT make_plan(const kdlae_st_handle* h, int B, int F, int H, int W) {
   for (int i = 0; i < L; ++i) colmax = std::max(colmax, npx(h, i, B, F, H, W) * h->hc[i]);
   for (auto& [name, ci, co, lvl] : convs) {
     const long long P = npx(h, lvl, B, F, H, W);
-    if (!dx_direct(ci, co)) colmax = std::max(colmax, P * 27 * ci);
+    if (!dx_direct(ci, co)) {
+      colmax = std::max(colmax, P * 27 * ci);
+      pl.col2im_max = std::max(pl.col2im_max, P * ci);
+    }
     if (!conv_direct(ci, co, W >> lvl)) pl.xcol[name] = pl.take(P * 27 * ci);
   }
   pl.col = pl.take(colmax);
@@ -535,8 +539,11 @@ int kdlae_st_forward(kdlae_st_handle* h, const float* theta, const float* x, int
   Ctx c{h, theta, nullptr, reinterpret_cast<char*>(workspace), make_plan(h, B, F, H, W), (hipStream_t)stream,
         B, F, H, W};
   if ((int64_t)c.pl.total > workspace_bytes) return fail(KDLAE_ESTATE, "training workspace too small");
-  if ((long long)B * F * H * W * 27 * 512 >= (1LL << 31) * 4)
-    return fail(KDLAE_EINVAL_SHAPE, "batch too large for the column matrix");
+  // the 32-bit limits that apply: the GEMMs' M / K (pixel counts) are int, and so is col2im's element
+  // index (P * cin) for the convs whose input gradient goes through columns; im2col, the column
+  // matrices and the pixel-reduction kernel index in 64 bits (or fall back to the tiled GEMM)
+  if ((long long)B * F * H * W >= (1LL << 31) || c.pl.col2im_max >= (1LL << 31))
+    return fail(KDLAE_EINVAL_SHAPE, "batch too large: B*F*H*W and P*cin of a column-gradient conv must be < 2^31");
   DeviceGuard dg(h->device);
   h->valid = false;
   TRY(net_fwd(c, x, out));

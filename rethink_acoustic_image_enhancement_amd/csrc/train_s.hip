@@ -169,7 +169,8 @@ __global__ __launch_bounds__(kThreads) void relu_mask_kernel(float* __restrict__
 }
 
 // MaxPool3d (1,2,2) backward (KDLAE_model.py:366): each pooled element's gradient goes to the first
-// maximal input of its 2 x 2 window in (row, column) order — PyTorch's tie rule (ReLU zeros tie often);
+// maximal input of its 2 x 2 window in (row, column) order — PyTorch's tie rule (ReLU zeros tie often) —
+// or to the last NaN of the window (PyTorch's `val > max || isnan(val)`);
 // din = dskip (the same tensor's gradient through the decoder's skip add, or 0) + that routed gradient.
 __global__ __launch_bounds__(kThreads) void maxpool2_bwd_kernel(const float* __restrict__ in, int ldi,
                                                                 const float* __restrict__ dout, int ldo,
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void maxpool2_bwd_kernel(const float* __r
 #pragma unroll
     for (int j = 1; j < 4; ++j) {
       const float v = in[ps[j] * ldi + c];
-      if (v > mx || (v != v && mx == mx)) {
+      if (v > mx || v != v) {
         mx = v;
         am = j;
       }

@@ -433,7 +433,10 @@ class KDLAESTrainer:
         out = eng.forward(self.theta, lq)
         self.output = out
         dout = torch.empty_like(out)
-        gt = gt.to(torch.float32).contiguous()
+        # the same device move as _L1FramesFn: the loss kernel dereferences gt on the GPU
+        gt = gt.to(device=out.device, dtype=torch.float32).contiguous()
+        if gt.shape != out.shape:
+            raise ValueError(f"gt shape {tuple(gt.shape)} != output shape {tuple(out.shape)}")
         N, Cf = out.shape[0], out.shape[1]
         lf = self.loss_fn
         if lf.reduction not in ("mean", "sum"):

@@ -147,6 +147,40 @@ def test_side_stream_backward_equals_serial_backward():
     assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
 
 
+@pytest.mark.parametrize("hw", [192, 384])
+def test_progressive_patch_sizes_train(hw):
+    """KDLAES.yml's progressive patches (gt_sizes up to 384, batch 4, 7 frames; train.py:381-418): one
+    step must run (finite loss and gradients) and the side-stream backward must equal the one-stream one
+    bit for bit.  r04 refused every batch above ~621k pixels through a hard-coded column-matrix guard."""
+    m = _model(dict(residual=True, hidden_channels=[16, 32, 64]))
+    x = torch.from_numpy(hash_images(f"pp_x{hw}", (4, 7, hw, hw))).to(DEV)
+    tgt = torch.from_numpy(hash_images(f"pp_t{hw}", (4, 7, hw, hw)))  # on the host: the trainer moves it
+    old = os.environ.get("KDLAE_DEBUG")
+    grads, losses = [], []
+    try:
+        for flag in ("train_serial", None):
+            if flag:
+                os.environ["KDLAE_DEBUG"] = flag
+            else:
+                os.environ.pop("KDLAE_DEBUG", None)
+            m.zero_grad()
+            loss = L1LossForVideoFrames()(m(x), tgt.to(DEV))
+            loss.backward()
+            torch.cuda.synchronize()
+            losses.append(float(loss))
+            grads.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone())
+    finally:
+        if old is None:
+            os.environ.pop("KDLAE_DEBUG", None)
+        else:
+            os.environ["KDLAE_DEBUG"] = old
+    assert all(np.isfinite(losses)) and torch.isfinite(grads[0]).all()
+    assert torch.equal(grads[0], grads[1])
+    # the trainer path with a CPU target (ADVICE r04: it used to hand the kernel a host pointer)
+    tr = KDLAESTrainer(m, lr=3e-4, weight_decay=1e-4, betas=(0.9, 0.99), max_norm=0.01)
+    assert np.isfinite(float(tr.optimize_parameters(x, tgt)))
+
+
 def test_unsupported_reduction_raises():
     with pytest.raises(NotImplementedError):
         L1LossForVideoFrames(reduction="max")(torch.zeros(1, 2, 4, 4, device=DEV), torch.zeros(1, 2, 4, 4, device=DEV))
