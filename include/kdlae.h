@@ -23,11 +23,7 @@
  * the same bits: "no_attn_in_fusion" keeps the attention-output GEMM and the
  * LN + ffn.project_in GEMM separate (every block); "no_attn_in_split" keeps
  * them separate for the C = 96 blocks only (by default their first
- * project_in weight group is fused as well); "ffn48" runs the
- * C = 48 blocks' FFN half as one kernel (x1, LN, project_in on the tile halo,
- * dwconv + gate, project_out) writing each block's output to a ping-pong
- * buffer, instead of gemm_attn_in + gdfn_out (measured slower at 512^2 and
- * 1024^2, so off by default).  KDLAE_PROBE_DUMP
+ * project_in weight group is fused as well).  KDLAE_PROBE_DUMP
  * names a CSV file kdlae_t_probe_read writes per-launch timings to.
  * One more KDLAE_DEBUG flag is read on EVERY training call (kdlae_tt_forward /
  * kdlae_tt_backward / kdlae_tt_backward_marked), not at pack time:

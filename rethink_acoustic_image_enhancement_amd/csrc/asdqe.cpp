@@ -209,6 +209,7 @@ static int build_program_a(asdqe_handle* h) {
       if (n >= cout || c >= cin) return PEx{};
       return PEx{W + (n * cin + c) * 9 + tap, sc[n]};
     }));
+    g.w3 = ar.split(g.w, g.ntiles, g.kgroups);
     std::vector<PEx> b((size_t)cos);
     for (int n = 0; n < cout; ++n) b[n].a = sh[n];
     g.bias = ar.add(b);
@@ -255,6 +256,7 @@ static int build_program_a(asdqe_handle* h) {
     g.w = ar.add(pack_fragments(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
       return n < m ? PEx{W + n * 64 + k, -1} : PEx{};
     }));
+    g.w3 = ar.split(g.w, g.ntiles, g.kgroups);
     std::vector<PEx> b((size_t)g.N);
     for (int n = 0; n < m; ++n) b[n].a = Bv + n;
     g.bias = ar.add(b);
@@ -379,7 +381,7 @@ int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int 
     }
     GemmCall c;
     c.g = &g;
-    c.W = D.P(g.w);
+    c.W = D.P3(g.w3);
     c.bias = D.P(g.bias);
     c.in = in;
     c.out = o;

@@ -1,4 +1,4 @@
-// MFMA f32 implicit-GEMM convolution for gfx950 (CDNA4), NHWC activations.
+// MFMA implicit-GEMM convolution for gfx950 (CDNA4), NHWC activations, fp32 values.
 //
 // out[p][n] = epilogue( sum_k A'[p][k] * W[n][k] )
 //   pointwise (ksize 1): k = input channel               — every 1x1 Conv2d of KDLAE-T
@@ -14,11 +14,15 @@
 //
 // Work decomposition: a block is 8 waves; each wave owns 2 x 16 pixel rows, holding its A rows
 // for the current k-chunk in VGPRs (float4 per lane per 16-deep k-group: 16 rows x 64 B
-// contiguous per wave load).  The packed weight chunk [NT tiles][KG groups] is staged once into
-// LDS and shared by all 8 waves; when the whole K fits one chunk it stays resident while the
-// block walks a contiguous run of 256-row pixel tiles.  v_mfma_f32_16x16x4_f32 is an exact f32
-// fma chain (no xf32 on gfx950), so numerics equal an f32 dot product with a permuted k order.
+// contiguous per wave load).  The weight chunk [NT tiles][KG/2 pairs] (split fragment order) is
+// staged into LDS and shared by all 8 waves; when the whole K fits one chunk it stays resident
+// while the block walks a contiguous run of 256-row pixel tiles.
+// Products (r05): the split-bf16 MFMA of mfma3.h — the A rows are split once per tile after the
+// LayerNorm, the weights are stored pre-split, and every accumulator sums its 32-deep pairs in
+// ascending k order with mfma6's term order, so all schedules (resident / chunked / fused) give the
+// same bits for a pixel as long as their k-chunks start on an even k-group (the host enforces it).
 #include "kernels.h"
+#include "mfma3.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -27,9 +31,8 @@ namespace kdlae {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
+// LDS bytes of `tiles` output tiles' split records over kg k-groups
+static inline size_t w3_bytes(long long tiles, int kg) { return (size_t)tiles * ((kg + 1) / 2) * 3072; }
 
 // OUT: 0 = plain NHWC store (N % 16 == 0), 1 = PixelUnshuffle(2) store, 2 = PixelShuffle(2) store.
 // Operand roles: the MFMA's A operand is the packed weight tile (rows = output channels) and its
@@ -89,9 +92,14 @@ __device__ __forceinline__ void load_a(const GemmParams& p, const float* __restr
 // STATS = false: the caller guarantees p.stats == nullptr (the straight-line resident kernels).  A
 // runtime stats branch there put its global load after the next tile's A prefetch, and the join of
 // the two paths waited vmcnt(0): every tile drained the prefetch and the previous tile's stores.
+// No fp contraction here: every kernel that normalises a row (gemm_res, gemm_attn_in, the r01 and
+// chunked kernels) must round the variance and the shift the same way, whatever code surrounds it
+// (with hipcc's default fp-contract=fast the split-MFMA kernels contracted d.x * d.x + d.y * d.y
+// differently from one another, and the fused attention-input kernel stopped matching the unfused pair).
 template <int KG, bool STATS = true>
 __device__ __forceinline__ void apply_ln(const GemmParams& p, int b, int row0, int li, int HW,
                                          f32x4 (&a)[kGemmRT][KG]) {
+#pragma clang fp contract(off)
   const float wb = (p.ln == 2) ? 1.f : 0.f;
 #pragma unroll
   for (int r = 0; r < kGemmRT; ++r) {
@@ -126,40 +134,27 @@ __device__ __forceinline__ void apply_ln(const GemmParams& p, int b, int row0, i
   }
 }
 
-// acc[t][r] += W-tile(t) x A(r) over KG k-groups; W tiles at wl[(t * ldk + g) * 64 + lane].
-// Work is walked in units of two tiles (4 independent accumulators per k-step: MFMA latency 40 >
-// issue 32) and the B fragments of the NEXT unit (possibly of the next k-group) are read from LDS
-// before the current unit's 16 MFMAs, so LDS latency hides under ~512 cycles of matrix work even
-// at two waves per SIMD.
+// acc[t][r] += W-tile(t) x A(r) over the KG k-groups of `a` (fp32 rows, LN applied): pair G's B
+// operands are split right before its MFMAs (2 x 12 VGPRs live, not KP x 24); split records of tile t
+// at wl + (t * ldk + G) * kRec3.  Tiles are walked in units of two (4 independent accumulators).
 template <int NT, int KG>
-__device__ __forceinline__ void mfma_chunk(const f32x4* __restrict__ wl, int ldk, int lane,
-                                           const f32x4 (&a)[kGemmRT][KG], f32x4 (&acc)[NT][kGemmRT]) {
-  constexpr int NU = (NT + 1) / 2;  // units per k-group
-  f32x4 c0 = wl[(0 * ldk + 0) * 64 + lane];
-  f32x4 c1 = NT > 1 ? wl[(1 * ldk + 0) * 64 + lane] : f32x4{0.f, 0.f, 0.f, 0.f};
+__device__ __forceinline__ void mfma_chunk3(const f32x4* __restrict__ wl, int ldk, int lane,
+                                            const f32x4 (&a)[kGemmRT][KG], f32x4 (&acc)[NT][kGemmRT]) {
+  constexpr int KP = (KG + 1) / 2, NU = (NT + 1) / 2;
 #pragma unroll
-  for (int g = 0; g < KG; ++g) {
+  for (int G = 0; G < KP; ++G) {
+    F3 x[kGemmRT];
+#pragma unroll
+    for (int r = 0; r < kGemmRT; ++r)
+      x[r] = split3(a[r][2 * G], 2 * G + 1 < KG ? a[r][2 * G + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int t = 2 * u;
-      // prefetch the next unit
-      const int nu = (u + 1 < NU) ? u + 1 : 0;
-      const int ng = (u + 1 < NU) ? g : g + 1;
-      const int nt = 2 * nu;
-      f32x4 n0 = c0, n1 = c1;
-      if (ng < KG) {
-        n0 = wl[(nt * ldk + ng) * 64 + lane];
-        if (nt + 1 < NT) n1 = wl[((nt + 1) * ldk + ng) * 64 + lane];
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int r = 0; r < kGemmRT; ++r) {
-          acc[t][r] = mfma4(c0[s], a[r][g][s], acc[t][r]);
-          if (t + 1 < NT) acc[t + 1][r] = mfma4(c1[s], a[r][g][s], acc[t + 1][r]);
-        }
-      c0 = n0;
-      c1 = n1;
+      const f32x4* w0 = wl + (t * ldk + G) * kRec3 + lane;
+      if (t + 1 < NT)
+        mfma6_pair<kGemmRT, true>(w0, w0 + ldk * kRec3, x, acc[t], acc[t + 1]);
+      else
+        mfma6_pair<kGemmRT, false>(w0, w0, x, acc[t], acc[t]);
     }
   }
 }
@@ -266,6 +261,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
   const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
   if (t_begin >= t_end) return;
 
+  constexpr int KP = (KG + 1) / 2;  // split pairs per k-chunk
   if constexpr (RES) {
     // ------------------------------------------------------------------ resident schedule
     const int g0 = blockIdx.y * p.group_tiles;                       // first output tile of the group
@@ -278,16 +274,16 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
       load_a<KG, CONV3>(p, p.A + (long long)b * HW * p.lda,
                         (t_begin - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16), 0, li, lq, HW, an);
     }
+    const int n4pad = ((gtiles + NT - 1) / NT) * NT * KP * kRec3;  // partial last chunk reads zeros
     for (int tile = t_begin; tile < t_end; ++tile) {
       const int b = tile / p.tiles_per_img;
       const int row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
       const int wkey = p.w_img_stride ? b : 0;
       if (staged != wkey) {
         __syncthreads();
-        const f32x4* wbase = reinterpret_cast<const f32x4*>(p.Wp + (long long)wkey * p.w_img_stride +
-                                                            (long long)g0 * p.kgroups * 256);
-        const int n4 = gtiles * p.kgroups * 64;
-        const int n4pad = ((gtiles + NT - 1) / NT) * NT * p.kgroups * 64;  // partial last chunk reads zeros
+        const f32x4* wbase =
+            reinterpret_cast<const f32x4*>(p.Wp + (long long)wkey * p.w_img_stride) + (long long)g0 * KP * kRec3;
+        const int n4 = gtiles * KP * kRec3;
         for (int idx = tid; idx < n4pad; idx += kGemmThreads)
           wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
         const int nb4 = ((gtiles + NT - 1) / NT) * NT * 4;                  // bias of the group's tiles
@@ -320,15 +316,17 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
         for (int t = 0; t < NT; ++t)
 #pragma unroll
           for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-        mfma_chunk<NT, KG>(wlds + (size_t)c0 * p.kgroups * 64, p.kgroups, lane, a, acc);
-        const f32x4* bl = wlds + ((gtiles + NT - 1) / NT) * NT * p.kgroups * 64 + c0 * 4;
+        mfma_chunk3<NT, KG>(wlds + (size_t)c0 * KP * kRec3, KP, lane, a, acc);
+        const f32x4* bl = wlds + n4pad + c0 * 4;
         if (p.R) epilogue<NT, OUT, true>(p, b, row0, g0 + c0, gtiles - c0, li, lq, HW, acc, bl);
         else epilogue<NT, OUT, false>(p, b, row0, g0 + c0, gtiles - c0, li, lq, HW, acc, bl);
       }
     }
   } else {
     // ------------------------------------------------------------------ chunked schedule (RES == false)
+    // k-chunk kc holds pairs kc KP .. kc KP + KP - 1 (the host keeps KG even when K takes several chunks)
     const int nc = blockIdx.y;
+    const int KPt = (p.kgroups + 1) / 2;
     for (int tile = t_begin; tile < t_end; ++tile) {
       const int b = tile / p.tiles_per_img;
       const int row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
@@ -341,31 +339,30 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void conv_gemm_kernel(GemmParams
       for (int kc = 0; kc < p.kchunks; ++kc) {
         const int wkey = p.w_img_stride ? b : 0;
         __syncthreads();
-        const float* wbase = p.Wp + (long long)wkey * p.w_img_stride;
-        for (int idx = tid; idx < NT * KG * 64; idx += kGemmThreads) {
-          const int t = idx / (KG * 64);
-          const int rem = idx - t * (KG * 64);
-          const int g = rem >> 6, l = rem & 63;
-          const int gt = nc * NT + t, gg = kc * KG + g;
+        const f32x4* wbase = reinterpret_cast<const f32x4*>(p.Wp + (long long)wkey * p.w_img_stride);
+        for (int idx = tid; idx < NT * KP * kRec3; idx += kGemmThreads) {
+          const int t = idx / (KP * kRec3);
+          const int rem = idx - t * (KP * kRec3);
+          const int G = rem / kRec3, sl = rem - G * kRec3;
+          const int gt = nc * NT + t, gp = kc * KP + G;
           f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (gt < p.ntiles && gg < p.kgroups)
-            v = *reinterpret_cast<const f32x4*>(wbase + ((long long)(gt * p.kgroups + gg) * 64 + l) * 4);
+          if (gt < p.ntiles && gp < KPt) v = wbase[((long long)gt * KPt + gp) * kRec3 + sl];
           wlds[idx] = v;
         }
         if (kc == 0)
           for (int idx = tid; idx < NT * 4; idx += kGemmThreads) {  // bias of the block's NT tiles
             const int n = nc * NT * 16 + 4 * idx;
-            wlds[NT * KG * 64 + idx] =
+            wlds[NT * KP * kRec3 + idx] =
                 (p.bias && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
           }
         __syncthreads();
         f32x4 a[kGemmRT][KG];
         load_a<KG, CONV3>(p, Ab, row0, kc, li, lq, HW, a);
         if (p.ln) apply_ln<KG>(p, b, row0, li, HW, a);
-        mfma_chunk<NT, KG>(wlds, KG, lane, a, acc);
+        mfma_chunk3<NT, KG>(wlds, KP, lane, a, acc);
       }
-      if (p.R) epilogue<NT, OUT, true>(p, b, row0, nc * NT, NT, li, lq, HW, acc, wlds + NT * KG * 64);
-      else epilogue<NT, OUT, false>(p, b, row0, nc * NT, NT, li, lq, HW, acc, wlds + NT * KG * 64);
+      if (p.R) epilogue<NT, OUT, true>(p, b, row0, nc * NT, NT, li, lq, HW, acc, wlds + NT * KP * kRec3);
+      else epilogue<NT, OUT, false>(p, b, row0, nc * NT, NT, li, lq, HW, acc, wlds + NT * KP * kRec3);
     }
   }
 }
@@ -426,7 +423,7 @@ template <int NT, int KG, int NCH, int WPE, bool HASR, bool PF>
 __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
   const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lq = lane >> 4;
   const int HW = p.F * p.H * p.W;
   int bx, by;
@@ -436,18 +433,19 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
   if (t_begin >= t_end) return;
   const int g0 = by * p.group_tiles;
   const int gtiles = min(p.group_tiles, p.ntiles - g0);
-  constexpr int TP = NT * NCH;  // tiles staged per group (zero weights past gtiles)
+  constexpr int KP = (KG + 1) / 2;  // split pairs
+  constexpr int TP = NT * NCH;      // tiles staged per group (zero weights past gtiles)
+  constexpr int WS = TP * KP * kRec3;  // weight slots in LDS; the bias follows
   // weights are per image when w_img_stride != 0 (the MDTA-folded projection M = W_proj blockdiag(A))
   auto stage = [&](int wkey) {
     const f32x4* wbase =
-        reinterpret_cast<const f32x4*>(p.Wp + (long long)wkey * p.w_img_stride + (long long)g0 * p.kgroups * 256);
-    const int n4 = gtiles * KG * 64;
-    for (int idx = tid; idx < TP * KG * 64; idx += kGemmThreads)
-      wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+        reinterpret_cast<const f32x4*>(p.Wp + (long long)wkey * p.w_img_stride) + (long long)g0 * KP * kRec3;
+    const int n4 = gtiles * KP * kRec3;
+    for (int idx = tid; idx < WS; idx += kGemmThreads) wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
     for (int idx = tid; idx < TP * 4; idx += kGemmThreads) {
       const int n = g0 * 16 + 4 * idx;
-      wlds[TP * KG * 64 + idx] = (p.bias && idx < gtiles * 4 && n < p.N)
-                                      ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      wlds[WS + idx] = (p.bias && idx < gtiles * 4 && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n)
+                                                                : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   int staged = p.w_img_stride ? t_begin / p.tiles_per_img : 0;
@@ -464,7 +462,8 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
   // stores it emits (the data VGPRs were rewritten right after issue: wrong outputs on the GPU).
   auto tile_voff = [&](int t, unsigned v, unsigned bytes) -> int {
     return (int)(((t < gtiles) ? v : bytes) + 64u * (unsigned)t);
-  };  auto rows_of = [&](int tile, int& b, int& row0) {
+  };
+  auto rows_of = [&](int tile, int& b, int& row0) {
     b = tile / p.tiles_per_img;
     row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
   };
@@ -480,7 +479,6 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       for (int g = 0; g < KG; ++g) dst[r][g] = buf_load4(ra, base + 64u * g);
     }
   };
-  f32x4 a[kGemmRT][KG];
   [[maybe_unused]] f32x4 an[kGemmRT][KG];
   if constexpr (PF) load_rows(t_begin, an);
   // The tile body runs once peeled, then in the loop: hipcc's waitcnt pass merges the loop header's
@@ -496,6 +494,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       __syncthreads();
       staged = b;
     }
+    f32x4 a[kGemmRT][KG];
     if constexpr (PF) {
 #pragma unroll
       for (int r = 0; r < kGemmRT; ++r)
@@ -506,6 +505,14 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       load_rows(tile, a);
     }
     if (p.ln) apply_ln<KG, false>(p, b, row0, li, HW, a);
+    // K = 96 (unit-major body below): every pair's B operands split once per tile
+    [[maybe_unused]] F3 xg[KP][kGemmRT];
+    if constexpr (KG == 6) {
+#pragma unroll
+      for (int G = 0; G < KP; ++G)
+#pragma unroll
+        for (int r = 0; r < kGemmRT; ++r) xg[G][r] = split3(a[r][2 * G], a[r][2 * G + 1]);
+    }
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
     [[maybe_unused]] __amdgpu_buffer_rsrc_t rr;
     if constexpr (HASR) rr = buf_rsrc(p.R + (long long)b * HW * p.ldr, r_bytes);
@@ -517,20 +524,15 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       vr[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldr * 4u + 16u * lq + 64u * g0 : r_bytes;
     }
     if constexpr (KG == 6) {
-    // K = 96: unit-major chunk body.  Each tile pair is accumulated over every k-group and stored
-    // before the next pair starts, so a pair's stores issue beside the next pair's MFMAs instead of
-    // in one burst after all of them (r03 ablation: dropping the stores sped the K = 96 shapes up
-    // 12-44%); only 4 accumulators are live.  Same per-tile summation order (k-group outer, k-step
-    // inner) as mfma_chunk: bit-identical outputs.  Measured -2..-4% on the KG = 6 shapes; slower for
-    // KG = 3 (+14%, HBM-bound) and KG = 12 (+2%), which keep the chunk-major body
-    // (profiles/r03_gemm_ab_probe.txt).
+    // K = 96: unit-major chunk body.  Each tile pair is accumulated over every pair and stored before
+    // the next tile pair starts, so a pair's stores issue beside the next pair's MFMAs instead of in
+    // one burst after all of them; only 4 accumulators are live.  Same per-tile summation order (pair
+    // ascending, mfma6's term order) as mfma_chunk3: identical outputs.
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
-      const f32x4* wl = wlds + (size_t)ch * NT * KG * 64;
-      const f32x4* bl = wlds + TP * KG * 64 + ch * NT * 4;
+      const f32x4* wl = wlds + (size_t)ch * NT * KP * kRec3;
+      const f32x4* bl = wlds + WS + ch * NT * 4;
       constexpr int NU = (NT + 1) / 2;
-      f32x4 c0 = wl[lane];
-      f32x4 c1 = NT > 1 ? wl[KG * 64 + lane] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int t = 2 * u;
@@ -549,24 +551,12 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r) a0[r] = a1[r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int g = 0; g < KG; ++g) {
-          // the next (tile pair, k-group)'s W fragments, read before this one's MFMAs
-          const int ng = g + 1 < KG ? g + 1 : 0;
-          const int nt = g + 1 < KG ? t : t + 2;
-          f32x4 n0 = c0, n1 = c1;
-          if (nt < NT) {
-            n0 = wl[(nt * KG + ng) * 64 + lane];
-            if (nt + 1 < NT) n1 = wl[((nt + 1) * KG + ng) * 64 + lane];
-          }
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int r = 0; r < kGemmRT; ++r) {
-              a0[r] = mfma4(c0[s], a[r][g][s], a0[r]);
-              if (t + 1 < NT) a1[r] = mfma4(c1[s], a[r][g][s], a1[r]);
-            }
-          c0 = n0;
-          c1 = n1;
+        for (int G = 0; G < KP; ++G) {
+          const f32x4* w0 = wl + (t * KP + G) * kRec3 + lane;
+          if (t + 1 < NT)
+            mfma6_pair<kGemmRT, true>(w0, w0 + KP * kRec3, xg[G], a0, a1);
+          else
+            mfma6_pair<kGemmRT, false>(w0, w0, xg[G], a0, a1);
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -599,10 +589,10 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_chunk<NT, KG>(wlds + (size_t)ch * NT * KG * 64, KG, lane, a, acc);
+      mfma_chunk3<NT, KG>(wlds + (size_t)ch * NT * KP * kRec3, KP, lane, a, acc);
       // bias after the K sum, as every other GEMM schedule does: a pixel's result must not depend
       // on which schedule (batch size) produced it
-      const f32x4* bl = wlds + TP * KG * 64 + ch * NT * 4;
+      const f32x4* bl = wlds + WS + ch * NT * 4;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const f32x4 bias = bl[4 * t + lq];
@@ -631,7 +621,7 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
 // accumulators through the residual add and LayerNorm into the project_in MFMAs without leaving
 // registers; it is stored once (the FFN's residual) and never re-read.  The unfused pair wrote x1,
 // then read it back, and its N = 48 GEMM ran at ~4.5 TB/s / 36 TF/s.
-// Numerics: both GEMMs accumulate k-group-major, k-step-minor exactly as gemm_res_kernel does, and
+// Numerics: both GEMMs accumulate pair-major in mfma6's term order exactly as gemm_res_kernel does, and
 // x1 = (acc + bias_m) + x in that order, so the result equals the unfused path bit for bit.
 template <int NT, int KG, int NCH>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParams p) {
@@ -643,24 +633,26 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
   const int t_begin = blockIdx.x * p.tiles_per_block;
   const int t_end = min(t_begin + p.tiles_per_block, p.total_tiles);
   if (t_begin >= t_end) return;
+  constexpr int KP = (KG + 1) / 2;   // split pairs
   constexpr int TP = NT * NCH;       // project_in tiles staged (zero weights past ntiles)
-  f32x4* ml = wlds + TP * KG * 64 + TP * 4;  // M fragments [KG tiles][KG groups][64], then bias_m [KG][4]
+  constexpr int WS = TP * KP * kRec3;
+  f32x4* ml = wlds + WS + TP * 4;    // M split records [KG tiles][KP pairs][kRec3], then bias_m [KG][4]
   {
     const f32x4* wbase = reinterpret_cast<const f32x4*>(p.Wp);
-    const int n4 = p.ntiles * KG * 64;
-    for (int idx = tid; idx < TP * KG * 64; idx += kGemmThreads)
-      wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int n4 = p.ntiles * KP * kRec3;
+    for (int idx = tid; idx < WS; idx += kGemmThreads) wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
     for (int idx = tid; idx < TP * 4; idx += kGemmThreads) {
       const int n = 4 * idx;
-      wlds[TP * KG * 64 + idx] = (p.bias && idx < p.ntiles * 4 && n < p.N)
-                                     ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      wlds[WS + idx] = (p.bias && idx < p.ntiles * 4 && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n)
+                                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   auto stage_m = [&](int b) {
     const f32x4* mb = reinterpret_cast<const f32x4*>(p.Wm + (long long)b * p.wm_img_stride);
-    for (int idx = tid; idx < KG * KG * 64; idx += kGemmThreads) ml[idx] = mb[idx];
+    for (int idx = tid; idx < KG * KP * kRec3; idx += kGemmThreads) ml[idx] = mb[idx];
     for (int idx = tid; idx < KG * 4; idx += kGemmThreads)
-      ml[KG * KG * 64 + idx] = p.bias_m ? *reinterpret_cast<const f32x4*>(p.bias_m + 4 * idx) : f32x4{0.f, 0.f, 0.f, 0.f};
+      ml[KG * KP * kRec3 + idx] =
+          p.bias_m ? *reinterpret_cast<const f32x4*>(p.bias_m + 4 * idx) : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   int staged = t_begin / p.tiles_per_img;
   stage_m(staged);
@@ -739,9 +731,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
       for (int t = 0; t < KG; ++t)
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r) acc1[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_chunk<KG, KG>(ml, KG, lane, a, acc1);
+      mfma_chunk3<KG, KG>(ml, KP, lane, a, acc1);
       if constexpr (KG >= 6) load_rows(p.R, p.ldr, r_bytes, tile, xr);
-      const f32x4* bm = ml + KG * KG * 64;
+      const f32x4* bm = ml + KG * KP * kRec3;
       const __amdgpu_buffer_rsrc_t r1 = buf_rsrc(p.out1 + (long long)b * HW * p.ldo1, o1_bytes);
 #pragma unroll
       for (int r = 0; r < kGemmRT; ++r) {
@@ -771,8 +763,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_chunk<NT, KG>(wlds + (size_t)ch * NT * KG * 64, KG, lane, a, acc);
-      const f32x4* bl = wlds + TP * KG * 64 + ch * NT * 4;
+      mfma_chunk3<NT, KG>(wlds + (size_t)ch * NT * KP * kRec3, KP, lane, a, acc);
+      const f32x4* bl = wlds + WS + ch * NT * 4;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const f32x4 bias = bl[4 * t + lq];
@@ -795,14 +787,16 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
 //   issue the NEXT step's weight chunk by buffer-load-to-LDS (double-buffered slots; out-of-range
 //   records come back as zeros) and its A rows into registers (buffer loads, zero outside the image
 //   or past K, so the 3x3 zero padding needs no branch);
-//   16 x NT x KG MFMAs on this step's operands; at a tile's last k-chunk the epilogue.
+//   6 x NT x KG / 2 split MFMAs per row subtile on this step's operands; at a tile's last k-chunk the
+//   epilogue.
 // r01's version staged each weight chunk through VGPRs behind two __syncthreads and loaded A only
 // after them, so every k-chunk exposed two memory latencies with both waves of a SIMD parked.
 template <int NT, int KG, bool CONV3, int OUT, bool HASR>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
-  constexpr int SLOT = NT * KG * 64;                  // f32x4 per weight slot
-  constexpr int PIECES = NT * KG;                     // 1 KiB records per chunk
+  constexpr int KP = (KG + 1) / 2;                    // split pairs per k-chunk (KG even when K takes several)
+  constexpr int SLOT = NT * KP * kRec3;               // f32x4 per weight slot
+  constexpr int PIECES = NT * KP * 3;                 // 1 KiB planes per chunk
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lq = lane >> 4;
@@ -818,9 +812,10 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
     const int n = nc * NT * 16 + 4 * idx;
     bias_l[idx] = (p.bias && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const unsigned w_bytes = (unsigned)p.ntiles * (unsigned)p.kgroups * 1024u;
+  const int KPt = (p.kgroups + 1) / 2;
+  const unsigned w_bytes = (unsigned)p.ntiles * (unsigned)KPt * 3072u;
   const unsigned a_bytes = (unsigned)HW * (unsigned)p.lda * 4u;
-  // weights of step (tile, kc) -> slot; record (t, g) of the chunk = packed record (nc*NT + t, kc*KG + g)
+  // weights of step (tile, kc) -> slot; record (t, G) of the chunk = split record (nc*NT + t, kc*KP + G)
   auto issue_w = [&](int tile, int kc, int slot) {
     const int b = tile / p.tiles_per_img;
     const __amdgpu_buffer_rsrc_t rw =
@@ -831,9 +826,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
     for (int j = 0; j < (PIECES + 7) / 8; ++j) {
       const int k = wave + 8 * j;
       if (k >= PIECES) break;
-      const int t = k / KG, g = k - (k / KG) * KG;
-      const int gt = nc * NT + t, gg = kc * KG + g;
-      const unsigned off = (gt < p.ntiles && gg < p.kgroups) ? (unsigned)(gt * p.kgroups + gg) * 1024u + 16u * lane : kOOB;
+      const int t = k / (3 * KP), rem = k - t * (3 * KP);
+      const int G = rem / 3, pl = rem - 3 * G;
+      const int gt = nc * NT + t, gp = kc * KP + G;
+      const unsigned off =
+          (gt < p.ntiles && gp < KPt) ? (unsigned)((gt * KPt + gp) * 3 + pl) * 1024u + 16u * lane : kOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + 64 * k), 16, (int)off,
                                                0, 0, 0);
     }
@@ -888,15 +885,18 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
     }
   };
   auto ln_apply = [&](int b, int row0, const float2 (&st)[kGemmRT], f32x4 (&x)[kGemmRT][KG]) {
+#pragma clang fp contract(off)  // apply_ln's rounding (the r01 kernel's stats path)
     if (!p.stats) {
       apply_ln<KG>(p, b, row0, li, HW, x);
       return;
     }
     const float wb = (p.ln == 2) ? 1.f : 0.f;
 #pragma unroll
-    for (int r = 0; r < kGemmRT; ++r)
+    for (int r = 0; r < kGemmRT; ++r) {
+      const float sh = st[r].x * wb;
 #pragma unroll
-      for (int g = 0; g < KG; ++g) x[r][g] = (x[r][g] - st[r].x * wb) * st[r].y;
+      for (int g = 0; g < KG; ++g) x[r][g] = (x[r][g] - sh) * st[r].y;
+    }
   };
   f32x4 a[kGemmRT][KG], an[kGemmRT][KG];
   f32x4 acc[NT][kGemmRT];
@@ -926,7 +926,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
       issue_w(tile, kc + 1, slot ^ 1);
       load_a2(tile, kc + 1, an);
       if (p.ln) ln_apply(b, row0, st, a);
-      mfma_chunk<NT, KG>(wlds + slot * SLOT, KG, lane, a, acc);
+        mfma_chunk3<NT, KG>(wlds + slot * SLOT, KP, lane, a, acc);
       slot ^= 1;
     }
     // last k-chunk: residual loads, then the next tile's first operands (clamped, so the count of
@@ -951,7 +951,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
     issue_w(ntile, 0, slot ^ 1);
     load_a2(ntile, 0, an);
     if (p.ln) ln_apply(b, row0, st, a);
-    mfma_chunk<NT, KG>(wlds + slot * SLOT, KG, lane, a, acc);
+      mfma_chunk3<NT, KG>(wlds + slot * SLOT, KP, lane, a, acc);
     slot ^= 1;
     if constexpr (OUT == 0) {
       const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
@@ -984,19 +984,22 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_chunk_kernel(GemmParams 
   X(6, 6, false, 0, true, 2, true) X(3, 6, false, 0, true, 2, true) X(3, 8, false, 0, true, 2, true) \
   X(6, 8, false, 0, true, 2, true) X(6, 12, false, 0, false, 2, true) X(8, 12, false, 0, false, 2, true) \
   X(3, 12, false, 0, false, 2, true) X(6, 16, false, 0, false, 2, true) X(3, 16, false, 0, false, 2, true) \
-  X(3, 3, false, 0, false, 2, false) X(6, 6, false, 0, false, 2, false) X(9, 12, false, 0, false, 2, false) \
+  X(3, 3, false, 0, false, 2, false) X(6, 6, false, 0, false, 2, false) \
   X(8, 12, false, 0, false, 2, false) X(6, 12, false, 0, false, 2, false) X(3, 12, false, 0, false, 2, false) \
   X(6, 16, false, 0, false, 2, false) X(3, 16, false, 0, false, 2, false) \
   X(12, 8, false, 0, false, 2, false) \
-  X(3, 3, true, 1, false, 2, false) X(3, 6, true, 1, false, 2, false) X(6, 6, true, 1, false, 2, false) \
-  X(6, 12, true, 1, false, 2, false) X(12, 3, true, 1, false, 2, false) X(12, 6, true, 1, false, 2, false) \
-  X(3, 3, true, 2, false, 2, false) X(3, 6, true, 2, false, 2, false) X(6, 6, true, 2, false, 2, false) \
-  X(6, 12, true, 2, false, 2, false) X(12, 3, true, 2, false, 2, false) X(12, 6, true, 2, false, 2, false) \
+  X(3, 6, true, 1, false, 2, false) X(6, 6, true, 1, false, 2, false) \
+  X(6, 12, true, 1, false, 2, false) X(12, 6, true, 1, false, 2, false) \
+  X(3, 6, true, 2, false, 2, false) X(6, 6, true, 2, false, 2, false) \
+  X(6, 12, true, 2, false, 2, false) X(12, 6, true, 2, false, 2, false) \
   X(2, 6, true, 2, false, 2, false) X(2, 6, true, 1, false, 2, false) \
-  X(1, 9, true, 0, false, 2, false) X(2, 9, true, 0, false, 2, false) X(4, 9, true, 0, false, 2, false) \
+  \
   X(8, 6, true, 0, false, 2, false) X(4, 6, true, 0, false, 2, false) X(2, 6, true, 0, false, 2, false) \
   X(1, 3, false, 0, false, 2, false) X(3, 4, false, 0, false, 2, false) X(4, 4, false, 2, false, 2, false) \
-  X(8, 4, false, 2, false, 2, false) X(4, 2, false, 2, false, 2, false) X(3, 3, false, 2, false, 2, false)
+  X(8, 4, false, 2, false, 2, false) X(4, 2, false, 2, false, 2, false) X(3, 3, false, 2, false, 2, false) \
+  X(6, 4, true, 1, false, 2, false) X(8, 4, true, 1, false, 2, false) X(6, 4, true, 2, false, 2, false) \
+  X(8, 4, true, 2, false, 2, false) X(8, 4, true, 0, false, 2, false) \
+  X(4, 4, true, 0, false, 2, false) X(2, 4, true, 0, false, 2, false)
 
 bool gemm_has_variant(int NT, int KG, bool conv3, int wpe, bool resident, int out_mode) {
 #define X(a, b, c, o, f, w, r) \
@@ -1027,11 +1030,11 @@ static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, si
 // (NT, KG, NCH, PF) of the straight-line resident kernel; launched for both HASR values
 #define KDLAE_GEMM_RES2_VARIANTS(X) \
   X(9, 3, 1, true) X(9, 3, 2, true) X(8, 3, 1, true) X(8, 3, 2, true) X(3, 3, 1, true) X(3, 3, 2, true) \
-  X(6, 3, 1, true) X(6, 3, 2, true) X(9, 6, 1, true) X(9, 6, 2, true) X(8, 6, 1, true) X(8, 6, 2, true) \
-  X(6, 6, 1, true) X(6, 6, 2, true) X(6, 6, 3, true) X(3, 6, 1, true) X(3, 6, 2, true) X(3, 8, 1, true) X(3, 8, 2, true) \
-  X(6, 8, 1, true) X(6, 8, 2, true) X(6, 12, 1, false) X(6, 12, 2, false) X(8, 12, 1, false) \
+  X(6, 3, 1, true) X(6, 3, 2, true) X(9, 6, 1, true) X(8, 6, 1, true) X(8, 6, 2, true) \
+  X(6, 6, 1, true) X(6, 6, 2, true) X(3, 6, 1, true) X(3, 6, 2, true) X(3, 8, 1, true) X(3, 8, 2, true) \
+  X(6, 8, 1, true) X(6, 8, 2, true) X(6, 12, 1, false) X(8, 12, 1, false) \
   X(3, 12, 1, false) X(3, 12, 2, false) X(6, 16, 1, false) X(3, 16, 1, false)
-// (every entry's NT x NCH x KG KiB of weights fits the 160 KiB LDS; choose_variant keeps it <= 158)
+// (choose_variant keeps an entry's NT x NCH x ceil(KG/2) x 3 KiB of split weights <= 158 KiB)
 
 // residual (HASR) instance only where launch_gemm's no-spill rule (res_ok) can admit a residual
 template <int NT, int KG, int NCH>
@@ -1067,21 +1070,28 @@ static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_
   return hipGetLastError();
 }
 
-// (NT, KG, CONV3, OUT) of the r02 chunked kernel: two weight slots of NT x KG KiB must fit the LDS
+// (NT, KG, CONV3, OUT) of the r02 chunked kernel: two weight slots of NT x ceil(KG/2) x 3 KiB must fit
+// the LDS
 // (only shapes whose A double buffer + accumulators fit 256 VGPRs without spills: NT x KG <= ~64)
 #define KDLAE_GEMM_CHUNK2_VARIANTS(X) \
-  X(3, 3, false, 0) X(6, 6, false, 0) X(8, 8, false, 0) X(12, 4, false, 0) X(1, 3, false, 0) X(3, 4, false, 0) \
-  X(3, 3, true, 1) X(3, 6, true, 1) X(6, 6, true, 1) X(2, 6, true, 1) X(8, 6, true, 1) \
-  X(3, 3, true, 2) X(3, 6, true, 2) X(6, 6, true, 2) X(2, 6, true, 2) X(8, 6, true, 2) \
-  X(1, 9, true, 0) X(2, 9, true, 0) X(4, 9, true, 0) X(8, 6, true, 0) X(4, 6, true, 0) X(2, 6, true, 0) \
-  X(4, 4, false, 2) X(8, 4, false, 2) X(4, 2, false, 2) X(3, 3, false, 2)
+  X(3, 3, false, 0) X(6, 6, false, 0) X(12, 4, false, 0) X(1, 3, false, 0) X(3, 4, false, 0) \
+  X(3, 6, true, 1) X(2, 6, true, 1) \
+  X(3, 6, true, 2) X(2, 6, true, 2) \
+  X(4, 6, true, 0) X(2, 6, true, 0) \
+  X(4, 4, false, 2) X(8, 4, false, 2) X(4, 2, false, 2) X(3, 3, false, 2) \
+  X(6, 4, true, 1) X(8, 4, true, 1) X(6, 4, true, 2) X(8, 4, true, 2) X(8, 4, true, 0) \
+  X(4, 4, true, 0) X(2, 4, true, 0)
+// (r05: the split-MFMA instances that spill at 256 VGPRs — NT x KG = 36..48 on the implicit 3x3 convs,
+// KG = 9 — were dropped; the 3x3 convs take 4-deep k-chunks instead)
 
 // (NT, KG, NCH) of the fused attention-output + project_in kernel (C = 48: K = 3 groups)
-#define KDLAE_GEMM_ATTN_IN_VARIANTS(X) X(8, 3, 2) X(9, 3, 2) X(6, 3, 3) X(8, 6, 2)
+#define KDLAE_GEMM_ATTN_IN_VARIANTS(X) X(8, 3, 2) X(9, 3, 2) X(6, 3, 3)
 
+// the variant exists and its project_in weights + the per-image M (split records) fit the LDS
 bool gemm_attn_in_variant(int NT, int KG, int nch) {
 #define X(a, b, c) \
-  if (NT == a && KG == b && nch == c) return true;
+  if (NT == a && KG == b && nch == c)     \
+    return w3_bytes((long long)NT * nch, KG) + (size_t)NT * nch * 64 + w3_bytes(KG, KG) + (size_t)KG * 64 <= 160 * 1024;
   KDLAE_GEMM_ATTN_IN_VARIANTS(X)
 #undef X
   return false;
@@ -1097,11 +1107,11 @@ bool gemm_has_variant2(int NT, int KG, bool conv3, int out_mode) {
 
 template <int NT, int KG, bool C3, int OUT>
 static hipError_t launch_chunk2(const GemmParams& p, int grid_x, int grid_y, hipStream_t s) {
-  const size_t lds = (size_t)2 * NT * KG * 1024 + (size_t)NT * 64;
+  const size_t lds = 2 * w3_bytes(NT, KG) + (size_t)NT * 64;
   static size_t attr_lds[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  constexpr bool R0 = (OUT == 0 && !C3 && NT * KG <= 36);  // residual variants without spills
+  constexpr bool R0 = (OUT == 0 && !C3 && NT * KG < 36);  // residual variants without spills
   if (lds > attr_lds[dev]) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_chunk_kernel<NT, KG, C3, OUT, false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1130,9 +1140,11 @@ hipError_t launch_gemm_route(const GemmParams& p, int NT, int KG, int wpe, int g
   const bool c3 = p.ksize == 3;
   const bool res = p.group_tiles > 0;
   if (p.ln && !p.stats && (p.kchunks > 1 || p.kgroups > KG)) return hipErrorInvalidValue;  // LN needs whole rows
+  // split pairs must not straddle k-chunks: every chunk starts on an even k-group (mfma3.h)
+  if (p.kchunks > 1 && KG % 2) return hipErrorInvalidValue;
   if (p.Wm) {  // fused attention output + LN + GEMM: one resident group, K = N of the M GEMM = C
     const int nch = (p.ntiles + NT - 1) / NT;
-    const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64 + (size_t)KG * KG * 1024 + (size_t)KG * 64;
+    const size_t lds = w3_bytes((long long)NT * nch, KG) + (size_t)NT * nch * 64 + w3_bytes(KG, KG) + (size_t)KG * 64;
     const long long HW = (long long)p.F * p.H * p.W;
     const long long mx = HW * std::max({p.lda, p.ldo, p.ldr, p.ldo1}) * 4;
     if (!res || c3 || p.out_mode || p.group_tiles < p.ntiles || p.kgroups != KG || p.kchunks != 1 || p.relu ||
@@ -1163,7 +1175,7 @@ hipError_t launch_gemm_route(const GemmParams& p, int NT, int KG, int wpe, int g
     const long long mx = HW * std::max(std::max(p.lda, p.ldo), p.R ? p.ldr : 0) * 4;
     const int nch = (p.group_tiles + NT - 1) / NT;
     const int grid_y = (p.ntiles + p.group_tiles - 1) / p.group_tiles;
-    const size_t lds = (size_t)NT * nch * KG * 1024 + (size_t)NT * nch * 64;
+    const size_t lds = w3_bytes((long long)NT * nch, KG) + (size_t)NT * nch * 64;
     // residual variants keep NT x 2 residual float4 live across the chunk's MFMAs: only where that
     // fits the 256-VGPR budget without spills (hipcc -Rpass-analysis), else the r01 kernel
     const bool res_ok = !p.R || (NT * nch <= 12 && NT * nch * KG <= 72 && KG <= 8 && p.ldr % 4 == 0);  // no VGPR spills
@@ -1183,17 +1195,17 @@ hipError_t launch_gemm_route(const GemmParams& p, int NT, int KG, int wpe, int g
     if (p.kgroups != KG || p.kchunks != 1) return hipErrorInvalidValue;
     grid_y = (p.ntiles + p.group_tiles - 1) / p.group_tiles;
     const size_t tiles_pad = (size_t)((p.group_tiles + NT - 1) / NT) * NT;
-    lds = tiles_pad * p.kgroups * 1024 + tiles_pad * 64;
+    lds = w3_bytes((long long)tiles_pad, p.kgroups) + tiles_pad * 64;
   } else {
     grid_y = (p.ntiles + NT - 1) / NT;
-    lds = (size_t)NT * KG * 1024 + (size_t)NT * 64;
+    lds = w3_bytes(NT, KG) + (size_t)NT * 64;
   }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (route == 0 && !res && gemm_has_variant2(NT, KG, c3, p.out_mode) && p.lda % 4 == 0) {
     const long long HW = (long long)p.F * p.H * p.W;
     const long long osz = p.out_mode == 2 ? 4 * HW : (p.out_mode == 1 ? HW / 4 : HW);
     const bool fits = HW * p.lda * 4 < (1LL << 31) && osz * p.ldo * 4 < (1LL << 31) &&
-                      (!p.R || osz * p.ldr * 4 < (1LL << 31)) && (long long)p.ntiles * p.kgroups * 1024 < (1LL << 31);
+                      (!p.R || osz * p.ldr * 4 < (1LL << 31)) && (long long)w3_bytes(p.ntiles, p.kgroups) < (1LL << 31);
     if (fits) {
 #define X(a, b, c, o) \
       if (NT == a && KG == b && c3 == c && p.out_mode == o) return launch_chunk2<a, b, c, o>(p, grid_x, grid_y, s);

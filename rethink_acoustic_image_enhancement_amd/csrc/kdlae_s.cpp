@@ -170,6 +170,7 @@ static int build_program_s(kdlae_s_handle* h) {
       if (n >= cout || c >= cin) return PEx{};
       return PEx{W + (n * cin + c) * 27 + tap, -1};
     }));
+    g.w3 = ar.split(g.w, g.ntiles, g.kgroups);
     std::vector<PEx> b((size_t)g.ntiles * 16);
     for (int n = 0; n < cout; ++n) b[n].a = Bv + n;
     g.bias = ar.add(b);
@@ -225,6 +226,7 @@ static int build_program_s(kdlae_s_handle* h) {
       if (c >= cout || k >= cin) return PEx{};
       return PEx{W + ((k * cout + c) * 2 + ii) * 2 + jj, -1};
     }));
+    g.w3 = ar.split(g.w, g.ntiles, g.kgroups);
     std::vector<PEx> b((size_t)g.ntiles * 16);
     for (int n = 0; n < 4 * cos; ++n)
       if ((n >> 2) < cout) b[n].a = Bv + (n >> 2);
@@ -358,7 +360,7 @@ int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int 
     }
     GemmCall c;
     c.g = &g;
-    c.W = D.P(g.w);
+    c.W = D.P3(g.w3);
     c.bias = D.P(g.bias);
     c.in = in;
     c.out = o;
@@ -408,7 +410,7 @@ int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int 
     float* sk = buf(pl.skip[i]);
     GemmCall c;  // ConvTranspose3d (1,2,2) + bias, + skip, written in place over the skip tensor
     c.g = &h->up[j];
-    c.W = D.P(h->up[j].w);
+    c.W = D.P3(h->up[j].w3);
     c.bias = D.P(h->up[j].bias);
     c.in = View{tB, ccur};
     c.out = View{sk, ci};

@@ -36,11 +36,6 @@ struct BlockW {
   // forms x1), a plain LN GEMM on x1 runs group 1
   bool attn_in_split = false;
   Gemm pin_g0, pin_g1;
-  // C = 48 (r04): the whole FFN half (x1 = x + M v, LN, project_in, dwconv + gate, project_out,
-  // residual) in one kernel (gdfn.hip ffn48_kernel) writing the block output to another buffer; the
-  // stage alternates buffers.  Opt-in (debug flag ffn48): bit-identical, but measured slower than
-  // gemm_attn_in + gdfn_out (12.46 vs 11.2 ms per 1024^2 block, profiles/r04_ffn48_ab_probe.txt)
-  bool ffn48 = false;
 };
 
 }  // namespace kdlae
@@ -72,6 +67,7 @@ struct kdlae_t_handle {
   std::vector<float*> taps;
 
   const float* P(size_t off) const { return dw.P(off); }
+  const float* P3(size_t off) const { return dw.P3(off); }
 };
 
 namespace kdlae {
@@ -183,6 +179,12 @@ struct Packer {
   size_t pack(int ntiles, int kgroups, F Wf) {
     return prog.add(pack_fragments(ntiles, kgroups, Wf));
   }
+  // f32 fragment block + its split-fragment-order copy (what the GEMM kernels read, mfma3.h)
+  template <class F>
+  void pack_gemm(Gemm& g, F Wf) {
+    g.w = pack(g.ntiles, g.kgroups, Wf);
+    g.w3 = prog.split(g.w, g.ntiles, g.kgroups);
+  }
 
   // 1x1 conv [Cout][Cin] with optional LN(weight, bias) folded on the input side.
   // row_map(n) -> source output row or -1 (padding); stored N = nstore.
@@ -202,7 +204,7 @@ struct Packer {
     g.ksize = 1;
     g.n_true = Cout;
     g.k_true = Cin;
-    g.w = pack(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
+    pack_gemm(g, [&](int n, int k) -> PEx {
       if (n >= nstore || k >= Cin) return PEx{};
       const int src = row_map(n);
       if (src < 0) return PEx{};
@@ -248,7 +250,7 @@ struct Packer {
     g.K = 9 * Cin;
     g.n_true = Cout;
     g.k_true = 9 * Cin;
-    g.w = pack(g.ntiles, g.kgroups, [&](int n, int k) -> PEx {
+    pack_gemm(g, [&](int n, int k) -> PEx {
       if (n >= Cout) return PEx{};
       const int tap = k / Cin, c = k - tap * Cin;
       return PEx{W + (n * Cin + c) * 9 + tap, -1};
@@ -352,6 +354,7 @@ struct Packer {
     const bool no_ai = debug_flag("no_attn_in_fusion");
     b.fused_attn_in = b.pin.group_tiles >= b.pin.ntiles && b.pin.KG == C / 16 && b.pin.WPE == 2 &&
                       gemm_attn_in_variant(b.pin.NT, b.pin.KG, (b.pin.ntiles + b.pin.NT - 1) / b.pin.NT) && !no_ai;
+    // (gemm_attn_in_variant also checks that the variant's weights + M fit the LDS)
     // C = 96 (two weight groups): the fused kernel on group 0 + a plain LN GEMM on group 1.  A wash in
     // r02 (profiles/r02_attn_in_probe.txt); since r04's fused-kernel waitcnt fix and XCD-paired GEMM
     // order -4.2% at 512^2 and -2.7% at 256^2 per block (profiles/r04k_attn_in_split_ab_probe.txt), so on
@@ -366,6 +369,7 @@ struct Packer {
       b.pin_g0.n_true = (int)((long long)b.pin.n_true * gt / b.pin.ntiles);
       b.pin_g1 = b.pin;
       b.pin_g1.w = b.pin.w + (size_t)gt * b.pin.kgroups * 256;
+      b.pin_g1.w3 = b.pin.w3 + (size_t)split3_floats(gt, b.pin.kgroups);
       if (b.pin.bias != kNone) b.pin_g1.bias = b.pin.bias + (size_t)16 * gt;
       b.pin_g1.ntiles = b.pin.ntiles - gt;
       b.pin_g1.N = b.pin.N - 16 * gt;
@@ -373,8 +377,6 @@ struct Packer {
       b.pin_g1.group_tiles = b.pin_g1.ntiles;
       b.fused_attn_in = b.attn_in_split = true;
     }
-    b.ffn48 = b.fused_attn_in && !b.attn_in_split && b.fused_gdfn && ffn48_supported(C, hidS, 16) &&
-              b.pin.ntiles == 2 * hidS / 16 && debug_flag("ffn48");
     return b;
   }
 
@@ -448,7 +450,7 @@ static Plan make_plan(const kdlae_t_handle* h, int B, int H, int W) {
       mst = std::max(mst, P * 2);
       mpart = std::max(mpart, (long long)B * b.heads * nslots_for(Hh, Ww, B, b.heads) * slot);
       mred = std::max(mred, (long long)B * b.heads * slot);
-      mM = std::max(mM, (long long)B * b.C * b.C);
+      mM = std::max(mM, (long long)B * split3_floats(b.C / 16, b.C / 16));
     }
   };
   acc(h->enc1, P1, H, W);
@@ -544,16 +546,15 @@ struct Fwd {
     return probe_end(1, probeC, bytes, 2.0 * P * g.n_true * g.k_true);
   }
 
-  // One TransformerBlock (:159-163) in place on x, or, with f48 (b.ffn48 and a width ffn48_kernel
-  // takes), from x into *f48 (which must not overlap x).
-  int block(const BlockW& b, View x, int Hh, int Ww, const View* f48 = nullptr) {
+  // One TransformerBlock (:159-163) in place on x.
+  int block(const BlockW& b, View x, int Hh, int Ww) {
     const int HW = Hh * Ww;
     const int ln = h->cfg.layernorm_biasfree ? 1 : 2;
     const long long P = (long long)B * HW;
     int rc;
     // --- attention
     View qkv{buf(pl.qkv), 3 * b.C};
-    rc = gemm(b.qkv, h->P(b.qkv.w), 0, x, Hh, Ww, qkv, 0, nullptr, 0, ln, b.C, b.C);
+    rc = gemm(b.qkv, h->P3(b.qkv.w3), 0, x, Hh, Ww, qkv, 0, nullptr, 0, ln, b.C, b.C);
     if (rc) return rc;
     GramParams gp{};
     gp.qkv = qkv.p;
@@ -579,34 +580,6 @@ struct Fwd {
     if ((rc = probe_end(2, b.C, 4.0 * P * 4 * b.C, 2.0 * P * (27.0 * b.C + (double)b.C * b.Ch)))) return rc;
     HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
     HIPCHK(launch_attn_fold(buf(pl.red), gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
-    if (f48) {
-      Ffn48Params q{};
-      q.v = buf(pl.vbuf);
-      q.ldv = b.C;
-      q.x = x.p;
-      q.ldx = x.ld;
-      q.Wm = buf(pl.Mp);
-      q.wm_img_stride = (long long)b.C * b.C;
-      q.bias_m = h->P(b.proj_b);
-      q.ln = ln;
-      q.Win = h->P(b.pin.w);
-      q.bias_in = h->P(b.pin.bias);
-      q.dw = h->P(b.dwffn);
-      q.Wout = h->P(b.pout.w);
-      q.bias_out = h->P(b.pout.bias);
-      q.out = f48->p;
-      q.ldo = f48->ld;
-      q.Bn = B;
-      q.H = Hh;
-      q.W = Ww;
-      if ((rc = probe_begin(3, b.C))) return rc;
-      tag = "ffn48 C" + std::to_string(b.C) + " hid" + std::to_string(b.hid) + " HW" + std::to_string(HW);
-      HIPCHK(launch_ffn48(q, s));
-      // algorithmic: read v and x, write the block output; M v, project_in, dwconv + gate, project_out
-      const double Pd = (double)P;
-      return probe_end(3, b.C, 4.0 * Pd * 3.0 * b.C,
-                       2.0 * Pd * ((double)b.C * b.C + 2.0 * b.C * b.hid + 18.0 * b.hid + (double)b.hid * b.C));
-    }
     View fpre{buf(pl.fpre), 2 * b.hidS};
     const bool fuse_in = b.fused_attn_in;
     if (fuse_in) {
@@ -614,7 +587,7 @@ struct Fwd {
       const Gemm& g0 = b.attn_in_split ? b.pin_g0 : b.pin;
       GemmCall c;
       c.g = &g0;
-      c.W = h->P(g0.w);
+      c.W = h->P3(g0.w3);
       c.bias = h->P(g0.bias);
       c.in = View{buf(pl.vbuf), b.C};
       c.out = fpre;
@@ -628,7 +601,7 @@ struct Fwd {
       c.ln_C = b.C;
       c.stats_buf = buf(pl.stats);
       c.Wm = buf(pl.Mp);
-      c.wm_img_stride = (long long)b.C * b.C;
+      c.wm_img_stride = split3_floats(b.C / 16, b.C / 16);
       c.bias_m = h->P(b.proj_b);
       c.out1 = x;
       if ((rc = probe_begin(1, b.C))) return rc;
@@ -643,19 +616,20 @@ struct Fwd {
                                   (double)g0.n_true * b.C);
       if ((rc = probe_end(1, b.C, bytes, 2.0 * Pd * ((double)b.C * b.C + (double)b.C * g0.n_true)))) return rc;
       if (b.attn_in_split) {  // project_in's second weight group on x1 (now in x)
-        rc = gemm(b.pin_g1, h->P(b.pin_g1.w), 0, x, Hh, Ww, View{fpre.p + 16 * b.pin_g0.ntiles, fpre.ld}, 0, nullptr,
+        rc = gemm(b.pin_g1, h->P3(b.pin_g1.w3), 0, x, Hh, Ww, View{fpre.p + 16 * b.pin_g0.ntiles, fpre.ld}, 0, nullptr,
                   0, ln, b.C, b.C);
         if (rc) return rc;
       }
     } else {
-      rc = gemm(b.proj_gemm, buf(pl.Mp), (long long)b.C * b.C, View{buf(pl.vbuf), b.C}, Hh, Ww, x, 0, x.p, x.ld, 0,
+      rc = gemm(b.proj_gemm, buf(pl.Mp), split3_floats(b.C / 16, b.C / 16), View{buf(pl.vbuf), b.C}, Hh, Ww, x, 0,
+                x.p, x.ld, 0,
                 0, b.C);
       if (rc) return rc;
     }
     // --- feed-forward
     if ((rc = tap(x, b.C, Hh, Ww))) return rc;  // x1 (diagnostics only)
     if (!fuse_in) {
-      rc = gemm(b.pin, h->P(b.pin.w), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
+      rc = gemm(b.pin, h->P3(b.pin.w3), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
       if (rc) return rc;
     }
     if (b.fused_gdfn) {
@@ -664,7 +638,7 @@ struct Fwd {
       gd.ld = fpre.ld;
       gd.hidS = b.hidS;
       gd.dw = h->P(b.dwffn);
-      gd.Wp = h->P(b.pout.w);
+      gd.Wp = h->P3(b.pout.w3);
       gd.bias = h->P(b.pout.bias);
       gd.R = x.p;
       gd.ldr = x.ld;
@@ -696,7 +670,7 @@ struct Fwd {
     tag = "gate C" + std::to_string(b.C) + " hid" + std::to_string(b.hid) + " HW" + std::to_string(HW);
     HIPCHK(launch_dwconv_gate(ga, s));
     if ((rc = probe_end(3, b.C, 4.0 * P * 3 * b.hid, 2.0 * P * 18.0 * b.hid))) return rc;
-    return gemm(b.pout, h->P(b.pout.w), 0, View{buf(pl.fg), b.hidS}, Hh, Ww, x, 0, x.p, x.ld, 0, 0, b.C);
+    return gemm(b.pout, h->P3(b.pout.w3), 0, View{buf(pl.fg), b.hidS}, Hh, Ww, x, 0, x.p, x.ld, 0, 0, b.C);
   }
 
   // kdlae_t_debug_taps: taps passed so far in this forward; the order is tap_list's (per stage: its
@@ -715,22 +689,8 @@ struct Fwd {
     if (st.empty()) return KDLAE_OK;
     int rc = tap(x, st[0].C, Hh, Ww);
     if (rc) return rc;
-    // ffn48 blocks write their output to the other buffer of (x, T), T = the project_in scratch they
-    // do not use; an even count of them keeps the stage's output in x (an odd last one runs unfused).
-    // Off while diagnostics taps are armed (they read x1, which ffn48 never materialises).
-    const bool f48 = st[0].ffn48 && h->taps.empty() && ffn48_supported(st[0].C, st[0].hidS, Ww);
-    const int nf = f48 ? (int)st.size() / 2 * 2 : 0;
-    const View T{buf(pl.fpre), st[0].C};
-    View cur = x;
-    for (int i = 0; i < (int)st.size(); ++i) {
-      const BlockW& b = st[i];
-      if (i < nf) {
-        const View nxt = (i % 2 == 0) ? T : x;
-        if ((rc = block(b, cur, Hh, Ww, &nxt))) return rc;
-        cur = nxt;
-      } else {
-        if ((rc = block(b, x, Hh, Ww))) return rc;
-      }
+    for (const BlockW& b : st) {
+      if ((rc = block(b, x, Hh, Ww))) return rc;
       if ((rc = tap(x, b.C, Hh, Ww))) return rc;
     }
     return KDLAE_OK;
@@ -799,24 +759,24 @@ struct Fwd {
     // patch_embed (:275) from NCHW img into the level-1 concat buffer's second half
     if ((rc = small_in(h->patch_embed, img, ci * HW, HW, W, 1, H, W, e1, 1))) return rc;
     if ((rc = stage(h->enc1, e1, H, W))) return rc;
-    if ((rc = gemm(h->down1_2, h->P(h->down1_2.w), 0, e1, H, W, e2, 1, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = gemm(h->down1_2, h->P3(h->down1_2.w3), 0, e1, H, W, e2, 1, nullptr, 0, 0, 0, -1))) return rc;
     if ((rc = stage(h->enc2, e2, H2, W2))) return rc;
-    if ((rc = gemm(h->down2_3, h->P(h->down2_3.w), 0, e2, H2, W2, e3, 1, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = gemm(h->down2_3, h->P3(h->down2_3.w3), 0, e2, H2, W2, e3, 1, nullptr, 0, 0, 0, -1))) return rc;
     if ((rc = stage(h->enc3, e3, H3, W3))) return rc;
-    if ((rc = gemm(h->down3_4, h->P(h->down3_4.w), 0, e3, H3, W3, lat, 1, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = gemm(h->down3_4, h->P3(h->down3_4.w3), 0, e3, H3, W3, lat, 1, nullptr, 0, 0, 0, -1))) return rc;
     if ((rc = stage(h->latent, lat, H4, W4))) return rc;
     // decoder level 3 (:288-291)
-    if ((rc = gemm(h->up4_3, h->P(h->up4_3.w), 0, lat, H4, W4, View{L3, 8 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = gemm(h->up4_3, h->P3(h->up4_3.w3), 0, lat, H4, W4, View{L3, 8 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
     View d3{buf(pl.dec3), 4 * d};
-    if ((rc = gemm(h->reduce3, h->P(h->reduce3.w), 0, View{L3, 8 * d}, H3, W3, d3, 0, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = gemm(h->reduce3, h->P3(h->reduce3.w3), 0, View{L3, 8 * d}, H3, W3, d3, 0, nullptr, 0, 0, 0, -1))) return rc;
     if ((rc = stage(h->dec3, d3, H3, W3))) return rc;
     // decoder level 2 (:293-296)
-    if ((rc = gemm(h->up3_2, h->P(h->up3_2.w), 0, d3, H3, W3, View{L2, 4 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = gemm(h->up3_2, h->P3(h->up3_2.w3), 0, d3, H3, W3, View{L2, 4 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
     View d2{buf(pl.dec2), 2 * d};
-    if ((rc = gemm(h->reduce2, h->P(h->reduce2.w), 0, View{L2, 4 * d}, H2, W2, d2, 0, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = gemm(h->reduce2, h->P3(h->reduce2.w3), 0, View{L2, 4 * d}, H2, W2, d2, 0, nullptr, 0, 0, 0, -1))) return rc;
     if ((rc = stage(h->dec2, d2, H2, W2))) return rc;
     // decoder level 1 + refinement (:298-302), in place on the full 2d-channel concat buffer
-    if ((rc = gemm(h->up2_1, h->P(h->up2_1.w), 0, d2, H2, W2, View{L1, 2 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
+    if ((rc = gemm(h->up2_1, h->P3(h->up2_1.w3), 0, d2, H2, W2, View{L1, 2 * d}, 2, nullptr, 0, 0, 0, -1))) return rc;
     View d1{L1, 2 * d};
     if ((rc = stage(h->dec1, d1, H, W))) return rc;
     if ((rc = stage(h->refinement, d1, H, W))) return rc;
@@ -837,7 +797,7 @@ struct Fwd {
       View cb{buf(pl.cenb), 2 * d};
       if ((rc = small_in(h->cen, hq, co * HW, HW, W, 1, H, W, cb, 1))) return rc;
       View sv{buf(pl.srs), d};
-      if ((rc = gemm(h->upen, h->P(h->upen.w), 0, cb, H, W, sv, 2, nullptr, 0, 0, 0, -1))) return rc;
+      if ((rc = gemm(h->upen, h->P3(h->upen.w3), 0, cb, H, W, sv, 2, nullptr, 0, 0, 0, -1))) return rc;
       if ((rc = stage(h->enhance, sv, 2 * H, 2 * W))) return rc;
       if ((rc = small_out(h->outputen, sv, 2 * H, 2 * W, sr, 1, 0, nullptr, nullptr))) return rc;
     }

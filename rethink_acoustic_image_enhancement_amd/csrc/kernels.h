@@ -7,8 +7,9 @@
 //
 // Packed 1x1 / implicit-GEMM weights ("fragment order"): for output tile t (16 channels) and
 // k-group g (16 reduction indices) one 1 KiB record of 64 lanes x float4 holds
-// W[16t + (lane & 15)][16g + 4*(lane >> 4) + e], e = 0..3 — exactly the B operand each lane of
-// v_mfma_f32_16x16x4_f32 consumes over four k-steps, so a wave reads it as one contiguous 1 KiB.
+// W[16t + (lane & 15)][16g + 4*(lane >> 4) + e], e = 0..3 — the float4 an activation lane of the same
+// k-group loads.  The GEMM kernels read the "split fragment order" derived from it (mfma3.h): per
+// output tile and pair of k-groups, three bf16 planes of 1 KiB that feed v_mfma_f32_16x16x32_bf16.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -26,7 +27,7 @@ struct GemmParams {
   int cg_per_tap;                  // channel groups (of 16) per tap = Cin_pad / 16
   int kgroups;                     // taps * cg_per_tap
   int ksize, dil;                  // 1 (pointwise) or 3 (implicit GEMM, zero padding = dil)
-  const float* Wp; long long w_img_stride; int ntiles;
+  const float* Wp; long long w_img_stride; int ntiles;  // split records [ntiles][ceil(kgroups/2)][kRec3]
   int N;                           // output channels stored (padded channels included)
   const float* bias;               // [ntiles*16] or null
   float* out; int ldo;
@@ -122,7 +123,7 @@ struct GdfnParams {
   int hidS;                        // padded hidden width (multiple of 16)
   const float* dw;                 // per chunk g (hidS/16 of them) 512 floats: [9 taps][32 ch] weights,
                                    // [32] bias at +288, zero pad (channel order as in x)
-  const float* Wp;                 // project_out fragments [C/16][hidS/16][64][4]
+  const float* Wp;                 // project_out split records [C/16][hidS/32][kRec3] (mfma3.h)
   const float* bias;               // [C] or null
   const float* R; int ldr;         // residual (may alias out) or null
   float* out; int ldo;
@@ -133,25 +134,6 @@ struct GdfnParams {
 bool gdfn_supported(int C, int hidS);
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s);
 
-// Fused C = 48 feed-forward half of a TransformerBlock (gdfn.hip, ffn48_kernel): from the attention's
-// v and the block input x, out = x1 + project_out(gate(dwconv(project_in(LN(x1))))) with
-// x1 = x + M v (+ bias_m) — the gemm_attn_in_kernel + gdfn_out_kernel pair in one pass, bit for bit,
-// without the 2 hid-wide project_in rows (or x1) ever reaching HBM.  `out` must not overlap x or v
-// (neighbouring tiles read them as halo).
-struct Ffn48Params {
-  const float* v; int ldv;                          // attention v, [P][ldv] (48 channels)
-  const float* x; int ldx;                          // block input
-  const float* Wm; long long wm_img_stride;         // folded projection fragments per image (attn_fold)
-  const float* bias_m;                              // [48] or null
-  int ln;                                           // 1 BiasFree, 2 WithBias
-  const float* Win; const float* bias_in;           // project_in fragments [16][3][64][4], bias [256] or null
-  const float* dw;                                  // GDFN dw blocks, [8 chunks][512]
-  const float* Wout; const float* bias_out;         // project_out fragments [3][8][64][4], bias [48] or null
-  float* out; int ldo;
-  int Bn, H, W;
-};
-bool ffn48_supported(int C, int hidS, int W);
-hipError_t launch_ffn48(const Ffn48Params& p, hipStream_t s);
 
 // Pre/post-processing around the forward (pipeline.hip)
 struct PreParams {

@@ -16,6 +16,7 @@
 #include <type_traits>
 
 #include "kernels.h"
+#include "mfma3.h"
 #include "lds_dma.h"
 
 namespace kdlae {
@@ -704,7 +705,8 @@ hipError_t launch_gram_reduce(const float* partial, float* reduced, int Bn, int 
 
 // --------------------------------------------------------------------------- softmax + fold
 // grid (C/16, heads, B).  Each block rebuilds A for (b, h) in LDS, then computes 16 rows of
-// M[n][h*Ch + c2] = sum_c1 Wproj[n][h*Ch + c1] * A[c1][c2], stored in fragment order.
+// M[n][h*Ch + c2] = sum_c1 Wproj[n][h*Ch + c1] * A[c1][c2], stored in split fragment order (the GEMM
+// kernels' weight format, mfma3.h).
 __global__ __launch_bounds__(256) void attn_fold_kernel(const float* __restrict__ reduced, int slot_floats,
                                                         const float* __restrict__ proj,
                                                         const float* __restrict__ temp,
@@ -748,18 +750,31 @@ __global__ __launch_bounds__(256) void attn_fold_kernel(const float* __restrict_
     for (int c = 0; c < Ch; ++c) row[c] *= inv;
   }
   __syncthreads();
-  const int kgroups = C / 16;
-  float* Mb = Mp + (long long)b * C * C;
+  // M in split fragment order (mfma3.h): element (n, k) is bf16 j of lane (n & 15) + 16 q in the three
+  // planes of record (n >> 4, k >> 5), with kk = k & 31, q = (kk & 15) >> 2, j = 4 (kk >> 4) + (kk & 3)
+  const int kgroups = C / 16, kpt = (kgroups + 1) / 2;
+  __bf16* Mb = reinterpret_cast<__bf16*>(Mp + (long long)b * split3_floats(kgroups, kgroups));
+  auto put = [&](int n, int k, float v) {
+    const int kk = k & 31;
+    const int lane = (n & 15) + 16 * ((kk & 15) >> 2), j = 4 * (kk >> 4) + (kk & 3);
+    const long long slot = ((long long)((n >> 4) * kpt + (k >> 5)) * 3) * 64 + lane;
+    __bf16 vh, vm, vl;
+    split1(v, vh, vm, vl);
+    Mb[slot * 8 + j] = vh;
+    Mb[(slot + 64) * 8 + j] = vm;
+    Mb[(slot + 128) * 8 + j] = vl;
+  };
   for (int idx = threadIdx.x; idx < 16 * Ch; idx += 256) {
     const int nl = idx / Ch, c2 = idx - (idx / Ch) * Ch;
     const int n = nb * 16 + nl;
     const float* wr = proj + (long long)n * C + h * Ch;
     float s = 0.f;
     for (int c1 = 0; c1 < Ch; ++c1) s = fmaf(wr[c1], A[c1 * ldA + c2], s);
-    const int k = h * Ch + c2;
-    const int lane = (n & 15) + 16 * ((k & 15) >> 2);
-    Mb[(((long long)(n >> 4) * kgroups + (k >> 4)) * 64 + lane) * 4 + (k & 3)] = s;
+    put(n, h * Ch + c2, s);
   }
+  // an odd k-group count: the last pair's upper half (k = C .. C + 15) is zero
+  if ((kgroups & 1) && h == heads - 1)
+    for (int idx = threadIdx.x; idx < 256; idx += 256) put(nb * 16 + (idx >> 4), C + (idx & 15), 0.f);
 }
 
 hipError_t launch_attn_fold(const float* reduced, int slot_floats, const float* proj, const float* temp,

@@ -32,7 +32,9 @@ bool debug_flag(const char* name) {
 // Tile-shape selection.  Resident schedule when a variant with KG == kgroups exists: the weights
 // are split into groups that fit the LDS budget (one group per grid.y), and NT (accumulator tiles
 // per pass) minimises padding inside a group.  Otherwise the chunked schedule over (NT, KG).
+// Weights sit in LDS in split fragment order (mfma3.h): 3 KiB per output tile and k-group pair.
 static constexpr int kLdsBudgetKB = 152;
+static long long tile_lds_bytes(int kgroups) { return (long long)((kgroups + 1) / 2) * 3072 + 64; }
 
 void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
   static const int nts[] = {1, 2, 3, 4, 6, 8, 9, 12};
@@ -45,14 +47,14 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
     for (int w : {2}) {
       // two resident blocks per CU at 4 waves/SIMD -> half the LDS budget each
       const int budget_kb = w == 4 ? 76 : kLdsBudgetKB;
-      const int budget = std::max(1, budget_kb / g.kgroups);
+      const int budget = (int)std::max<long long>(1, budget_kb * 1024LL / tile_lds_bytes(g.kgroups));
       const int ngroups = (int)ceil_div(g.ntiles, budget);
       const int gt = (int)ceil_div(g.ntiles, ngroups);
       for (int nt : nts) {
         if (!gemm_has_variant(nt, g.kgroups, false, w, true, g.out_mode)) continue;
         const long long padded = ceil_div(gt, nt) * nt;
-        // weights (1 KiB per tile x k-group) + the group's bias (64 B per tile) must fit 160 KiB
-        if (padded * g.kgroups + ceil_div(padded, 16) > (w == 4 ? 80 : 158)) continue;
+        // split weights + the group's bias (64 B per tile) must fit 160 KiB
+        if (padded * tile_lds_bytes(g.kgroups) > (w == 4 ? 80 : 158) * 1024LL) continue;
         // default policy: 2 waves/SIMD.  4 waves/SIMD used to win on the store-heavy K <= 48 shapes
         // while every epilogue load drained the stores; with that fixed, 2 waves measure 10-15%
         // faster on all of them (r01 probe: C48 project_in @1024^2 5864 -> 5099 us)
@@ -71,7 +73,7 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
     }
     if (best_nt) {
       const int budget_kb = best_w == 4 ? 76 : kLdsBudgetKB;
-      const int budget = std::max(1, budget_kb / g.kgroups);
+      const int budget = (int)std::max<long long>(1, budget_kb * 1024LL / tile_lds_bytes(g.kgroups));
       g.NT = best_nt;
       g.KG = g.kgroups;
       g.WPE = best_w;
@@ -82,8 +84,9 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
   double best = 1e30;
   for (int nt : nts)
     for (int kg : kgs) {
-      if (!gemm_has_variant2(nt, kg, g.ksize == 3, g.out_mode) || (g.has_res && nt * kg > 36)) continue;
+      if (!gemm_has_variant2(nt, kg, g.ksize == 3, g.out_mode) || (g.has_res && nt * kg >= 36)) continue;
       const long long nch = ceil_div(g.ntiles, nt), kch = ceil_div(g.kgroups, kg);
+      if (kch > 1 && kg % 2) continue;  // split pairs may not straddle k-chunks (mfma3.h)
       const double waste = (double)(nch * nt) * (kch * kg) / ((double)g.ntiles * g.kgroups);
       // every k-chunk restages weights behind two barriers; every n-chunk re-reads A.
       // 1x1 (r01 v15 probe): n-chunks cost more than k-chunks; with penalties 0.06 / 0.02 the

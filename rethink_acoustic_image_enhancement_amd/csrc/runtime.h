@@ -12,6 +12,7 @@
 
 #include "../../include/kdlae.h"
 #include "kernels.h"
+#include "mfma3.h"
 
 namespace kdlae {
 
@@ -35,6 +36,7 @@ constexpr size_t kNone = (size_t)-1;
 // packed 1x1 / implicit-GEMM weights (offsets in floats into a device weight arena)
 struct Gemm {
   size_t w = kNone, bias = kNone;
+  size_t w3 = kNone;  // the same weights in split fragment order (mfma3.h), offset into the split arena
   int ntiles = 0, kgroups = 0, N = 0, K = 0, ksize = 1, cg_per_tap = 0, kt = 1;
   int out_mode = 0;  // store map the variant must support (0 plain, 1 unshuffle, 2 shuffle)
   int NT = 0, KG = 0, group_tiles = 0, WPE = 2;
@@ -63,10 +65,16 @@ struct PDer {                 // derived source value src[nsrc + j], computed be
   int32_t kind = 0;           // 0: src[a] / sqrt(src[b] + 1e-5)     (BatchNorm scale)
   int32_t a = -1, b = -1, c = -1, d = -1;  // 1: (src[a] - src[b]) * src[c] + src[d]  (BatchNorm shift)
 };
+struct PSplit {               // split arena [dst, +split3_floats) = split3 of the f32 records at arena[src]
+  int64_t src = 0, dst = 0, first = 0;  // first: index of the descriptor's first work item (record x lane)
+  int32_t ntiles = 0, kgroups = 0;
+};
 struct PackProgram {
   std::vector<PEx> ex;        // one per arena float
   std::vector<PDot> dots;
   std::vector<PDer> der;
+  std::vector<PSplit> splits;  // run after the gathers and dots
+  int64_t n3 = 0;              // floats in the split arena
   int64_t nsrc = 0;           // floats in the flat parameter vector
   size_t add(const std::vector<PEx>& v) {
     size_t off = (ex.size() + 63) / 64 * 64;
@@ -78,6 +86,18 @@ struct PackProgram {
     std::vector<PEx> v(n);
     for (size_t i = 0; i < n; ++i) v[i].a = base + (int32_t)i;
     return add(v);
+  }
+  // the split-fragment-order copy of the f32 fragment block at arena offset w (ntiles x kgroups records)
+  size_t split(size_t w, int ntiles, int kgroups) {
+    PSplit d;
+    d.src = (int64_t)w;
+    d.dst = n3;
+    d.ntiles = ntiles;
+    d.kgroups = kgroups;
+    d.first = splits.empty() ? 0 : splits.back().first + (int64_t)splits.back().ntiles * ((splits.back().kgroups + 1) / 2) * 64;
+    splits.push_back(d);
+    n3 += (split3_floats(ntiles, kgroups) + 63) / 64 * 64;
+    return (size_t)d.dst;
   }
   int32_t derive(const PDer& d) {
     der.push_back(d);
@@ -123,6 +143,11 @@ struct ParamStore {
 struct DeviceWeights {
   float* dev = nullptr;       // packed arena
   size_t n = 0;
+  float* dev3 = nullptr;      // split arena (GEMM weights in split fragment order, mfma3.h)
+  size_t n3 = 0;
+  PSplit* splits = nullptr;
+  int n_splits = 0;
+  int64_t split_items = 0;
   PEx* ex = nullptr;
   PDot* dots = nullptr;
   PDer* der = nullptr;
@@ -136,6 +161,7 @@ struct DeviceWeights {
   int run_host(const std::vector<float>& params, hipStream_t s);  // host copy of the flat vector
   void release();
   const float* P(size_t off) const { return off == kNone ? nullptr : dev + off; }
+  const float* P3(size_t off) const { return off == kNone ? nullptr : dev3 + off; }
 };
 
 // Restores the caller's current device when it goes out of scope.

@@ -78,8 +78,27 @@ extern "C" int kdlae_debug_gemm(const kdlae_debug_gemm_desc* d, void* stream) {
   p.kgroups = d->kgroups;
   p.ksize = d->ksize;
   p.dil = d->dil > 0 ? d->dil : 1;
-  p.Wp = d->Wp;
-  p.w_img_stride = d->w_img_stride;
+  // the caller hands f32 fragment order (runtime.h pack_fragments); the GEMM kernels read split
+  // fragment order (mfma3.h): convert into scratch owned by this call
+  hipStream_t s = (hipStream_t)stream;
+  const int nimg_w = d->w_img_stride ? d->Bn : 1;
+  const long long w3_img = kdlae::split3_floats(d->ntiles, d->kgroups);
+  float* w3 = nullptr;
+  float* m3 = nullptr;
+  struct Scratch {
+    float** a;
+    float** b;
+    hipStream_t s;
+    ~Scratch() {
+      (void)hipStreamSynchronize(s);
+      if (*a) (void)hipFree(*a);
+      if (*b) (void)hipFree(*b);
+    }
+  } scratch{&w3, &m3, s};
+  HIPCHK(hipMalloc(&w3, (size_t)(w3_img * nimg_w) * sizeof(float)));
+  HIPCHK(kdlae::launch_split3(d->Wp, w3, d->ntiles, d->kgroups, nimg_w, d->w_img_stride, w3_img, s));
+  p.Wp = w3;
+  p.w_img_stride = d->w_img_stride ? w3_img : 0;
   p.ntiles = d->ntiles;
   p.N = d->N;
   p.bias = d->bias;
@@ -100,12 +119,16 @@ extern "C" int kdlae_debug_gemm(const kdlae_debug_gemm_desc* d, void* stream) {
   p.total_tiles = d->Bn * p.tiles_per_img;
   p.kchunks = d->group_tiles ? 1 : (int)ceil_div(d->kgroups, d->KG);
   p.group_tiles = d->group_tiles;
-  p.Wm = d->Wm;
-  p.wm_img_stride = d->wm_img_stride;
+  if (d->Wm) {  // the per-image folded projection: kgroups x kgroups tiles per image
+    const long long m3_img = kdlae::split3_floats(d->kgroups, d->kgroups);
+    HIPCHK(hipMalloc(&m3, (size_t)(m3_img * d->Bn) * sizeof(float)));
+    HIPCHK(kdlae::launch_split3(d->Wm, m3, d->kgroups, d->kgroups, d->Bn, d->wm_img_stride, m3_img, s));
+    p.Wm = m3;
+    p.wm_img_stride = m3_img;
+  }
   p.bias_m = d->bias_m;
   p.out1 = d->out1;
   p.ldo1 = d->ldo1;
-  hipStream_t s = (hipStream_t)stream;
   if (d->ln && !d->Wm && (p.kchunks > 1 || d->kgroups * 16 != d->ln_C)) {
     if (!d->stats || d->ln_C > 512 || d->lda % 4) return fail(KDLAE_EINVAL_CONFIG, "chunked LN needs stats scratch");
     HIPCHK(kdlae::launch_ln_stats(d->A, d->lda, d->ln_C, (long long)d->Bn * HW, d->stats, s));

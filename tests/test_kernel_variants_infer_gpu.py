@@ -193,8 +193,9 @@ def _gemm_case(NT, KG, c3, out_mode, route, group_tiles=0, ntiles=None, with_r=F
 
 
 def _resident_group(NT, KG):
-    """group size for a resident 1x1 case: ragged chunks where the LDS budget (~150 KiB) allows"""
-    budget = 150 // KG
+    """group size for a resident 1x1 case: ragged chunks where the LDS budget (~150 KiB of split
+    records, 3 KiB per tile and pair of k-groups) allows"""
+    budget = 150 // (3 * ((KG + 1) // 2))
     return min(2 * NT - 1, max(NT, budget // NT * NT)) if NT > 1 else 1
 
 
@@ -217,9 +218,9 @@ def test_conv_gemm_variant(v):
     elif c3:
         _gemm_case(NT, KG, True, out_mode, 1, kchunks=2, dil=2 if out_mode == 0 else 1, with_r=out_mode != 0,
                    seed=i)
-    else:
-        _gemm_case(NT, KG, False, out_mode, 1, kchunks=3, ln=1 if out_mode == 0 else 0, with_r=out_mode == 0,
-                   relu=1, seed=i)
+    else:   # split pairs may not straddle k-chunks: an odd KG runs K in one chunk
+        _gemm_case(NT, KG, False, out_mode, 1, kchunks=1 if KG % 2 else 3, ln=1 if out_mode == 0 else 0,
+                   with_r=out_mode == 0, relu=1, seed=i)
 
 
 # ------------------------------------------------------------------------------ r02 kernels
@@ -256,13 +257,14 @@ def test_gemm_chunk_variant(v):
     if c3:
         _gemm_case(NT, KG, True, out_mode, 0, kchunks=2, dil=2 if out_mode == 0 else 1, with_r=out_mode != 0,
                    seed=300 + i)
-        if (NT, KG, out_mode) == (2, 9, 0):
-            _gemm_case(NT, KG, True, 0, 0, kchunks=1, kt=3, seed=350 + i)
-    else:
-        _gemm_case(NT, KG, False, out_mode, 0, kchunks=3, ln=1 if out_mode == 0 else 0,
+        if (NT, KG, out_mode) == (2, 4, 0):
+            _gemm_case(NT, KG, True, 0, 0, kchunks=7, kt=3, seed=350 + i)
+    else:   # split pairs may not straddle k-chunks: an odd KG runs K in one chunk
+        kch = 1 if KG % 2 else 3
+        _gemm_case(NT, KG, False, out_mode, 0, kchunks=kch, ln=1 if out_mode == 0 else 0,
                    relu=1 if out_mode == 0 else 0, seed=300 + i)
-        if out_mode == 0 and NT * KG <= 36:
-            _gemm_case(NT, KG, False, 0, 0, kchunks=3, with_r=True, seed=400 + i)
+        if out_mode == 0 and NT * KG < 36:
+            _gemm_case(NT, KG, False, 0, 0, kchunks=kch, with_r=True, seed=400 + i)
 
 
 ATTN = _variants(3) if torch.cuda.is_available() else []

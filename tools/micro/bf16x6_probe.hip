@@ -71,6 +71,13 @@ __global__ void tile_kernel(const float* __restrict__ A, const float* __restrict
         acc = mfma_bf(sa.m, sb.h, acc);
         acc = mfma_bf(sa.h, sb.m, acc);
         acc = mfma_bf(sa.h, sb.h, acc);
+      } else if (MODE == 61) {  // the library's order (mfma3.h mfma6): grouped by the A plane
+        acc = mfma_bf(sa.l, sb.h, acc);
+        acc = mfma_bf(sa.m, sb.m, acc);
+        acc = mfma_bf(sa.m, sb.h, acc);
+        acc = mfma_bf(sa.h, sb.l, acc);
+        acc = mfma_bf(sa.h, sb.m, acc);
+        acc = mfma_bf(sa.h, sb.h, acc);
       } else if (MODE == 60) {  // big term first (order check)
         acc = mfma_bf(sa.h, sb.h, acc);
         acc = mfma_bf(sa.m, sb.h, acc);
@@ -165,6 +172,7 @@ void accuracy(int K, int tiles, float spread) {
   run_mode<0>("f32 MFMA 16x16x4", K, tiles, dA, dB, dC, ref, scale);
   run_mode<3>("bf16 x3", K, tiles, dA, dB, dC, ref, scale);
   run_mode<6>("bf16 x6 (small first)", K, tiles, dA, dB, dC, ref, scale);
+  run_mode<61>("bf16 x6 (library order)", K, tiles, dA, dB, dC, ref, scale);
   run_mode<60>("bf16 x6 (big first)", K, tiles, dA, dB, dC, ref, scale);
   run_mode<9>("bf16 x9", K, tiles, dA, dB, dC, ref, scale);
   hipFree(dA);
