@@ -23,6 +23,7 @@
 // same bits for a pixel as long as their k-chunks start on an even k-group (the host enforces it).
 #include "kernels.h"
 #include "mfma3.h"
+#include "rowops.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -92,69 +93,48 @@ __device__ __forceinline__ void load_a(const GemmParams& p, const float* __restr
 // STATS = false: the caller guarantees p.stats == nullptr (the straight-line resident kernels).  A
 // runtime stats branch there put its global load after the next tile's A prefetch, and the join of
 // the two paths waited vmcnt(0): every tile drained the prefetch and the previous tile's stores.
-// No fp contraction here: every kernel that normalises a row (gemm_res, gemm_attn_in, the r01 and
-// chunked kernels) must round the variance and the shift the same way, whatever code surrounds it
-// (with hipcc's default fp-contract=fast the split-MFMA kernels contracted d.x * d.x + d.y * d.y
-// differently from one another, and the fused attention-input kernel stopped matching the unfused pair).
-template <int KG, bool STATS = true>
+// LayerNorm of the A rows: in registers (rowops.h ln_rows: the whole row is in the lane group; host:
+// kchunks == 1, kgroups * 16 == ln_C), or from precomputed row statistics (STATS, K chunked).
+template <int KG, bool STATS = true, int RT = kGemmRT>
 __device__ __forceinline__ void apply_ln(const GemmParams& p, int b, int row0, int li, int HW,
-                                         f32x4 (&a)[kGemmRT][KG]) {
+                                         f32x4 (&a)[RT][KG]) {
 #pragma clang fp contract(off)
-  const float wb = (p.ln == 2) ? 1.f : 0.f;
+  if (STATS && p.stats) {
+    const float wb = (p.ln == 2) ? 1.f : 0.f;
 #pragma unroll
-  for (int r = 0; r < kGemmRT; ++r) {
-    float mean, rstd;
-    if (STATS && p.stats) {
+    for (int r = 0; r < RT; ++r) {
       const int prow = min(row0 + r * 16 + li, HW - 1);
       const float2 st = *reinterpret_cast<const float2*>(p.stats + 2 * ((long long)b * HW + prow));
-      mean = st.x;
-      rstd = st.y;
-    } else {
-      // the whole LN row is in registers (host: kchunks == 1, kgroups * 16 == ln_C)
-      float s = 0.f;
+      const float sh = st.x * wb;
 #pragma unroll
-      for (int g = 0; g < KG; ++g) s += (a[r][g].x + a[r][g].y) + (a[r][g].z + a[r][g].w);
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      mean = s / (float)p.ln_C;
-      float v2 = 0.f;
-#pragma unroll
-      for (int g = 0; g < KG; ++g) {
-        const f32x4 d = a[r][g] - mean;
-        const float dd = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
-        v2 += (g < p.kgroups) ? dd : 0.f;
-      }
-      v2 += __shfl_xor(v2, 16);
-      v2 += __shfl_xor(v2, 32);
-      rstd = 1.0f / sqrtf(v2 / (float)p.ln_C + 1e-5f);
+      for (int g = 0; g < KG; ++g) a[r][g] = (a[r][g] - sh) * st.y;
     }
-    const float sh = mean * wb;
-#pragma unroll
-    for (int g = 0; g < KG; ++g) a[r][g] = (a[r][g] - sh) * rstd;
+    return;
   }
+  ln_rows<KG, RT>(p.ln, p.ln_C, p.kgroups, a);
 }
 
 // acc[t][r] += W-tile(t) x A(r) over the KG k-groups of `a` (fp32 rows, LN applied): pair G's B
 // operands are split right before its MFMAs (2 x 12 VGPRs live, not KP x 24); split records of tile t
 // at wl + (t * ldk + G) * kRec3.  Tiles are walked in units of two (4 independent accumulators).
-template <int NT, int KG>
+template <int NT, int KG, int RT = kGemmRT>
 __device__ __forceinline__ void mfma_chunk3(const f32x4* __restrict__ wl, int ldk, int lane,
-                                            const f32x4 (&a)[kGemmRT][KG], f32x4 (&acc)[NT][kGemmRT]) {
+                                            const f32x4 (&a)[RT][KG], f32x4 (&acc)[NT][RT]) {
   constexpr int KP = (KG + 1) / 2, NU = (NT + 1) / 2;
 #pragma unroll
   for (int G = 0; G < KP; ++G) {
-    F3 x[kGemmRT];
+    F3 x[RT];
 #pragma unroll
-    for (int r = 0; r < kGemmRT; ++r)
+    for (int r = 0; r < RT; ++r)
       x[r] = split3(a[r][2 * G], 2 * G + 1 < KG ? a[r][2 * G + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int t = 2 * u;
       const f32x4* w0 = wl + (t * ldk + G) * kRec3 + lane;
       if (t + 1 < NT)
-        mfma6_pair<kGemmRT, true>(w0, w0 + ldk * kRec3, x, acc[t], acc[t + 1]);
+        mfma6_pair<RT, true>(w0, w0 + ldk * kRec3, x, acc[t], acc[t + 1]);
       else
-        mfma6_pair<kGemmRT, false>(w0, w0, x, acc[t], acc[t]);
+        mfma6_pair<RT, false>(w0, w0, x, acc[t], acc[t]);
     }
   }
 }
@@ -386,11 +366,19 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* base, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)bytes, 0x00020000);
 }
+// cache policy of the streaming activation loads / output stores (gfx950 CPol: 1 sc0, 2 nt, 16 sc1);
+// A/B knobs, default policy
+#ifndef KDLAE_GEMM_LD_POL
+#define KDLAE_GEMM_LD_POL 0
+#endif
+#ifndef KDLAE_GEMM_ST_POL
+#define KDLAE_GEMM_ST_POL 0
+#endif
 __device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, KDLAE_GEMM_LD_POL));
 }
 __device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, KDLAE_GEMM_ST_POL);
 }
 constexpr unsigned kOOB = 0x80000000u;  // a byte offset past every descriptor's range
 
@@ -419,8 +407,13 @@ static dim3 gemm_grid(int grid_x, int grid_y) {
   return dim3((unsigned)(((grid_x + 7) / 8) * 8 * grid_y));
 }
 
+// WPE = 2: 8 waves x 2 row subtiles (RT) per wave; WPE = 4 (r05): 16 waves x 1 subtile — the same
+// 256-pixel block tile with twice the waves in flight at <= 128 VGPRs each (more loads and stores
+// outstanding per CU; every W plane read from LDS feeds 1 row subtile instead of 2).
 template <int NT, int KG, int NCH, int WPE, bool HASR, bool PF>
-__global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams p) {
+__global__ __launch_bounds__(kGemmThreads * WPE / 2, WPE) void gemm_res_kernel(GemmParams p) {
+  constexpr int RT = WPE == 4 ? 1 : kGemmRT;
+  constexpr int THREADS = kGemmThreads * WPE / 2;
   extern __shared__ __attribute__((aligned(16))) f32x4 wlds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -441,8 +434,8 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
     const f32x4* wbase =
         reinterpret_cast<const f32x4*>(p.Wp + (long long)wkey * p.w_img_stride) + (long long)g0 * KP * kRec3;
     const int n4 = gtiles * KP * kRec3;
-    for (int idx = tid; idx < WS; idx += kGemmThreads) wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int idx = tid; idx < TP * 4; idx += kGemmThreads) {
+    for (int idx = tid; idx < WS; idx += THREADS) wlds[idx] = idx < n4 ? wbase[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int idx = tid; idx < TP * 4; idx += THREADS) {
       const int n = g0 * 16 + 4 * idx;
       wlds[WS + idx] = (p.bias && idx < gtiles * 4 && n < p.N) ? *reinterpret_cast<const f32x4*>(p.bias + n)
                                                                 : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -465,21 +458,21 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
   };
   auto rows_of = [&](int tile, int& b, int& row0) {
     b = tile / p.tiles_per_img;
-    row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (kGemmRT * 16);
+    row0 = (tile - b * p.tiles_per_img) * kGemmRows + wave * (RT * 16);
   };
-  auto load_rows = [&](int tile, f32x4 (&dst)[kGemmRT][KG]) {
+  auto load_rows = [&](int tile, f32x4 (&dst)[RT][KG]) {
     int b, row0;
     rows_of(tile, b, row0);
     const __amdgpu_buffer_rsrc_t ra = buf_rsrc(p.A + (long long)b * HW * p.lda, a_bytes);
 #pragma unroll
-    for (int r = 0; r < kGemmRT; ++r) {
+    for (int r = 0; r < RT; ++r) {
       const unsigned pix = (unsigned)(row0 + r * 16 + li);
       const unsigned base = pix < (unsigned)HW ? pix * (unsigned)p.lda * 4u + 16u * lq : kOOB;
 #pragma unroll
       for (int g = 0; g < KG; ++g) dst[r][g] = buf_load4(ra, base + 64u * g);
     }
   };
-  [[maybe_unused]] f32x4 an[kGemmRT][KG];
+  [[maybe_unused]] f32x4 an[RT][KG];
   if constexpr (PF) load_rows(t_begin, an);
   // The tile body runs once peeled, then in the loop: hipcc's waitcnt pass merges the loop header's
   // predecessors and keeps the smaller outstanding count, so with the prologue (12 loads in flight)
@@ -494,31 +487,31 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       __syncthreads();
       staged = b;
     }
-    f32x4 a[kGemmRT][KG];
+    f32x4 a[RT][KG];
     if constexpr (PF) {
 #pragma unroll
-      for (int r = 0; r < kGemmRT; ++r)
+      for (int r = 0; r < RT; ++r)
 #pragma unroll
         for (int g = 0; g < KG; ++g) a[r][g] = an[r][g];
       load_rows(min(tile + 1, t_end - 1), an);  // unconditional: same op count on every path
     } else {
       load_rows(tile, a);
     }
-    if (p.ln) apply_ln<KG, false>(p, b, row0, li, HW, a);
+    if (p.ln) apply_ln<KG, false, RT>(p, b, row0, li, HW, a);
     // K = 96 (unit-major body below): every pair's B operands split once per tile
-    [[maybe_unused]] F3 xg[KP][kGemmRT];
+    [[maybe_unused]] F3 xg[KP][RT];
     if constexpr (KG == 6) {
 #pragma unroll
       for (int G = 0; G < KP; ++G)
 #pragma unroll
-        for (int r = 0; r < kGemmRT; ++r) xg[G][r] = split3(a[r][2 * G], a[r][2 * G + 1]);
+        for (int r = 0; r < RT; ++r) xg[G][r] = split3(a[r][2 * G], a[r][2 * G + 1]);
     }
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(p.out + (long long)b * HW * p.ldo, o_bytes);
     [[maybe_unused]] __amdgpu_buffer_rsrc_t rr;
     if constexpr (HASR) rr = buf_rsrc(p.R + (long long)b * HW * p.ldr, r_bytes);
-    unsigned vo[kGemmRT], vr[kGemmRT];
+    unsigned vo[RT], vr[RT];
 #pragma unroll
-    for (int r = 0; r < kGemmRT; ++r) {
+    for (int r = 0; r < RT; ++r) {
       const unsigned pix = (unsigned)(row0 + r * 16 + li);
       vo[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldo * 4u + 16u * lq + 64u * g0 : o_bytes;
       vr[r] = pix < (unsigned)HW ? pix * (unsigned)p.ldr * 4u + 16u * lq + 64u * g0 : r_bytes;
@@ -536,38 +529,38 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int t = 2 * u;
-        [[maybe_unused]] f32x4 rs[2][kGemmRT];
+        [[maybe_unused]] f32x4 rs[2][RT];
         if constexpr (HASR) {
 #pragma unroll
           for (int q = 0; q < 2; ++q)
 #pragma unroll
-            for (int r = 0; r < kGemmRT; ++r)
+            for (int r = 0; r < RT; ++r)
               rs[q][r] = (t + q < NT)
                              ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                              rr, tile_voff(ch * NT + t + q, vr[r], r_bytes), 0, 0))
                              : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        f32x4 a0[kGemmRT], a1[kGemmRT];
+        f32x4 a0[RT], a1[RT];
 #pragma unroll
-        for (int r = 0; r < kGemmRT; ++r) a0[r] = a1[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < RT; ++r) a0[r] = a1[r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int G = 0; G < KP; ++G) {
           const f32x4* w0 = wl + (t * KP + G) * kRec3 + lane;
           if (t + 1 < NT)
-            mfma6_pair<kGemmRT, true>(w0, w0 + KP * kRec3, xg[G], a0, a1);
+            mfma6_pair<RT, true>(w0, w0 + KP * kRec3, xg[G], a0, a1);
           else
-            mfma6_pair<kGemmRT, false>(w0, w0, xg[G], a0, a1);
+            mfma6_pair<RT, false>(w0, w0, xg[G], a0, a1);
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           if (t + q >= NT) continue;
           const f32x4 bias = bl[4 * (t + q) + lq];
 #pragma unroll
-          for (int r = 0; r < kGemmRT; ++r) {
+          for (int r = 0; r < RT; ++r) {
             f32x4 v = (q == 0 ? a0[r] : a1[r]) + bias;
             if constexpr (HASR) v += rs[q][r];
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
-                                                   tile_voff(ch * NT + t + q, vo[r], o_bytes), 0, 0);
+                                                   tile_voff(ch * NT + t + q, vo[r], o_bytes), 0, KDLAE_GEMM_ST_POL);
           }
         }
       }
@@ -575,21 +568,21 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
     } else {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
-      [[maybe_unused]] f32x4 res[NT][kGemmRT];
+      [[maybe_unused]] f32x4 res[NT][RT];
       if constexpr (HASR) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int r = 0; r < kGemmRT; ++r)
+          for (int r = 0; r < RT; ++r)
             res[t][r] = __builtin_bit_cast(
                 f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, tile_voff(ch * NT + t, vr[r], r_bytes), 0, 0));
       }
-      f32x4 acc[NT][kGemmRT];
+      f32x4 acc[NT][RT];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < kGemmRT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_chunk3<NT, KG>(wlds + (size_t)ch * NT * KP * kRec3, KP, lane, a, acc);
+        for (int r = 0; r < RT; ++r) acc[t][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_chunk3<NT, KG, RT>(wlds + (size_t)ch * NT * KP * kRec3, KP, lane, a, acc);
       // bias after the K sum, as every other GEMM schedule does: a pixel's result must not depend
       // on which schedule (batch size) produced it
       const f32x4* bl = wlds + WS + ch * NT * 4;
@@ -597,11 +590,11 @@ __global__ __launch_bounds__(kGemmThreads, WPE) void gemm_res_kernel(GemmParams 
       for (int t = 0; t < NT; ++t) {
         const f32x4 bias = bl[4 * t + lq];
 #pragma unroll
-        for (int r = 0; r < kGemmRT; ++r) {
+        for (int r = 0; r < RT; ++r) {
           f32x4 v = acc[t][r] + bias;
           if constexpr (HASR) v += res[t][r];
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro, tile_voff(ch * NT + t, vo[r], o_bytes),
-                                                 0, 0);
+                                                 0, KDLAE_GEMM_ST_POL);
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
@@ -771,7 +764,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t][r] + bias), ro,
-                                                 tile_voff(ch * NT + t, vo[r], o_bytes), 0, 0);
+                                                 tile_voff(ch * NT + t, vo[r], o_bytes), 0, KDLAE_GEMM_ST_POL);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
     }
@@ -1040,18 +1033,24 @@ static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, si
 template <int NT, int KG, int NCH>
 constexpr bool res2_hasr_ok() { return NT * NCH <= 12 && NT * NCH * KG <= 72 && KG <= 8; }
 
+// waves per SIMD of the resident kernel for K <= 96 (A/B knob): 2 = 8 waves x 32 rows, 4 = 16 waves x 16 rows
+#ifndef KDLAE_RES_WPE
+#define KDLAE_RES_WPE 2
+#endif
 template <int NT, int KG, int NCH, bool PF>
 static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
   constexpr bool RK = res2_hasr_ok<NT, KG, NCH>();
+  constexpr int W = (KDLAE_RES_WPE == 4 && KG <= 6) ? 4 : 2;
+  constexpr int TH = kGemmThreads * W / 2;
   static size_t attr_lds[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   if (lds > attr_lds[dev]) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, 2, false, PF>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, W, false, PF>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if constexpr (RK) {
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, 2, true, PF>),
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_res_kernel<NT, KG, NCH, W, true, PF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
@@ -1059,14 +1058,12 @@ static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_
   }
   if constexpr (RK) {
     if (p.R) {
-      hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, true, PF>), gemm_grid(grid_x, grid_y), dim3(kGemmThreads), lds, s,
-                         p);
+      hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, W, true, PF>), gemm_grid(grid_x, grid_y), dim3(TH), lds, s, p);
       return hipGetLastError();
     }
   }
   if (p.R) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, 2, false, PF>), gemm_grid(grid_x, grid_y), dim3(kGemmThreads), lds, s,
-                     p);
+  hipLaunchKernelGGL((gemm_res_kernel<NT, KG, NCH, W, false, PF>), gemm_grid(grid_x, grid_y), dim3(TH), lds, s, p);
   return hipGetLastError();
 }
 

@@ -36,6 +36,10 @@ struct BlockW {
   // forms x1), a plain LN GEMM on x1 runs group 1
   bool attn_in_split = false;
   Gemm pin_g0, pin_g1;
+  // r05: the whole feed-forward half (LN, project_in, dwconv + gate, project_out, residual) in one
+  // kernel (ffn.hip), project_in recomputed on each tile's halo; the block output goes to the other
+  // buffer of a ping-pong pair (stage()).  Debug flag no_ffn_fusion keeps the unfused kernels.
+  bool ffn_fused = false;
 };
 
 }  // namespace kdlae
@@ -377,6 +381,8 @@ struct Packer {
       b.pin_g1.group_tiles = b.pin_g1.ntiles;
       b.fused_attn_in = b.attn_in_split = true;
     }
+    b.ffn_fused = b.fused_gdfn && ffn_fused_supported(C, hidS) && b.pin.ntiles == 2 * hidS / 16 &&
+                  !debug_flag("no_ffn_fusion");
     return b;
   }
 
@@ -546,8 +552,9 @@ struct Fwd {
     return probe_end(1, probeC, bytes, 2.0 * P * g.n_true * g.k_true);
   }
 
-  // One TransformerBlock (:159-163) in place on x.
-  int block(const BlockW& b, View x, int Hh, int Ww) {
+  // One TransformerBlock (:159-163) in place on x, or — with ffn (b.ffn_fused) — its attention half in
+  // place and its feed-forward half from x into *ffn (which must not overlap x).
+  int block(const BlockW& b, View x, int Hh, int Ww, const View* ffn = nullptr) {
     const int HW = Hh * Ww;
     const int ln = h->cfg.layernorm_biasfree ? 1 : 2;
     const long long P = (long long)B * HW;
@@ -581,7 +588,7 @@ struct Fwd {
     HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
     HIPCHK(launch_attn_fold(buf(pl.red), gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
     View fpre{buf(pl.fpre), 2 * b.hidS};
-    const bool fuse_in = b.fused_attn_in;
+    const bool fuse_in = b.fused_attn_in && !ffn;
     if (fuse_in) {
       // x1 = x + M v written back into x, LN(x1) -> project_in into fpre, one kernel
       const Gemm& g0 = b.attn_in_split ? b.pin_g0 : b.pin;
@@ -628,6 +635,29 @@ struct Fwd {
     }
     // --- feed-forward
     if ((rc = tap(x, b.C, Hh, Ww))) return rc;  // x1 (diagnostics only)
+    if (ffn) {
+      FfnParams q{};
+      q.x = x.p;
+      q.ldx = x.ld;
+      q.out = ffn->p;
+      q.ldo = ffn->ld;
+      q.ln = ln;
+      q.hidS = b.hidS;
+      q.Win = h->P3(b.pin.w3);
+      q.bias_in = h->P(b.pin.bias);
+      q.dw = h->P(b.dwffn);
+      q.Wout = h->P3(b.pout.w3);
+      q.bias_out = h->P(b.pout.bias);
+      q.Bn = B;
+      q.H = Hh;
+      q.W = Ww;
+      if ((rc = probe_begin(3, b.C))) return rc;
+      tag = "ffn C" + std::to_string(b.C) + " hid" + std::to_string(b.hid) + " HW" + std::to_string(HW);
+      HIPCHK(launch_ffn_fused(q, b.C, s));
+      // algorithmic: read x1, write the block output; project_in, dwconv + gate, project_out FLOPs
+      return probe_end(3, b.C, 4.0 * P * 2.0 * b.C,
+                       2.0 * P * ((double)b.C * 2.0 * b.hid + 18.0 * b.hid + (double)b.hid * b.C));
+    }
     if (!fuse_in) {
       rc = gemm(b.pin, h->P3(b.pin.w3), 0, x, Hh, Ww, fpre, 0, nullptr, 0, ln, b.C, b.C);
       if (rc) return rc;
@@ -685,13 +715,26 @@ struct Fwd {
     }
     return KDLAE_OK;
   }
+  // A stage whose blocks all take the fused feed-forward half (an even count) ping-pongs between x and
+  // T = the project_in scratch (unused by the fused blocks), so its output lands in x.
   int stage(const std::vector<BlockW>& st, View x, int Hh, int Ww) {
     if (st.empty()) return KDLAE_OK;
     int rc = tap(x, st[0].C, Hh, Ww);
     if (rc) return rc;
-    for (const BlockW& b : st) {
-      if ((rc = block(b, x, Hh, Ww))) return rc;
-      if ((rc = tap(x, b.C, Hh, Ww))) return rc;
+    bool fused = st.size() % 2 == 0;
+    for (const BlockW& b : st) fused = fused && b.ffn_fused;
+    const View T{buf(pl.fpre), st[0].C};
+    View cur = x;
+    for (size_t i = 0; i < st.size(); ++i) {
+      const BlockW& b = st[i];
+      if (fused) {
+        const View nxt = (i % 2 == 0) ? T : x;
+        if ((rc = block(b, cur, Hh, Ww, &nxt))) return rc;
+        cur = nxt;
+      } else {
+        if ((rc = block(b, x, Hh, Ww))) return rc;
+      }
+      if ((rc = tap(cur, b.C, Hh, Ww))) return rc;
     }
     return KDLAE_OK;
   }

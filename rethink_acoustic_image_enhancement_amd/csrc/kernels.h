@@ -134,6 +134,24 @@ struct GdfnParams {
 bool gdfn_supported(int C, int hidS);
 hipError_t launch_gdfn_out(const GdfnParams& p, int C, hipStream_t s);
 
+// Fused feed-forward half (ffn.hip): out = x + project_out(gate(dwconv(project_in(LN(x))))) for C = 48 /
+// 96 — project_in recomputed on each tile's halo, so its 2 hidS-wide rows never reach HBM.  `out` must
+// not overlap x (neighbouring tiles read x as halo).
+struct FfnParams {
+  const float* x; int ldx;         // block input after the attention half (x1), [P][ldx]
+  float* out; int ldo;
+  int ln;                          // 1 BiasFree, 2 WithBias
+  int hidS;                        // padded hidden width
+  const float* Win;                // project_in split records [2 hidS / 16][C / 32 (round up)][kRec3], chunk-interleaved rows
+  const float* bias_in;            // [2 hidS] (chunk-interleaved) or null
+  const float* dw;                 // [hidS / 16][512] dw blocks (gdfn.hip layout)
+  const float* Wout;               // project_out split records [C / 16][hidS / 32][kRec3]
+  const float* bias_out;           // [C] or null
+  int Bn, H, W;
+};
+bool ffn_fused_supported(int C, int hidS);
+hipError_t launch_ffn_fused(const FfnParams& p, int C, hipStream_t s);
+
 
 // Pre/post-processing around the forward (pipeline.hip)
 struct PreParams {

@@ -175,6 +175,25 @@ def test_fused_attention_input_equals_unfused_bit_for_bit(ln, split, monkeypatch
     assert torch.equal(fused["hq"], unfused["hq"]) and torch.equal(fused["sr"], unfused["sr"])
 
 
+@pytest.mark.parametrize("ln,bias,shape", [
+    ("BiasFree", False, (3, 3, 48, 64)),    # full tiles; 3 images per launch
+    ("WithBias", True, (2, 3, 40, 56)),     # WithBias LN + conv biases; partial 16 x 8 tiles at the edges
+    ("BiasFree", False, (1, 3, 72, 40)),    # ragged width (40 = 2.5 tiles) and height
+])
+def test_fused_ffn_equals_unfused_bit_for_bit(ln, bias, shape, monkeypatch):
+    """ffn_fused_kernel (ffn.hip: LN + project_in recomputed on each tile's halo, dwconv + gate,
+    project_out, residual; output to the other buffer of a ping-pong pair) gives the same bits as the
+    unfused project_in GEMM + gdfn_out_kernel (KDLAE_DEBUG=no_ffn_fusion), for the C = 48 and C = 96
+    stages (every stage here has an even block count, so all of them take the fused kernel)."""
+    kw = dict(dim=48, LayerNorm_type=ln, num_blocks=[2, 2, 2, 2], num_refinement_blocks=2, bias=bias)
+    img = torch.from_numpy(hash_images("ffnf", shape))
+    rate = torch.from_numpy(hash_images("ffnfr", (shape[0], 1) + shape[2:]))
+    fused = _run(_model(kw), img, rate)
+    monkeypatch.setenv("KDLAE_DEBUG", "no_ffn_fusion")  # read when a new handle builds its blocks
+    unfused = _run(_model(kw), img, rate)
+    assert torch.equal(fused["hq"], unfused["hq"]) and torch.equal(fused["sr"], unfused["sr"])
+
+
 def test_weight_reload_is_picked_up():
     kw = dict(dim=16, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1)
     m = _model(kw)
