@@ -21,7 +21,7 @@ def _bench(*argv, timeout=240):
                           capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_gpus_n_runs_n_ranks(n):
     steps, B = 3, 4
     p = _bench("--gpus", str(n), "--cpu-standin", "--steps", str(steps), "--warmup", "1", "--batch", str(B),
@@ -42,6 +42,28 @@ def test_gpus_n_runs_n_ranks(n):
     assert res["elapsed_s"] >= max(r["local_s"] for r in ranks) - 1e-6
     assert res["elapsed_s"] >= steps * 0.01 * (n - 1)
     assert abs(res["value"] - n * B * steps / res["elapsed_s"]) <= 1e-3 * res["value"] + 1e-3
+
+
+def test_config5_width_under_torchrun():
+    """Config 5's width (KDLAE-T bs=128 over 8 ranks, 16 per rank; Train/train.sh:5) launched the way the
+    driver launches the scaling bench: torch.distributed.run --nproc-per-node 8, gloo stand-in.  The
+    gather must reassemble images 0..127 in rank order."""
+    n, B, steps = 8, 16, 2
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                        "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
+                        "--gpus", str(n), "--cpu-standin", "--steps", str(steps), "--warmup", "1", "--batch", str(B),
+                        "--size", "8"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == n and res["config"]["global_batch"] == 128 and res["config"]["per_gpu_batch"] == 16
+    ranks = sorted(res["standin"]["ranks"], key=lambda r: r["rank"])
+    assert [(r["first"], r["last"]) for r in ranks] == [(16 * i, 16 * i + 15) for i in range(n)]
+    assert res["standin"]["gather_equal"]
+    assert res["elapsed_s"] >= steps * 0.01 * (n - 1)
 
 
 def test_gpus_n_fails_without_enough_devices():
