@@ -284,6 +284,12 @@ def bench_secondary(args, world, rank, dev, distributed, workload, batch=0, size
     roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": "whole forward (all launches)",
             "algorithmic_flops_per_step": flops}
+    tr = pmc_workload_traffic(workload) if (B, H) == ((8, 512) if workload == "s8" else (64, 256)) else None
+    if tr is not None:  # HBM bytes of one forward of this exact batch, and the rate they imply here
+        roof["traffic"], roof["traffic_source"] = tr
+        roof["traffic_unit"] = "bytes per forward (all launches)"
+        roof["traffic_rate_GBps"] = round(tr[0] * args.steps / (dev_ms / 1e3) / 1e9, 1)
+        roof["traffic_frac_of_hbm"] = round(roof["traffic_rate_GBps"] / PEAK_HBM_GBS, 4)
     total = world * B * args.steps
     res = {"metric": metric, "value": round(total / elapsed, 3), "unit": "images/s" if workload == "a64"
            else "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -766,6 +772,18 @@ def pmc_traffic(cls):
     if not c:
         return None
     return c["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
+def pmc_workload_traffic(workload):
+    """HBM bytes of one whole S8 / A64 forward from the committed PMC pass (profiles/rNN_pmc_<w>.json,
+    tools/pmc_workload.py: FETCH_SIZE x2 + WRITE_SIZE, weight packing excluded); latest round wins."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d["traffic_bytes_per_forward"], os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(model, batch, out, threads):

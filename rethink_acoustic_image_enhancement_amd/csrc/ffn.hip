@@ -62,6 +62,24 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+#ifdef KDLAE_FFN_STAMPS
+// Diagnostic build only (tools/ffn_stamps.py): per-segment cycle sums of every wave, [C48 / C96][P / G]
+// [segment]; the stamps fence the schedule, so read shares, not lengths.
+__device__ unsigned long long g_ffn_stamps[2][2][8];
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define FFN_ST(v) const unsigned long long v = stamp()
+#define FFN_ADD(k, d) seg[k] += (d)
+#else
+#define FFN_ST(v)
+#define FFN_ADD(k, d)
+#endif
+
 template <int C>
 struct FfnShape {
   static constexpr int KG = C / 16;          // k-groups of project_in
@@ -100,6 +118,10 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
   const int xcd = (int)(blockIdx.x & 7), nxb = (int)(gridDim.x >> 3), xb = (int)(blockIdx.x >> 3);
   const int t_lo = (int)((long long)ntiles * xcd / 8), t_hi = (int)((long long)ntiles * (xcd + 1) / 8);
   if (t_lo + xb >= t_hi) return;  // block-uniform
+#ifdef KDLAE_FFN_STAMPS
+  unsigned long long seg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  FFN_ST(k0);
+#endif
 
   // resident: every chunk's dw block, both biases
   for (int i = tid; i < kch * kDwF4; i += 512) lds[S::kDw + i] = reinterpret_cast<const f32x4*>(p.dw)[i];
@@ -253,9 +275,12 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
       lds_barrier();  // B_0
       const bool more = t + nxb < t_hi;
       for (int g = 0; g < kch; ++g) {
+        FFN_ST(s0);
         // W-in slot g & 1 was last read by pin(g) (before B_g): chunk g + 2 (mod kch: the next tile)
         issue_win((g + 2) % kch);
+        FFN_ST(s1);
         if (g + 1 < kch) pin(g + 1);
+        FFN_ST(s2);
         if (g == kch - 1) {
           if (more) load_x1(t + nxb);  // the next tile's rows, during this chunk and the G epilogue
           // past B_kch pin(0) of the next tile reads W-in slot 0 (issued at chunk kch - 2): at most this
@@ -269,7 +294,13 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
         } else {
           wait_vm<0>();  // W-in of chunk g + 2 (read by pin(g + 2) in the next chunk)
         }
+        FFN_ST(s3);
         lds_barrier();  // B_{g+1}
+        FFN_ST(s4);
+        FFN_ADD(0, s1 - s0);
+        FFN_ADD(1, s2 - s1);
+        FFN_ADD(2, s3 - s2);
+        FFN_ADD(3, s4 - s3);
       }
     }
   } else {
@@ -301,11 +332,14 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
       lds_barrier();  // B_0: chunk 0's image
       for (int g = 0; g < kch; ++g) {
         const f32x4* sl = lds + (g & 1) * kImg;
+        FFN_ST(s0);
         // chunk 2j (even): the W of pair j + 1 (or of the next tile's pair 0) into the other W slot;
         // its last reader, pair j - 1, finished before this chunk's barrier
         if ((g & 1) == 0) issue_w((g >> 1) + 1 < npairs ? (g >> 1) + 1 : 0, (pc + 1) & 1);
+        FFN_ST(s1);
         f32x4 gn[kRPW];
         gate_rows<kRPW, kGeluPacked>(sl, lds + S::kDw + g * kDwF4, lo, lq, gn);
+        FFN_ST(s2);
         if (g & 1) {
           mfma_pair(gbp, gn, pc & 1);  // chunks g - 1, g
           ++pc;
@@ -321,7 +355,13 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
           else
             wait_w(std::integral_constant<int, 0>{});
         }
+        FFN_ST(s3);
         lds_barrier();  // B_{g+1}: the next chunk's image
+        FFN_ST(s4);
+        FFN_ADD(0, s1 - s0);
+        FFN_ADD(1, s2 - s1);
+        FFN_ADD((g & 1) ? 2 : 5, s3 - s2);
+        FFN_ADD(3, s4 - s3);
       }
       // epilogue: y = acc + x1 + bias (gdfn_out's order); rows / columns past the image dropped
       const int xo = x0 + li;
@@ -351,7 +391,32 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) W DMA lands before exit
+#ifdef KDLAE_FFN_STAMPS
+  FFN_ST(k1);
+  seg[7] = k1 - k0;
+  seg[6] = seg[7] - seg[0] - seg[1] - seg[2] - seg[3] - seg[5];  // tile prologue / epilogue, rest
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      unsigned long long v = seg[k];
+      v = (unsigned)__builtin_amdgcn_readfirstlane((int)v) |
+          ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32);
+      atomicAdd(&g_ffn_stamps[C == 96][gw ? 1 : 0][k], v);
+    }
+  }
+#endif
 }
+
+#ifdef KDLAE_FFN_STAMPS
+extern "C" int kdlae_debug_ffn_stamps(unsigned long long* out, int reset) {
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ffn_stamps), sizeof(g_ffn_stamps)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long zero[2][2][8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ffn_stamps), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // an even chunk count (the released config: hidS = 128 / 256), so every pair is full
 bool ffn_fused_supported(int C, int hidS) {

@@ -71,6 +71,16 @@ probe)  # a tools/ probe script (args: script [script args]), then the same unde
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $s "$@" > $O/prof_probe.log 2>&1 || exit $?
   ;;
+pmc_sec)  # FETCH_SIZE / WRITE_SIZE passes over one S8 and one A64 forward -> profiles-ready json
+  cd /tmp && export TMPDIR=/tmp
+  for w in s8 a64; do
+    B="python3 $R/bench.py --workload $w --steps 1 --warmup 0 --no-cpu-baseline"
+    timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${w}_fetch -o run -- $B > $O/${w}_fetch.log 2>&1 || exit $?
+    timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${w}_write -o run -- $B > $O/${w}_write.log 2>&1 || exit $?
+    python3 $R/tools/pmc_workload.py $(ls $O/${w}_fetch/*counter_collection.csv | head -1) \
+      $(ls $O/${w}_write/*counter_collection.csv | head -1) $O/pmc_$w.json $w || exit $?
+  done
+  ;;
 pmc)
   cd /tmp && export TMPDIR=/tmp
   B="python3 $R/bench.py --steps 1 --warmup 0 --probe 0 --no-cpu-baseline --no-bs1 --no-secondary"

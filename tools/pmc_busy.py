@@ -26,6 +26,8 @@ CLASSES = [("conv_gemm_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
            ("gemm_chunk_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
            ("gemm_attn_in_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
            ("dwconv_gram", "dwconv_gram (MDTA pass 1: dwconv + MFMA Gram)"),
+           ("ffn_fused_kernel<96>", "ffn_fused C96 (LN + project_in + gate + project_out)"),
+           ("ffn_fused_kernel<48>", "ffn_fused C48 (LN + project_in + gate + project_out)"),
            ("gdfn_out_kernel", "gdfn_out (fused GDFN tail: dwconv + gate + MFMA project_out)"),
            ("gdfn2_kernel", "gdfn_out (fused GDFN tail: dwconv + gate + MFMA project_out)"),
            ("dwconv_gate_kernel", "dwconv_gate (unfused GDFN gate, C >= 192)"),

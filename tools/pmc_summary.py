@@ -12,7 +12,7 @@ import json
 import sys
 
 CLASSES = {"conv_gemm_kernel": 1, "gemm_res_kernel": 1, "gemm_chunk_kernel": 1, "gemm_attn_in_kernel": 1, "dwconv_gram": 2,
-           "dwconv_gate_kernel": 3, "gdfn_out_kernel": 3, "gdfn2_kernel": 3}
+           "dwconv_gate_kernel": 3, "ffn_fused_kernel": 3, "gdfn_out_kernel": 3, "gdfn2_kernel": 3}
 
 
 def load(path, counter):
