@@ -637,6 +637,14 @@ def main():
                 ach = by.value / sec / 1e9
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
+            if fl.value:  # the FLOP side of the same launches, against both fp32-product peaks
+                tf = fl.value / sec / 1e12
+                roof["compute_view"] = {"achieved_tflops": round(tf, 2),
+                                        "frac_of_split_bf16_peak": round(tf / PEAK_SPLIT_TFLOPS, 4),
+                                        "frac_of_fp32_mfma_peak": round(tf / PEAK_FP32_TFLOPS, 4),
+                                        "note": "fp32-accurate products; the split-bf16 peak (419.4) is the "
+                                                "ceiling of this arithmetic, the fp32 MFMA peak (157.3) the "
+                                                "ceiling of the r04 kernels"}
             tr = pmc_traffic(args.probe)
             if tr is not None:
                 roof["traffic"], roof["traffic_source"] = tr
