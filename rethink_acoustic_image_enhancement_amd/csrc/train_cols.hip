@@ -4,18 +4,22 @@
 // :127, :143) and the MDTA Gram G = q^T k / dA = dout^T v per (image, head) (KDLAE_model.py:137-138).
 // Both operands are NHWC rows (channels contiguous): A(m, p) = A[p * lda + m], B(p, n) = B[p * ldb + n].
 //
-// v_mfma_f32_16x16x4_f32 takes its k (= pixel) index from lane >> 4 for both operands, so lane
-// (li, lq) supplies A[pixel 4j + lq][16i + li] and B[pixel 4j + lq][16t + li]: one dword per
-// operand tile per k-step, straight from HBM into VGPRs (16 lanes read 64 contiguous bytes of one
-// pixel row; the tiles of a wave cover whole lines).  A wave owns TM x TN accumulator tiles over a
-// pixel chunk; each loaded A value feeds TN MFMAs and each B value TM, so the wave moves
-// (TM + TN) x 256 B per TM x TN MFMAs.  The four waves of a block take neighbouring wave tiles of
+// Products on the bf16 matrix cores in the exact-split form of every inference GEMM (mfma3.h: each
+// fp32 operand split into three bf16 planes, six v_mfma_f32_16x16x32_bf16 per 32-deep step, as
+// accurate as an fp32 fma chain at 2.67x the f32 MFMA rate).  The MFMA takes k index 8 (lane >> 4)
+// + j (j < 8) for both operands; any pixel order serves a contraction as long as A and B share it, so
+// lane (li, lq) supplies A[pixel 4j + lq][16i + li] and B[pixel 4j + lq][16t + li], j = 0..7: one
+// dword per operand tile per 4-pixel step, straight from HBM into VGPRs (16 lanes read 64 contiguous
+// bytes of one pixel row; the tiles of a wave cover whole lines), the 8 dwords of a 32-pixel stage
+// split in registers.  A wave owns TM x TN accumulator tiles over a pixel chunk; each loaded A value
+// feeds TN MFMAs and each B value TM, so the wave moves (TM + TN) x 256 B per 4-pixel step.  The four waves of a block take neighbouring wave tiles of
 // the same pixel chunk (their rows meet in L1/L2).  Pixel chunks are split-K partials
 // [batch][chunk][M][N], summed in fixed order by tgemm_reduce_kernel: deterministic.
 // Loads are unconditional buffer ops (rows past P / channels past M, N read 0 through the
 // descriptor range), so the prefetch of the next k-steps is never drained by a dynamic vmcnt.
 #include <stdint.h>
 
+#include "mfma3.h"
 #include "train_kernels.h"
 
 namespace kdlae {
@@ -26,7 +30,7 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;  // at most 4 waves
-constexpr int kU = 4;          // k-steps (4 pixels each) per pipeline stage
+constexpr int kU = 8;          // k-steps (4 pixels each) per pipeline stage = one 32-deep MFMA step
 
 struct ColsArgs {
   TGemm g;
@@ -36,9 +40,6 @@ struct ColsArgs {
   int wtm, wtn;   // wave tiles along M and N
 };
 
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, long long bytes) {
   const long long cap = 0x7fffff00LL;
@@ -100,57 +101,63 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_cols_kernel(ColsArgs a) {
 
   // stage = kU k-steps = 4 kU pixels: lane reads pixel q + 4u + lq for u < kU
   auto load = [&](int q, float (&av)[kU][TM], float (&bv)[kU][TN]) {
-    // IMPB: the stage's 16 pixels q .. q + 15 lie in one image row (q % 16 == 0, W % 16 == 0)
-    [[maybe_unused]] int x0 = 0, y = 0, f = 0;
-    [[maybe_unused]] bool rok[TN];
-    if constexpr (IMPB) {
-      const int row = q / g.W;
-      x0 = q - row * g.W;
-      y = row % g.H;
-      f = (row / g.H) % g.F;
 #pragma unroll
-      for (int t = 0; t < TN; ++t)
-        rok[t] = (unsigned)(f + tdf[t]) < (unsigned)g.F && (unsigned)(y + tdy[t]) < (unsigned)g.H;
-    }
+    for (int hf = 0; hf < kU / 4; ++hf) {
+      // IMPB: the 16 pixels qh .. qh + 15 lie in one image row (qh % 16 == 0, W % 16 == 0)
+      const int qh = q + 16 * hf;
+      [[maybe_unused]] int x0 = 0, y = 0, f = 0;
+      [[maybe_unused]] bool rok[TN];
+      if constexpr (IMPB) {
+        const int row = qh / g.W;
+        x0 = qh - row * g.W;
+        y = row % g.H;
+        f = (row / g.H) % g.F;
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const unsigned pa = (unsigned)(q + 4 * u) * sa, pb = (unsigned)(q + 4 * u) * sb;
+        for (int t = 0; t < TN; ++t)
+          rok[t] = (unsigned)(f + tdf[t]) < (unsigned)g.F && (unsigned)(y + tdy[t]) < (unsigned)g.H;
+      }
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        av[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, (int)(am[i] + pa), 0, 0));
+      for (int uu = 0; uu < 4; ++uu) {
+        const int u = 4 * hf + uu;
+        const unsigned pa = (unsigned)(q + 4 * u) * sa, pb = (unsigned)(q + 4 * u) * sb;
 #pragma unroll
-      for (int t = 0; t < TN; ++t) {
-        unsigned off;
-        if constexpr (IMPB) {
-          const int x = x0 + 4 * u + lq;
-          const bool ok = rok[t] && (unsigned)(x + tdx[t]) < (unsigned)g.W && bn[t] != kOOB;
-          off = ok ? (unsigned)(q + 4 * u + lq + tdel[t]) * sb + bn[t] : kOOB;
-        } else {
-          off = bn[t] + pb;
+        for (int i = 0; i < TM; ++i)
+          av[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, (int)(am[i] + pa), 0, 0));
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          unsigned off;
+          if constexpr (IMPB) {
+            const int x = x0 + 4 * uu + lq;
+            const bool ok = rok[t] && (unsigned)(x + tdx[t]) < (unsigned)g.W && bn[t] != kOOB;
+            off = ok ? (unsigned)(q + 4 * u + lq + tdel[t]) * sb + bn[t] : kOOB;
+          } else {
+            off = bn[t] + pb;
+          }
+          bv[u][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (int)off, 0, 0));
         }
-        bv[u][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (int)off, 0, 0));
       }
     }
   };
-  auto compute = [&](const float (&av)[kU][TM], const float (&bv)[kU][TN]) {
-#pragma unroll
-    for (int u = 0; u < kU; ++u)
+  // One 32-deep step per stage: k index j of lane lq = pixel q + 4j + lq for both operands.  The raw
+  // stage is split into bf16 planes first, then the next stage loads into the same registers while
+  // this stage's MFMAs run (1.5 buffers: the planes and one raw stage).
+  constexpr int kStage = 4 * kU;
+  float av[kU][TM], bv[kU][TN];
+  if (p0 < p1) {
+    load(p0, av, bv);
+    for (int q = p0; q < p1; q += kStage) {
+      F3 xa[TM], xb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
+        xa[i] = split3(f32x4{av[0][i], av[1][i], av[2][i], av[3][i]}, f32x4{av[4][i], av[5][i], av[6][i], av[7][i]});
 #pragma unroll
-        for (int t = 0; t < TN; ++t) acc[i][t] = mfma4(av[u][i], bv[u][t], acc[i][t]);
-  };
-
-  constexpr int kStage = 4 * kU;
-  float a0[kU][TM], b0[kU][TN], a1[kU][TM], b1[kU][TN];
-  if (p0 < p1) {
-    load(p0, a0, b0);
-    for (int q = p0; q < p1; q += 2 * kStage) {
-      if (q + kStage < p1) load(q + kStage, a1, b1);
-      compute(a0, b0);
-      if (q + kStage >= p1) break;
-      if (q + 2 * kStage < p1) load(q + 2 * kStage, a0, b0);
-      compute(a1, b1);
+      for (int t = 0; t < TN; ++t)
+        xb[t] = split3(f32x4{bv[0][t], bv[1][t], bv[2][t], bv[3][t]}, f32x4{bv[4][t], bv[5][t], bv[6][t], bv[7][t]});
+      if (q + kStage < p1) load(q + kStage, av, bv);
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][t] = mfma6(xa[i], xb[t], acc[i][t]);
     }
   }
   // partial [z][ks][M][N]: lane (li, lq) of (i, t) holds rows 16(wm TM + i) + 4lq + r, column 16(wn TN + t) + li

@@ -4,18 +4,22 @@
 // (KDLAE_model.py:99-106, :124-145 and their derivatives).
 //
 // The inference GEMM's layout (gemm.hip) with the weights taken raw: a block stages its NT output
-// tiles' weights for the whole K into LDS once, in MFMA fragment order (tile t, k-group g: lane
-// (li, lq) holds B(16g + 4lq + s, 16t + li), s = 0..3), straight from the caller's B (the flat
-// parameter buffer, or an attention matrix) — no packed copy to refresh after an optimizer step.
-// A rows stream HBM -> VGPRs as float4 (lane: pixel li, channels 16g + 4lq..+3), which IS the
-// v_mfma_f32_16x16x4_f32 B-operand layout, so A never touches LDS; the next (row tile, k-chunk)'s
-// A registers load while the current one's MFMAs run.  The accumulator of (tile t, subtile r) holds
-// output channels 16t + 4lq..+3 of pixel 16r + li: one float4 store per lane.  A block walks row
-// tiles with a grid stride, so the weight staging is paid once per block, not per tile.
-// Summation order per output: k-group ascending, k-step ascending, one fp32 accumulator; bias, then
-// the residual added after the K sum (as the generic kernel's epilogue does).
+// tiles' weights for the whole K into LDS once, split into bf16 planes in split fragment order
+// (mfma3.h: record (tile t, k-group pair G) = planes h, m, l of lane (li, lq) holding
+// B(32G + 4lq + j, 16t + li), j < 4, and B(32G + 16 + 4lq + j - 4, 16t + li), j >= 4), straight from
+// the caller's B (the flat parameter buffer, or an attention matrix) — no packed copy to refresh after
+// an optimizer step.  A rows stream HBM -> VGPRs as float4 (lane: pixel li, channels 16g + 4lq..+3);
+// two k-groups' float4 split in registers ARE the v_mfma_f32_16x16x32_bf16 B operand, so A never
+// touches LDS; the next (row tile, k-chunk)'s A registers load while the current one's MFMAs run.
+// The accumulator of (tile t, subtile r) holds output channels 16t + 4lq..+3 of pixel 16r + li: one
+// float4 store per lane.  A block walks row tiles with a grid stride, so the weight staging is paid
+// once per block, not per tile.
+// Products: the split-bf16 form of every inference GEMM (mfma3.h: six bf16 MFMAs per 32-deep pair,
+// as accurate as an fp32 fma chain, 2.67x the f32 MFMA rate).  Summation order per output: pair
+// ascending, mfma6 term order; bias, then the residual added after the K sum.
 #include <stdint.h>
 
+#include "mfma3.h"
 #include "train_kernels.h"
 
 namespace kdlae {
@@ -35,14 +39,11 @@ struct RowsArgs {
   TGemm g;
   int ncb, gx;    // column blocks, row-block slots (grid.x = ncb * gx rounded up to 8)
   int kg;         // k-groups: ceil(K / 16)
+  int kp;         // k-group pairs: ceil(kg / 2)
   int nchunk;     // ceil(kg / kKC)
   int row_tiles;  // ceil(M / kTileRows)
   int klast;      // K - 16 (kg - 1): valid k in the last group (16 = full)
 };
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, long long bytes) {
   const long long cap = 0x7fffff00LL;
@@ -57,7 +58,7 @@ constexpr unsigned kOOB = 0x80000000u;  // past every descriptor's range: loads 
 // (2 waves per SIMD: the r03 sweep measured a 1-wave-per-SIMD register budget slower)
 template <int NT, bool HASR, bool VECC>
 __global__ __launch_bounds__(kThreads, 2) void tgemm_rows_kernel(RowsArgs a) {
-  // [NT][kg][64] fragments, then [NT][4] bias and [NT][4] residual scale
+  // [NT][kp] split records (3 KiB), then [NT][4] bias and [NT][4] residual scale
   extern __shared__ __attribute__((aligned(16))) f32x4 wl[];
   const TGemm& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -76,26 +77,36 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_rows_kernel(RowsArgs a) {
   const int n0 = cbk * NT * 16;
   const int z = blockIdx.z, z1 = z / g.nz2, z2 = z - z1 * g.nz2;
 
-  // ---- stage this block's weight fragments, bias and residual scale
+  // ---- stage this block's weight records (split), bias and residual scale
+  const int kp = a.kp;
   const float* B = g.B + z1 * g.bB1 + z2 * g.bB2;
   const bool bk1 = g.sbk == 1 && ((uintptr_t)B & 15) == 0 && (g.sbn & 3) == 0;
-  for (int idx = tid; idx < NT * kg * 64; idx += kThreads) {
+  for (int idx = tid; idx < NT * kp * 64; idx += kThreads) {
     const int l = idx & 63, tg = idx >> 6;
-    const int t = tg / kg, gg = tg - t * kg;
-    const int n = n0 + 16 * t + (l & 15), k = 16 * gg + 4 * (l >> 4);
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (n < g.N) {
-      if (bk1 && k + 3 < g.K) {
-        v = *reinterpret_cast<const f32x4*>(B + (long long)n * g.sbn + k);
-      } else {
+    const int t = tg / kp, G = tg - t * kp;
+    const int n = n0 + 16 * t + (l & 15);
+    f32x4 v[2];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (k + e < g.K) v[e] = B[(long long)(k + e) * g.sbk + (long long)n * g.sbn];
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * G + 16 * h + 4 * (l >> 4);
+      v[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (n < g.N) {
+        if (bk1 && k + 3 < g.K) {
+          v[h] = *reinterpret_cast<const f32x4*>(B + (long long)n * g.sbn + k);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (k + e < g.K) v[h][e] = B[(long long)(k + e) * g.sbk + (long long)n * g.sbn];
+        }
       }
     }
-    wl[idx] = v;
+    const F3 w = split3(v[0], v[1]);
+    f32x4* rec = wl + (long long)(t * kp + G) * kRec3 + l;
+    rec[0] = __builtin_bit_cast(f32x4, w.h);
+    rec[64] = __builtin_bit_cast(f32x4, w.m);
+    rec[128] = __builtin_bit_cast(f32x4, w.l);
   }
-  f32x4* bl = wl + NT * kg * 64;
+  f32x4* bl = wl + NT * kp * kRec3;
   const float* rs = g.rs ? g.rs + z1 * g.brs1 + z2 * g.brs2 : nullptr;
   for (int idx = tid; idx < NT * 8; idx += kThreads) {
     const int which = idx / (NT * 4), qi = idx - which * NT * 4;
@@ -188,16 +199,17 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_rows_kernel(RowsArgs a) {
               if (e >= kv_last) av[r][gi][e] = 0.f;
     }
 #pragma unroll
-    for (int gi = 0; gi < kKC; ++gi) {
-      const int gg = ch * kKC + gi;
-      if (gg < kg) {
+    for (int pi = 0; pi < kKC / 2; ++pi) {
+      const int G = ch * (kKC / 2) + pi;  // (k-groups past kg were loaded as zeros)
+      if (G < kp) {
+        F3 xs[kRT];
+#pragma unroll
+        for (int r = 0; r < kRT; ++r) xs[r] = split3(av[r][2 * pi], av[r][2 * pi + 1]);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          const f32x4 w = wl[(t * kg + gg) * 64 + lane];
+          const F3 w = load_w3(wl + (t * kp + G) * kRec3, lane);
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int r = 0; r < kRT; ++r) acc[t][r] = mfma4(w[s], av[r][gi][s], acc[t][r]);
+          for (int r = 0; r < kRT; ++r) acc[t][r] = mfma6(w, xs[r], acc[t][r]);
         }
       }
     }
@@ -319,8 +331,8 @@ bool tgemm_rows_eligible(const TGemm& g) {
   if ((long long)g.M * g.sam * 4 >= (1LL << 31) - 64 || (long long)g.M * g.scm * 4 >= (1LL << 31) - 64 ||
       (g.R && (long long)g.M * g.srm * 4 >= (1LL << 31) - 64))
     return false;
-  const int kg = (g.K + 15) / 16;
-  if (kg > 128) return false;  // NT = 1 keeps at most 128 KiB of fragments
+  const int kp = (g.K + 31) / 32;
+  if (kp > 48) return false;  // NT = 1 keeps at most 144 KiB of split records
   return true;
 }
 
@@ -329,6 +341,7 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   RowsArgs a;
   a.g = g;
   a.kg = (g.K + 15) / 16;
+  a.kp = (a.kg + 1) / 2;
   a.nchunk = (a.kg + kKC - 1) / kKC;
   a.row_tiles = (g.M + kTileRows - 1) / kTileRows;
   a.klast = g.K - 16 * (a.kg - 1);
@@ -336,7 +349,7 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   const bool vecc = al16(g.C) && m4(g.scm) && m4(g.bC1) && m4(g.bC2) &&
                     (g.N % 4 == 0 || (g.c_pad_ok && g.scm >= (g.N + 3) / 4 * 4));
   // output tiles per block: one column block when the N tiles fit (A read once), else the width
-  // with the least padding; LDS for the fragments <= 96 KiB (NT * kg KiB)
+  // with the least padding; LDS for the split records <= 96 KiB (3 NT kp KiB)
   const int ntiles = (g.N + 15) / 16;
   // (residual variants: NT <= 4, the residual registers of wider tiles spill)
   static const int nts[] = {8, 6, 4, 3, 2, 1};
@@ -347,12 +360,12 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   int NT = 1;
   if (ntiles <= ntmax) {
     for (int c : nts)
-      if (c <= ntmax && c >= ntiles && c * a.kg <= 96) NT = c;
+      if (c <= ntmax && c >= ntiles && 3 * c * a.kp <= 96) NT = c;
   }
   if (NT < ntiles) {
     int best = -1, best_pad = 1 << 30;
     for (int c : nts) {
-      if (c > ntmax || (c * a.kg > 96 && c > 1)) continue;
+      if (c > ntmax || (3 * c * a.kp > 96 && c > 1)) continue;
       const int pad = (ntiles + c - 1) / c * c;
       if (pad < best_pad) best = c, best_pad = pad;
     }
@@ -360,7 +373,7 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   }
   const int ncb = (ntiles + NT - 1) / NT;
   const int nz = g.nz1 * g.nz2;
-  const size_t lds = (size_t)NT * a.kg * 1024 + (size_t)NT * 128;
+  const size_t lds = (size_t)NT * a.kp * 3072 + (size_t)NT * 128;
   a.ncb = ncb;
   a.gx = 1;
 #define NTCASE(n)                                                            \
