@@ -62,6 +62,25 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+#ifndef KDLAE_FFN_UNIFORM_DMA
+#define KDLAE_FFN_UNIFORM_DMA 48
+#endif
+// every wave issues the same number of DMA pieces, straight-line (piece k = w + 4 j; the padding
+// pieces past the chunk's last read nothing and land in a dummy slot): no per-piece branch.  A/B
+// (profiles/r05r_ffn_dma_ab.txt): C = 48 -5%, C = 96 +4% (3 more spilled VGPRs), so C = 48 only
+// (the knob: 0 = never, 1 = both widths, 48 / 96 = that width)
+template <int C>
+constexpr bool uniform_dma() {
+  return KDLAE_FFN_UNIFORM_DMA == 1 || KDLAE_FFN_UNIFORM_DMA == C;
+}
+#ifndef KDLAE_FFN_PIN_PIPE
+#define KDLAE_FFN_PIN_PIPE 1
+#endif
+constexpr bool kPinPipe = KDLAE_FFN_PIN_PIPE != 0;  // project_in W planes read one step ahead
+#ifndef KDLAE_FFN_ABL
+#define KDLAE_FFN_ABL 0  // timing-only ablations (wrong outputs): 1 no gate, 2 no gate + no project_out,
+                         // 3 no project_in in the chunk loop
+#endif
 #ifdef KDLAE_FFN_STAMPS
 // Diagnostic build only (tools/ffn_stamps.py): per-segment cycle sums of every wave, [C48 / C96][P / G]
 // [segment]; the stamps fence the schedule, so read shares, not lengths.
@@ -82,6 +101,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 template <int C>
 struct FfnShape {
+  static constexpr bool kUniformDma = uniform_dma<C>();
   static constexpr int KG = C / 16;          // k-groups of project_in
   static constexpr int KP = (KG + 1) / 2;    // split pairs of project_in
   static constexpr int NTO = C / 16;         // project_out output tiles
@@ -93,11 +113,12 @@ struct FfnShape {
   static constexpr int kBout = kBin + KCH * 8;
   static constexpr int kWin = kBout + NTO * 4;                 // 2 slots of one chunk's project_in records
   static constexpr int kWinSlot = 2 * KP * kRec3;              // (tiles 2g, 2g + 1) x KP pairs
-  static constexpr int kLds = (kWin + 2 * kWinSlot) * 16;
+  static constexpr int kDummy = kWin + 2 * kWinSlot;           // 1 KiB landing slot of padding DMA pieces
+  static constexpr int kLds = (kDummy + (kUniformDma ? 64 : 0)) * 16;
   // project_out W pieces (1 KiB) of one pair dealt over the 4 G waves: piece k -> wave k % 4
-  static constexpr int pw(int w) { return (3 * NTO - w + 3) / 4; }
+  static constexpr int pw(int w) { return kUniformDma ? (3 * NTO + 3) / 4 : (3 * NTO - w + 3) / 4; }
   // project_in pieces of one chunk dealt over the 4 P waves
-  static constexpr int pwin(int w) { return (6 * KP - w + 3) / 4; }
+  static constexpr int pwin(int w) { return kUniformDma ? (6 * KP + 3) / 4 : (6 * KP - w + 3) / 4; }
 };
 
 }  // namespace
@@ -140,13 +161,25 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
       const_cast<float*>(p.Wout), 0, NTO * npairs * kRec3 * 16, 0x00020000);
   auto issue_w = [&](int pair, int slot) {
     f32x4* dst = lds + S::kW + slot * (NTO * kRec3);
+    if constexpr (S::kUniformDma) {
 #pragma unroll
-    for (int k = 0; k < 3 * NTO; ++k)
-      if (k % 4 == wi) {
+      for (int j = 0; j < (3 * NTO + 3) / 4; ++j) {
+        const int k = wi + 4 * j;
+        const bool real = k < 3 * NTO;
         const int t = k / 3, pl = k - 3 * t;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lptr_f)(dst + 64 * k), 16, (int)(16u * lane),
-                                                 ((t * npairs + pair) * 3 + pl) * 1024, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lptr_f)(real ? dst + 64 * k : lds + S::kDummy), 16,
+                                                 (int)(real ? 16u * lane : kOOBf),
+                                                 real ? ((t * npairs + pair) * 3 + pl) * 1024 : 0, 0, 0);
       }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3 * NTO; ++k)
+        if (k % 4 == wi) {
+          const int t = k / 3, pl = k - 3 * t;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lptr_f)(dst + 64 * k), 16, (int)(16u * lane),
+                                                   ((t * npairs + pair) * 3 + pl) * 1024, 0, 0);
+        }
+    }
   };
   // wait until at most N VMEM ops of this G wave are outstanding (exact per-wave counts)
   auto wait_w = [&](auto extra) {
@@ -185,14 +218,27 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
       const_cast<float*>(p.Win), 0, 2 * kch * KP * kRec3 * 16, 0x00020000);
   auto issue_win = [&](int g) {
     f32x4* dst = lds + S::kWin + (g & 1) * S::kWinSlot;
+    if constexpr (S::kUniformDma) {
 #pragma unroll
-    for (int k = 0; k < 6 * KP; ++k)
-      if (k % 4 == wi) {  // piece k = (tile j = k / (3 KP), pair G, plane) of records (2g + j, G)
+      for (int i = 0; i < (6 * KP + 3) / 4; ++i) {
+        const int k = wi + 4 * i;  // piece k = (tile j = k / (3 KP), pair G, plane) of records (2g + j, G)
+        const bool real = k < 6 * KP;
         const int j = k / (3 * KP), rem = k - j * 3 * KP;
         const int G = rem / 3, pl = rem - 3 * G;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rwin, (lptr_f)(dst + 64 * k), 16, (int)(16u * lane),
-                                                 (((2 * g + j) * KP + G) * 3 + pl) * 1024, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rwin, (lptr_f)(real ? dst + 64 * k : lds + S::kDummy), 16,
+                                                 (int)(real ? 16u * lane : kOOBf),
+                                                 real ? (((2 * g + j) * KP + G) * 3 + pl) * 1024 : 0, 0, 0);
       }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6 * KP; ++k)
+        if (k % 4 == wi) {  // piece k = (tile j = k / (3 KP), pair G, plane) of records (2g + j, G)
+          const int j = k / (3 * KP), rem = k - j * 3 * KP;
+          const int G = rem / 3, pl = rem - 3 * G;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rwin, (lptr_f)(dst + 64 * k), 16, (int)(16u * lane),
+                                                   (((2 * g + j) * KP + G) * 3 + pl) * 1024, 0, 0);
+        }
+    }
   };
   f32x4 a[3][KG];  // P waves: the x1 rows of the next tile (loaded ahead)
   auto load_x1 = [&](int t) {
@@ -259,8 +305,47 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
         f32x4 a1[3], a2[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) a1[k] = a2[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (kPinPipe) {
+          // the W planes one step ahead of their MFMAs (steps = (pair, plane l / m / h): mfma6_pair's
+          // term order), fenced so each step's reads issue under the previous step's MFMAs
+          bf16x8 w[2][2];
+          auto ld = [&](int st, int buf) {
+            const int G = st / 3, off = (2 - (st - 3 * G)) * 64;  // planes l, m, h at +128, +64, +0
+            w[buf][0] = __builtin_bit_cast(bf16x8, wl[G * kRec3 + off]);
+            w[buf][1] = __builtin_bit_cast(bf16x8, wl[(KP + G) * kRec3 + off]);
+          };
+          ld(0, 0);
 #pragma unroll
-        for (int G = 0; G < KP; ++G) mfma6_pair<3, true>(wl + G * kRec3, wl + (KP + G) * kRec3, xs[G], a1, a2);
+          for (int st = 0; st < 3 * KP; ++st) {
+            if (st + 1 < 3 * KP) ld(st + 1, (st + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+            const int G = st / 3, pl = st - 3 * G;
+            const bf16x8 p0 = w[st & 1][0], p1 = w[st & 1][1];
+            if (pl == 2) {
+#pragma unroll
+              for (int r = 0; r < 3; ++r) {
+                a1[r] = mfma_bf(p0, xs[G][r].l, a1[r]);
+                a2[r] = mfma_bf(p1, xs[G][r].l, a2[r]);
+              }
+            }
+            if (pl >= 1) {
+#pragma unroll
+              for (int r = 0; r < 3; ++r) {
+                a1[r] = mfma_bf(p0, xs[G][r].m, a1[r]);
+                a2[r] = mfma_bf(p1, xs[G][r].m, a2[r]);
+              }
+            }
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+              a1[r] = mfma_bf(p0, xs[G][r].h, a1[r]);
+              a2[r] = mfma_bf(p1, xs[G][r].h, a2[r]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {
+#pragma unroll
+          for (int G = 0; G < KP; ++G) mfma6_pair<3, true>(wl + G * kRec3, wl + (KP + G) * kRec3, xs[G], a1, a2);
+        }
         const f32x4 b1 = lds[S::kBin + 4 * (2 * g) + lq], b2 = lds[S::kBin + 4 * (2 * g + 1) + lq];
         f32x4* img = lds + (g & 1) * kImg;
 #pragma unroll
@@ -279,7 +364,11 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
         // W-in slot g & 1 was last read by pin(g) (before B_g): chunk g + 2 (mod kch: the next tile)
         issue_win((g + 2) % kch);
         FFN_ST(s1);
+#if KDLAE_FFN_ABL == 3
+        if (g + 1 < kch && lds[0].x == 12345.f) pin(g + 1);  // ablation: (never) project_in
+#else
         if (g + 1 < kch) pin(g + 1);
+#endif
         FFN_ST(s2);
         if (g == kch - 1) {
           if (more) load_x1(t + nxb);  // the next tile's rows, during this chunk and the G epilogue
@@ -338,10 +427,18 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
         if ((g & 1) == 0) issue_w((g >> 1) + 1 < npairs ? (g >> 1) + 1 : 0, (pc + 1) & 1);
         FFN_ST(s1);
         f32x4 gn[kRPW];
+#if KDLAE_FFN_ABL == 1 || KDLAE_FFN_ABL == 2
+        for (int r = 0; r < kRPW; ++r) gn[r] = sl[lo[0][1] + r * kHalo * 8];  // ablation: no gate
+#else
         gate_rows<kRPW, kGeluPacked>(sl, lds + S::kDw + g * kDwF4, lo, lq, gn);
+#endif
         FFN_ST(s2);
         if (g & 1) {
+#if KDLAE_FFN_ABL == 2
+          if (gn[0].x == 12345.f) mfma_pair(gbp, gn, pc & 1);  // ablation: (never) project_out
+#else
           mfma_pair(gbp, gn, pc & 1);  // chunks g - 1, g
+#endif
           ++pc;
         } else {
 #pragma unroll
