@@ -13,8 +13,13 @@
 //
 // MFMA roles as in gemm.hip: A = weights (rows = output channels), B = pixels; lane (li, lq) ends with
 // pixel li and output channels 4 lq .. 4 lq + 3 of each channel tile.
+// Products (r05): the split-bf16 form of every inference GEMM (mfma3.h): consecutive k-groups of the
+// chunk's (tap, group) sequence pair up; both operands are split in registers — the pixel fragments
+// from LDS and the weight fragments from L2 — and six v_mfma_f32_16x16x32_bf16 replace eight
+// v_mfma_f32_16x16x4_f32 per 16 x 16 x 32 block.
 #include "kernels.h"
 #include "lds_dma.h"
+#include "mfma3.h"
 
 namespace kdlae {
 
@@ -23,10 +28,6 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int TR = 4, TC = 64, HR = TR + 2, HC = TC + 2;
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 
 }  // namespace
 
@@ -82,36 +83,47 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
     __syncthreads();
     const int ngrp = min(NG, (p.cin_pad - c0) / 16);
     const int nk = NTAP * ngrp;  // k-groups of this chunk: (tap, group) with group fastest
-    f32x4 wc[NT];
-    {
-      const int g = 0 * cgt + c0 / 16;
+    const int np = (nk + 1) / 2;  // split pairs (k-groups 2P, 2P + 1; an odd last one pairs with zeros)
+    // weight fragments of pair P (f32 fragment order, L2-resident), split in registers per pair
+    auto wpair = [&](int P, f32x4 (&wv)[2][NT]) {
 #pragma unroll
-      for (int n = 0; n < NT; ++n) wc[n] = wfrag(n, g);
-    }
-    for (int kk = 0; kk < nk; ++kk) {
-      const int tap = kk / ngrp, grp = kk - tap * ngrp;
-      // prefetch the next k-group's weights
-      f32x4 wn[NT];
-      if (kk + 1 < nk) {
-        const int tap1 = (kk + 1) / ngrp, grp1 = (kk + 1) - tap1 * ngrp;
-        const int g1 = tap1 * cgt + c0 / 16 + grp1;
+      for (int h = 0; h < 2; ++h) {
+        const int kk = 2 * P + h;
+        const int tap = kk / ngrp, grp = kk - tap * ngrp;
+        const int g = tap * cgt + c0 / 16 + grp;
 #pragma unroll
-        for (int n = 0; n < NT; ++n) wn[n] = wfrag(n, g1);
+        for (int n = 0; n < NT; ++n) wv[h][n] = kk < nk ? wfrag(n, g) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      const int df = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
-      const f32x4* row = tile + (((grp * KT + df) * HR + wave + dy) * HC + dx + li) * 4 + lq;
-      f32x4 xv[4];
+    };
+    f32x4 wc[2][NT];
+    wpair(0, wc);
+    for (int P = 0; P < np; ++P) {
+      f32x4 wn[2][NT];
+      if (P + 1 < np) wpair(P + 1, wn);  // the next pair's weights load under this pair's MFMAs
+      f32x4 xv[2][4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) xv[t] = row[t * 16 * 4];
+      for (int h = 0; h < 2; ++h) {
+        const int kk = 2 * P + h;
+        const int tap = kk / ngrp, grp = kk - tap * ngrp;
+        const int df = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
+        const f32x4* row = tile + (((grp * KT + df) * HR + wave + dy) * HC + dx + li) * 4 + lq;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int t = 0; t < 4; ++t) xv[h][t] = kk < nk ? row[t * 16 * 4] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      F3 xs[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t) xs[t] = split3(xv[0][t], xv[1][t]);
 #pragma unroll
-          for (int n = 0; n < NT; ++n) acc[n][t] = mfma4(wc[n][s], xv[t][s], acc[n][t]);
-      if (kk + 1 < nk) {
+      for (int n = 0; n < NT; ++n) {
+        const F3 w = split3(wc[0][n], wc[1][n]);
 #pragma unroll
-        for (int n = 0; n < NT; ++n) wc[n] = wn[n];
+        for (int t = 0; t < 4; ++t) acc[n][t] = mfma6(w, xs[t], acc[n][t]);
+      }
+      if (P + 1 < np) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int n = 0; n < NT; ++n) wc[h][n] = wn[h][n];
       }
     }
   }
