@@ -365,6 +365,7 @@ int asdqe_forward(asdqe_handle* h, const float* lq, const float* gt, int B, int 
       q.ldi = in.ld;
       q.cin_pad = g.cg_per_tap * 16;
       q.wp = D.P(g.w);
+      q.wp3 = D.P3(g.w3);
       q.ntiles = g.ntiles;
       q.kgroups = g.kgroups;
       q.bias = D.P(g.bias);

@@ -31,7 +31,7 @@ constexpr int TR = 4, TC = 64, HR = TR + 2, HC = TC + 2;
 
 }  // namespace
 
-template <int KT, int NT, int CC>
+template <int KT, int NT, int CC, bool PRE>
 __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
   constexpr int NG = CC / 16;                   // 16-channel groups per staged chunk
   constexpr int FPX = KT * HR * HC;             // halo pixels per group
@@ -52,6 +52,8 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
   const long long fhw = (long long)p.H * p.W;
   const float* inb = p.in + (long long)b * p.F * fhw * p.ldi;
   const int cgt = p.cin_pad / 16;               // channel groups per tap
+  static_assert(!PRE || (KT == 1 && CC == 32), "pre-split records: 2-D, 2-group chunks");
+  const int kpt = (p.kgroups + 1) / 2;           // record pairs per output tile
 
   f32x4 acc[NT][4];
 #pragma unroll
@@ -95,6 +97,43 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
         for (int n = 0; n < NT; ++n) wv[h][n] = kk < nk ? wfrag(n, g) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     };
+    if constexpr (PRE) {
+      // pre-split records: pair P of the chunk = k-groups (tap P, groups c0/16, c0/16 + 1) = the
+      // record pair G = (P cgt + c0 / 16) / 2 of the GEMM pack (cgt and c0 / 16 even)
+      auto wrec = [&](int P, F3 (&wv)[NT]) {
+        const int G = (P * cgt + c0 / 16) >> 1;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int tt = t0 + n;
+          if (tt < p.ntiles) {
+            wv[n] = load_w3(reinterpret_cast<const f32x4*>(p.wp3) + ((size_t)tt * kpt + G) * kRec3, lane);
+          } else {
+            wv[n].h = wv[n].m = wv[n].l = bf16x8{};
+          }
+        }
+      };
+      F3 wq[NT];
+      wrec(0, wq);
+      for (int P = 0; P < np; ++P) {
+        F3 wn3[NT];
+        if (P + 1 < np) wrec(P + 1, wn3);  // the next pair's records load under this pair's MFMAs
+        F3 xs[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f32x4* row = tile + (((0 * KT + 0) * HR + wave + P / 3) * HC + P % 3 + li) * 4 + lq;
+          const f32x4* row1 = row + FPX * 4;  // group 1 of the chunk
+          xs[t] = split3(row[t * 16 * 4], row1[t * 16 * 4]);
+        }
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[n][t] = mfma6(wq[n], xs[t], acc[n][t]);
+        if (P + 1 < np) {
+#pragma unroll
+          for (int n = 0; n < NT; ++n) wq[n] = wn3[n];
+        }
+      }
+    } else {
     f32x4 wc[2][NT];
     wpair(0, wc);
     for (int P = 0; P < np; ++P) {
@@ -125,6 +164,7 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
 #pragma unroll
           for (int n = 0; n < NT; ++n) wc[h][n] = wn[h][n];
       }
+    }
     }
   }
 
@@ -168,13 +208,20 @@ hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s) {
   // slower than two NT = 4 blocks that stage the same halo (r01, ASDQE 128-channel convs)
   const int nt = p.ntiles <= 2 ? 2 : 4;
   dim3 grid((unsigned)blocks, (unsigned)((p.ntiles + nt - 1) / nt));
-  // staged chunk: 32 channels (2-D, 51 KiB) or 16 channels (3-D, 76 KiB) of halo
+  // staged chunk: 32 channels (2-D, 51 KiB) or 16 channels (3-D, 76 KiB) of halo; 2-D with split
+  // weight records when the caller has them and the chunks pair like the records (cin_pad % 32 == 0)
+  const bool pre = p.kt == 1 && p.wp3 && p.cin_pad % 32 == 0;
   if (p.kt == 1) {
-    if (nt == 2) hipLaunchKernelGGL((conv_lds_kernel<1, 2, 32>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((conv_lds_kernel<1, 4, 32>), grid, dim3(256), 0, s, p);
+    if (nt == 2) {
+      if (pre) hipLaunchKernelGGL((conv_lds_kernel<1, 2, 32, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv_lds_kernel<1, 2, 32, false>), grid, dim3(256), 0, s, p);
+    } else {
+      if (pre) hipLaunchKernelGGL((conv_lds_kernel<1, 4, 32, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv_lds_kernel<1, 4, 32, false>), grid, dim3(256), 0, s, p);
+    }
   } else {
-    if (nt == 2) hipLaunchKernelGGL((conv_lds_kernel<3, 2, 16>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((conv_lds_kernel<3, 4, 16>), grid, dim3(256), 0, s, p);
+    if (nt == 2) hipLaunchKernelGGL((conv_lds_kernel<3, 2, 16, false>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv_lds_kernel<3, 4, 16, false>), grid, dim3(256), 0, s, p);
   }
   return hipGetLastError();
 }

@@ -212,6 +212,9 @@ struct ConvLdsParams {
   float* out; int ldo;
   int Bn, F, H, W;
   int kt, relu;
+  // optional: the same weights as split records (mfma3.h, pairs of consecutive k-groups); used by the
+  // 2-D kernel when cin_pad % 32 == 0, where its (tap, 2-group chunk) pairs are exactly those pairs
+  const float* wp3 = nullptr;
 };
 bool conv_lds_supported(int kt, int ntiles, int cin_pad);
 hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s);
