@@ -8,10 +8,12 @@
 // x 16 channels, 64 B per pixel — and each wave keeps all 27 weight fragments in VGPRs for the whole
 // block, so the inner loop is one conflict-free ds_read_b128 (16 pixels x 64 B) per 4 MFMAs.
 //
-// MFMA roles as in gemm.hip: A = weights (rows = output channels), B = pixels, k = 4 consecutive input
-// channels of one tap; lane (li, lq) ends with pixel li, output channels 4 lq .. 4 lq + 3.
+// MFMA roles as in gemm.hip: A = weights (rows = output channels), B = pixels; lane (li, lq) ends with
+// pixel li, output channels 4 lq .. 4 lq + 3.  Products (r05): split-bf16 (mfma3.h) over pairs of taps,
+// the k index 8 lq + j being input channel 4 lq + j of tap 2P (j < 4) or of tap 2P + 1 (j >= 4).
 #include "kernels.h"
 #include "lds_dma.h"
+#include "mfma3.h"
 
 namespace kdlae {
 
@@ -23,10 +25,6 @@ constexpr int TR = 4;             // output rows per block (one per wave)
 constexpr int TC = 64;            // output columns per block (4 pixel tiles of 16 per wave)
 constexpr int HR = TR + 2, HC = TC + 2;
 constexpr int HALO_PX = 3 * HR * HC;  // up to 1188 pixels x 16 channels = 74.25 KiB (KT = 3)
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 
 }  // namespace
 
@@ -67,17 +65,22 @@ __global__ __launch_bounds__(256, 2) void conv3d_c16_kernel(Conv3dC16Params p) {
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // taps in pairs (2P, 2P + 1; an odd last tap pairs with zeros): both operands split in registers,
+  // six bf16 MFMAs per 16 x 16 x 32 block (mfma3.h)
 #pragma unroll
-  for (int tap = 0; tap < NTAP; ++tap) {
-    const int df = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
-    const f32x4* row = tile + ((df * HR + wave + dy) * HC + dx + li) * 4 + lq;
-    f32x4 xv[4];
+  for (int P = 0; P < (NTAP + 1) / 2; ++P) {
+    f32x4 xv[2][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) xv[t] = row[t * 16 * 4];
+    for (int h = 0; h < 2; ++h) {
+      const int tap = 2 * P + h;
+      const int df = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
+      const f32x4* row = tile + ((df * HR + wave + dy) * HC + dx + li) * 4 + lq;
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+      for (int t = 0; t < 4; ++t) xv[h][t] = tap < NTAP ? row[t * 16 * 4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const F3 wp = split3(w[2 * P], 2 * P + 1 < NTAP ? w[2 * P + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = mfma4(w[tap][s], xv[t][s], acc[t]);
+    for (int t = 0; t < 4; ++t) acc[t] = mfma6(wp, split3(xv[0][t], xv[1][t]), acc[t]);
   }
 
   const int y = y0 + wave;
