@@ -36,7 +36,10 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
   constexpr int NG = CC / 16;                   // 16-channel groups per staged chunk
   constexpr int FPX = KT * HR * HC;             // halo pixels per group
   constexpr int NTAP = 9 * KT;
-  __shared__ __attribute__((aligned(16))) f32x4 tile[NG * FPX * 4];
+  // PRE: the chunk's two 16-channel groups staged already split, [plane][quad][pixel] of bf16x8 (quad q:
+  // channels 4q..4q+3 of group 0, then of group 1 = one lane's B operand), pixels padded to 16
+  constexpr int FPXP = (FPX + 15) / 16 * 16;
+  __shared__ __attribute__((aligned(16))) f32x4 tile[PRE ? 12 * FPXP : NG * FPX * 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int tx_n = (p.W + TC - 1) / TC, ty_n = (p.H + TR - 1) / TR;
@@ -71,6 +74,36 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
   for (int c0 = 0; c0 < p.cin_pad; c0 += CC) {
     __syncthreads();  // previous chunk's reads are done
     // stage channels [c0, c0 + CC): item = (group, halo pixel, quad)
+    if constexpr (PRE) {
+      // item = (quad, pixel): both groups' float4 of the quad, split, three 16-byte planes
+      constexpr int SB = 4;
+#pragma unroll 1
+      for (int base = 0; base < 4 * FPX; base += 256 * SB) {
+        f32x4 v[SB][2];
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+          const int i = base + tid + 256 * k;
+          const int q = i / FPX, px = i - q * FPX;
+          const int c = px % HC, r = px / HC;
+          const int yy = y0 + r - 1, xx = x0 + c - 1;
+          const bool ok = i < 4 * FPX && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+          const float* src = inb + ((long long)fr * fhw + (long long)yy * p.W + xx) * p.ldi + c0 + 4 * q;
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            v[k][h] = ok ? *reinterpret_cast<const f32x4*>(src + 16 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+          const int i = base + tid + 256 * k;
+          if (i >= 4 * FPX) continue;
+          const int q = i / FPX, px = i - q * FPX;
+          const F3 sv = split3(v[k][0], v[k][1]);
+          tile[(0 * 4 + q) * FPXP + px] = __builtin_bit_cast(f32x4, sv.h);
+          tile[(1 * 4 + q) * FPXP + px] = __builtin_bit_cast(f32x4, sv.m);
+          tile[(2 * 4 + q) * FPXP + px] = __builtin_bit_cast(f32x4, sv.l);
+        }
+      }
+    } else
     dma::stage_batched<NG * FPX * 4, 8>(tile, tid, [&](int i) -> f32x4 {
       const int q = i & 3, gp = i >> 2;
       const int px = gp % FPX, grp = gp / FPX;
@@ -118,11 +151,12 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
         F3 wn3[NT];
         if (P + 1 < np) wrec(P + 1, wn3);  // the next pair's records load under this pair's MFMAs
         F3 xs[4];
+        const f32x4* xp = tile + lq * FPXP + (wave + P / 3) * HC + P % 3 + li;  // tap P, plane h
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const f32x4* row = tile + (((0 * KT + 0) * HR + wave + P / 3) * HC + P % 3 + li) * 4 + lq;
-          const f32x4* row1 = row + FPX * 4;  // group 1 of the chunk
-          xs[t] = split3(row[t * 16 * 4], row1[t * 16 * 4]);
+          xs[t].h = __builtin_bit_cast(bf16x8, xp[16 * t]);
+          xs[t].m = __builtin_bit_cast(bf16x8, xp[4 * FPXP + 16 * t]);
+          xs[t].l = __builtin_bit_cast(bf16x8, xp[8 * FPXP + 16 * t]);
         }
 #pragma unroll
         for (int n = 0; n < NT; ++n)
