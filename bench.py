@@ -518,7 +518,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=0, help="images per GPU (0 = workload default)")
     ap.add_argument("--size", type=int, default=0, help="frame size (0 = workload default)")
-    ap.add_argument("--probe", type=int, default=1, help="kernel class for the roofline (0 = off)")
+    ap.add_argument("--probe", default="3,1",
+                    help="kernel classes to probe, comma-separated; the first is the line's roofline (0 = off): "
+                         "1 conv_gemm, 2 dwconv_gram, 3 feed-forward half")
     ap.add_argument("--probe-level", type=int, default=0, help="channel filter for the probe (0 = all)")
     ap.add_argument("--probe-steps", type=int, default=3,
                     help="steps of the separate probe pass after the timed steps (at most --steps)")
@@ -604,16 +606,16 @@ def main():
     if gather:  # this rank's own images of the gathered batch (for the parity leg)
         out = {k: (v[rank * B:(rank + 1) * B] if v is not None else None) for k, v in out.items()}
 
-    roof = None
-    if args.probe:
+    def probe(cls):
+        """Per-launch HIP-event probe of one kernel class over a separate launch-by-launch pass."""
         import ctypes
         import tempfile
         probe_steps = max(1, min(args.steps, args.probe_steps))
         model.hip_graphs = False
-        L.kdlae_t_probe_arm(eng.handle, args.probe, args.probe_level)
+        L.kdlae_t_probe_arm(eng.handle, cls, args.probe_level)
         step()  # untimed: creates the probe's event pool outside the measured window
         torch.cuda.synchronize(dev)
-        L.kdlae_t_probe_arm(eng.handle, args.probe, args.probe_level)
+        L.kdlae_t_probe_arm(eng.handle, cls, args.probe_level)
         p_elapsed, _, _ = timed_steps(step, probe_steps, distributed, dev)
         model.hip_graphs = True
         ms, n, by, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
@@ -629,38 +631,52 @@ def main():
             del os.environ["KDLAE_PROBE_DUMP"]
             os.unlink(dump)
         L.kdlae_t_probe_arm(eng.handle, 0, 0)
-        if n.value:
-            sec = ms.value / 1e3
-            if args.probe == 1 and fl.value / (PEAK_SPLIT_TFLOPS * 1e12) > by.value / (PEAK_HBM_GBS * 1e9):
-                ach = fl.value / sec / 1e12
-                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(PEAK_SPLIT_TFLOPS, 1),
-                        "unit": "TFLOP/s", "frac": round(ach / PEAK_SPLIT_TFLOPS, 4), "traffic": None,
-                        "peak_definition": "fp32 products via split-bf16 MFMAs: dense bf16 2516.6 TF/s / 6"}
-            else:
-                ach = by.value / sec / 1e9
-                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
-            if fl.value:  # the FLOP side of the same launches, against both fp32-product peaks
-                tf = fl.value / sec / 1e12
-                roof["compute_view"] = {"achieved_tflops": round(tf, 2),
-                                        "frac_of_split_bf16_peak": round(tf / PEAK_SPLIT_TFLOPS, 4),
-                                        "frac_of_fp32_mfma_peak": round(tf / PEAK_FP32_TFLOPS, 4),
-                                        "note": "fp32-accurate products; the split-bf16 peak (419.4) is the "
-                                                "ceiling of this arithmetic, the fp32 MFMA peak (157.3) the "
-                                                "ceiling of the r04 kernels"}
-            tr = pmc_traffic(args.probe)
-            if tr is not None:
-                roof["traffic"], roof["traffic_source"] = tr
-            if launch_roof is not None:
-                roof["per_shape_roof"] = launch_roof
-            roof.update({"kernel": PROBE_CLASSES[args.probe], "launches": int(n.value),
-                         "avg_launch_us": round(ms.value * 1e3 / n.value, 2),
-                         "probe_pass": {"steps": probe_steps, "ms_per_step": round(p_elapsed / probe_steps * 1e3, 2),
-                                        "path": "launch by launch with HIP events around each probed launch, "
-                                                "after the timed steps (which ran un-instrumented)"},
-                         "share_of_step": round(ms.value / 1e3 / p_elapsed, 4),
-                         "algorithmic_bytes_per_launch": by.value / n.value,
-                         "algorithmic_flops_per_launch": fl.value / n.value})
+        if not n.value:
+            return None
+        sec = ms.value / 1e3
+        # the class's bound: its algorithmic FLOPs at the split-bf16 ceiling vs its bytes at 8 TB/s
+        if fl.value / (PEAK_SPLIT_TFLOPS * 1e12) > by.value / (PEAK_HBM_GBS * 1e9):
+            ach = fl.value / sec / 1e12
+            r = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(PEAK_SPLIT_TFLOPS, 1),
+                 "unit": "TFLOP/s", "frac": round(ach / PEAK_SPLIT_TFLOPS, 4), "traffic": None,
+                 "peak_definition": "fp32 products via split-bf16 MFMAs: dense bf16 2516.6 TF/s / 6"}
+        else:
+            ach = by.value / sec / 1e9
+            r = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                 "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
+        if fl.value:  # the FLOP side of the same launches, against both fp32-product peaks
+            tf = fl.value / sec / 1e12
+            r["compute_view"] = {"achieved_tflops": round(tf, 2),
+                                 "frac_of_split_bf16_peak": round(tf / PEAK_SPLIT_TFLOPS, 4),
+                                 "frac_of_fp32_mfma_peak": round(tf / PEAK_FP32_TFLOPS, 4),
+                                 "note": "fp32-accurate products; the split-bf16 peak (419.4) is the "
+                                         "ceiling of this arithmetic, the fp32 MFMA peak (157.3) the "
+                                         "ceiling of the r04 kernels"}
+        tr = pmc_traffic(cls)
+        if tr is not None:
+            r["traffic"], r["traffic_source"] = tr
+        if launch_roof is not None:
+            r["per_shape_roof"] = launch_roof
+        r.update({"kernel": PROBE_CLASSES[cls], "launches": int(n.value),
+                  "avg_launch_us": round(ms.value * 1e3 / n.value, 2),
+                  "probe_pass": {"steps": probe_steps, "ms_per_step": round(p_elapsed / probe_steps * 1e3, 2),
+                                 "path": "launch by launch with HIP events around each probed launch, "
+                                         "after the timed steps (which ran un-instrumented)"},
+                  "share_of_step": round(ms.value / 1e3 / p_elapsed, 4),
+                  "algorithmic_bytes_per_launch": by.value / n.value,
+                  "algorithmic_flops_per_launch": fl.value / n.value})
+        return r
+
+    # the first listed class is the line's `roofline` (the dominant class, by its share of the step);
+    # the others are reported under `roofline_classes`
+    classes = [int(c) for c in str(args.probe).split(",") if c.strip() and int(c) != 0]
+    roof, other = None, {}
+    for i, cls in enumerate(classes):
+        r = probe(cls)
+        if i == 0:
+            roof = r
+        elif r is not None:
+            other[PROBE_CLASSES[cls]] = r
 
     bs1 = None
     if not args.no_bs1 and B > 1 and world == 1:
@@ -714,6 +730,8 @@ def main():
                                                                 if gather else ", no data-path collective)")},
         "roofline": roof,
     }
+    if other:
+        res["roofline_classes"] = other
     if bs1 is not None:
         res["bs1"] = bs1
     # algorithmic per-image figures of SURVEY.md §8d (KDLAE-T 512^2 static=train)
