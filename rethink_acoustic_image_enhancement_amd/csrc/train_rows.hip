@@ -353,6 +353,9 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   const int ntiles = (g.N + 15) / 16;
   // (residual variants: NT <= 4, the residual registers of wider tiles spill)
   static const int nts[] = {8, 6, 4, 3, 2, 1};
+#ifndef KDLAE_ROWS_LDS_KB
+#define KDLAE_ROWS_LDS_KB 96  // split-record LDS budget per block (KiB)
+#endif
 #ifndef KDLAE_ROWS_NTMAX
 #define KDLAE_ROWS_NTMAX 8
 #endif
@@ -360,12 +363,12 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   int NT = 1;
   if (ntiles <= ntmax) {
     for (int c : nts)
-      if (c <= ntmax && c >= ntiles && 3 * c * a.kp <= 96) NT = c;
+      if (c <= ntmax && c >= ntiles && 3 * c * a.kp <= KDLAE_ROWS_LDS_KB) NT = c;
   }
   if (NT < ntiles) {
     int best = -1, best_pad = 1 << 30;
     for (int c : nts) {
-      if (c > ntmax || (3 * c * a.kp > 96 && c > 1)) continue;
+      if (c > ntmax || (3 * c * a.kp > KDLAE_ROWS_LDS_KB && c > 1)) continue;
       const int pad = (ntiles + c - 1) / c * c;
       if (pad < best_pad) best = c, best_pad = pad;
     }

@@ -21,10 +21,10 @@ import csv
 import json
 import sys
 
-CLASSES = [("conv_gemm_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
-           ("gemm_res_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
-           ("gemm_chunk_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
-           ("gemm_attn_in_kernel", "conv_gemm (1x1 / implicit-GEMM, MFMA f32)"),
+CLASSES = [("conv_gemm_kernel", "conv_gemm (1x1 / implicit-GEMM, split-bf16 MFMA)"),
+           ("gemm_res_kernel", "conv_gemm (1x1 / implicit-GEMM, split-bf16 MFMA)"),
+           ("gemm_chunk_kernel", "conv_gemm (1x1 / implicit-GEMM, split-bf16 MFMA)"),
+           ("gemm_attn_in_kernel", "conv_gemm (1x1 / implicit-GEMM, split-bf16 MFMA)"),
            ("dwconv_gram", "dwconv_gram (MDTA pass 1: dwconv + MFMA Gram)"),
            ("ffn_fused_kernel<96>", "ffn_fused C96 (LN + project_in + gate + project_out)"),
            ("ffn_fused_kernel<48>", "ffn_fused C48 (LN + project_in + gate + project_out)"),
