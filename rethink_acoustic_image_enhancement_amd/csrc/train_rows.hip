@@ -349,12 +349,12 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   const bool vecc = al16(g.C) && m4(g.scm) && m4(g.bC1) && m4(g.bC2) &&
                     (g.N % 4 == 0 || (g.c_pad_ok && g.scm >= (g.N + 3) / 4 * 4));
   // output tiles per block: one column block when the N tiles fit (A read once), else the width
-  // with the least padding; LDS for the split records <= 96 KiB (3 NT kp KiB)
+  // with the least padding; LDS for the split records <= KDLAE_ROWS_LDS_KB KiB (3 NT kp KiB)
   const int ntiles = (g.N + 15) / 16;
   // (residual variants: NT <= 4, the residual registers of wider tiles spill)
   static const int nts[] = {8, 6, 4, 3, 2, 1};
 #ifndef KDLAE_ROWS_LDS_KB
-#define KDLAE_ROWS_LDS_KB 96  // split-record LDS budget per block (KiB)
+#define KDLAE_ROWS_LDS_KB 144  // split-record LDS budget per block (KiB); r05 A/B: 96 116.5, 120 116.6, 144 119.6, 156 119.7 img/s
 #endif
 #ifndef KDLAE_ROWS_NTMAX
 #define KDLAE_ROWS_NTMAX 8
