@@ -86,10 +86,15 @@ struct kdlae_tt_handle {
   // bias column sums run there, beside the input-gradient chain on the caller's stream
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // stage_bwd's lagged synchronisation: recorded after each block's last side launch (its scratch
+  // region and gradient buffers are reused two blocks later)
+  hipEvent_t ev_blk[2] = {nullptr, nullptr};
   ~kdlae_tt_handle() {
     for (hipEvent_t e : mark_ev) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    for (hipEvent_t e : {ev_blk[0], ev_blk[1]})
+      if (e) (void)hipEventDestroy(e);
     if (side) (void)hipStreamDestroy(side);
   }
 };
@@ -192,7 +197,6 @@ struct Ctx {
   bool dry = true;
   hipStream_t s = nullptr;  // the stream launches go to: main_s, or side_s inside a side segment
   float* splitk = nullptr;   // split-K partials of the current stream (splitk_main / splitk_side)
-  float* red = nullptr;
   // backward side stream (kdlae_tt_backward*): a side segment (side_begin .. side_end) holds
   // launches that only READ buffers the main stream does not write until the next join.  Every
   // segment starts with a fork (the side stream waits for the main stream's current point), so side
@@ -201,6 +205,8 @@ struct Ctx {
   // pending side launch reads, and before scratch is released.  side_s == nullptr: one stream.
   hipStream_t main_s = nullptr, side_s = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_blk[2] = {nullptr, nullptr};
+  bool blk_rec[2] = {false, false};  // ev_blk[p] holds a record of this call (stage_bwd)
   float* splitk_main = nullptr;
   float* splitk_side = nullptr;
   bool in_side = false, side_pending = false;
@@ -212,12 +218,18 @@ struct Ctx {
   // launch trace (diagnostics only: KDLAE_DEBUG=train_trace); tag = the layer being sequenced
   std::vector<kdlae_tt_handle::TraceRec>* trace = nullptr;
   std::string tag;
-  // queued partial reductions of the backward (one batched launch at the next flush: a mark, the
-  // end of a TransformerBlock, or a full queue); red_off = floats of `red` their partials occupy
-  std::vector<tr::RedDesc> pend;
-  size_t red_off = 0;
+  // queued partial reductions of the backward, one list per stream (partials written on the side
+  // stream are reduced on it, those of the main stream on the main stream, so a flush never waits
+  // for the other stream): one batched launch at the next flush (a full queue, the end of a
+  // TransformerBlock, a mark, the end); red_off = floats of the stream's `red` buffer in use
+  struct RedList {
+    std::vector<tr::RedDesc> pend;
+    float* red = nullptr;
+    size_t red_off = 0;
+  } rl[2];  // [0] main stream, [1] side segments
+  RedList& cur_rl() { return rl[in_side ? 1 : 0]; }
 
-  size_t red_cap = 0;  // floats of `red` (red_floats(): the largest single reduction's partials)
+  size_t red_cap = 0;  // floats of each `red` buffer (red_floats(): the largest single reduction's partials)
   int red_err = KDLAE_OK;  // why the last red_take returned nullptr
   float* alloc(size_t n) {
     off = (off + 255) / 256 * 256;
@@ -243,6 +255,7 @@ struct Ctx {
 };
 
 int flush_reduce(Ctx& c);
+int flush_all(Ctx& c);
 
 int hip_fail(hipError_t e, const char* what) {
   return fail(KDLAE_EHIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -281,12 +294,26 @@ int join(Ctx& c) {
   return e == hipSuccess ? KDLAE_OK : hip_fail(e, "side stream join");
 }
 
+// record ev on the side stream after every side launch enqueued so far (no-op on one stream)
+int side_record(Ctx& c, hipEvent_t ev) {
+  if (c.dry || !c.side_s || !ev) return KDLAE_OK;
+  hipError_t e = hipEventRecord(ev, c.side_s);
+  return e == hipSuccess ? KDLAE_OK : hip_fail(e, "side stream event");
+}
+
+// the main stream waits for a side-stream event recorded earlier (typically long complete)
+int main_wait(Ctx& c, hipEvent_t ev) {
+  if (c.dry || !c.side_s || !ev) return KDLAE_OK;
+  hipError_t e = hipStreamWaitEvent(c.main_s, ev, 0);
+  return e == hipSuccess ? KDLAE_OK : hip_fail(e, "side stream wait");
+}
+
 // a region of the reduction buffer for a queued reduction's partials (flushes when full)
 // Returns nullptr with c.red_err set (and the message in kdlae_last_error) when the flush fails
 // (a HIP error) or when one request alone exceeds the buffer (a sizing bug: KDLAE_ESTATE).
 float* red_take(Ctx& c, size_t n) {
   n = (n + 63) / 64 * 64;
-  if (c.red_off + n > c.red_cap) {
+  if (c.cur_rl().red_off + n > c.red_cap) {
     const int rc = flush_reduce(c);
     if (rc != KDLAE_OK) {
       c.red_err = rc;
@@ -299,8 +326,9 @@ float* red_take(Ctx& c, size_t n) {
                                        std::to_string(c.red_cap) + " (red_floats() misses it)");
     return nullptr;
   }
-  float* p = c.red + c.red_off;
-  c.red_off += n;
+  Ctx::RedList& l = c.cur_rl();
+  float* p = l.red + l.red_off;
+  l.red_off += n;
   return p;
 }
 
@@ -308,7 +336,7 @@ float* red_take(Ctx& c, size_t n) {
 // one head conv, ...).  kdlae_tt_backward_marked records an event at the marks that close a suffix
 // of the flat buffer, so the caller can all-reduce that suffix while the backward continues.
 int mark(Ctx& c) {
-  int rc = flush_reduce(c);  // the gradients this mark declares final (joins the side stream)
+  int rc = flush_all(c);  // the gradients this mark declares final (joins the side stream)
   if (rc) return rc;
   if (c.record_marks && !c.dry && c.cur_mark < (int)c.h->mark_slot.size()) {
     const int j = c.h->mark_slot[c.cur_mark];
@@ -355,14 +383,32 @@ void trace_end(Ctx& c, hipEvent_t a, const char* what) {
 
 inline int ld4(int n) { return (n + 3) / 4 * 4; }
 
-// on the main stream after a join (queued partials may come from either stream); inside a side
-// segment the segment is re-entered afterwards, so later side writes to `red` follow the flush
+// the current stream's queued reductions, on that stream (its partials were written there, and its
+// later writes to the same `red` buffer follow the flush in stream order)
 int flush_reduce(Ctx& c) {
+  Ctx::RedList& l = c.cur_rl();
+  if (!l.pend.empty()) LAUNCH(tr::launch_part_reduce_multi(l.pend.data(), (int)l.pend.size(), c.s));
+  l.pend.clear();
+  l.red_off = 0;
+  return KDLAE_OK;
+}
+
+// every queued reduction (the side list on the side stream), then the main stream joins the side
+// stream: all gradients so far are final on the main stream
+int flush_all(Ctx& c) {
   const bool was_side = c.in_side;
+  Ctx::RedList& sl = c.rl[1];
+  if (!sl.pend.empty()) {
+    hipStream_t keep = c.s;
+    c.s = c.side_s && !c.dry ? c.side_s : c.main_s;
+    if (c.side_s && !c.dry) c.side_pending = true;
+    LAUNCH(tr::launch_part_reduce_multi(sl.pend.data(), (int)sl.pend.size(), c.s));
+    c.s = keep;
+  }
+  sl.pend.clear();
+  sl.red_off = 0;
   TRY(join(c));
-  if (!c.pend.empty()) LAUNCH(tr::launch_part_reduce_multi(c.pend.data(), (int)c.pend.size(), c.s));
-  c.pend.clear();
-  c.red_off = 0;
+  TRY(flush_reduce(c));
   if (was_side) TRY(side_begin(c));
   return KDLAE_OK;
 }
@@ -376,8 +422,9 @@ int queue_reduce(Ctx& c, const float* part, int nblk, int ncols, int pstride, fl
   d.nblk = nblk;
   d.ncols = ncols;
   d.pstride = pstride;
-  c.pend.push_back(d);
-  if ((int)c.pend.size() == tr::kRedBatch) return flush_reduce(c);
+  Ctx::RedList& l = c.cur_rl();
+  l.pend.push_back(d);
+  if ((int)l.pend.size() == tr::kRedBatch) return flush_reduce(c);
   return KDLAE_OK;
 }
 
@@ -386,6 +433,9 @@ int queue_reduce(Ctx& c, const float* part, int nblk, int ncols, int pstride, fl
 // The K >= 1024 ones take the split-K partials too (launch_tgemm splits only where the grid is short).
 // r04 trace A/B (gpurun_out/trab): dX 1536 x 384 K 2042 0.544 -> 0.386 ms, 6144 x 192 K 1020 0.688 ->
 // 0.660; at K = 510 / 576 the partial round trip lost (0.42 -> 0.53, 0.42 -> 0.50 ms).
+#ifndef KDLAE_TRAIN_LAG
+#define KDLAE_TRAIN_LAG 1  // stage_bwd's lagged side-stream synchronisation (0: join per block)
+#endif
 #ifndef KDLAE_TRAIN_SPLIT_SMALL
 #define KDLAE_TRAIN_SPLIT_SMALL 1
 #endif
@@ -644,8 +694,8 @@ int block_fwd(Ctx& c, BlockRec& r) {
   r.sumsq = c.alloc((size_t)Bn * 2 * C);
   {
     const int nb = nblk_for(HW, (long long)2 * C * Bn, 256);
-    LAUNCH(tr::launch_colsum(r.qkvd, C3, 2 * C, HW, Bn, 1, c.red, nb, c.s));
-    LAUNCH(tr::launch_part_reduce(c.red, nb, 2 * C, Bn, r.sumsq, 0, 1.f, c.s));
+    LAUNCH(tr::launch_colsum(r.qkvd, C3, 2 * C, HW, Bn, 1, c.rl[0].red, nb, c.s));
+    LAUNCH(tr::launch_part_reduce(c.rl[0].red, nb, 2 * C, Bn, r.sumsq, 0, 1.f, c.s));
   }
   const size_t mats = (size_t)Bn * heads * Ch * Ch;
   r.G = c.alloc(mats);
@@ -728,7 +778,15 @@ int ln_bwd(Ctx& c, const float* dy, const float* x, const float* st, int C, long
 }
 
 // d: [P][C] gradient of the block output on entry, of the block input on exit
-int block_bwd(Ctx& c, const BlockRec& r, float* d) {
+// d_in: [P][C] gradient of the block output; d_out: of the block input (a different buffer).
+// Synchronisation with the side stream (stage_bwd passes lag = true): the main stream never waits for
+// the block's own side launches.  The side launches read d_in (project_out weight gradient) and this
+// block's scratch (the dW GEMMs' dy, dx1, dqkv and the bias sums); stage_bwd rotates three gradient
+// buffers and alternates two scratch regions, so neither is written again before the block after
+// next, whose start waits for this block's side launches.  lag = false: a join before the last
+// LayerNorm backward and a full flush + join at the end.  *extent: end of the block's scratch.
+int block_bwd(Ctx& c, const BlockRec& r, const float* d_in, float* d_out, bool lag, size_t* extent) {
+  float* d = const_cast<float*>(d_in);
   const int C = r.C, C3 = 3 * C, hid = r.hid, heads = r.heads, Ch = C / heads, Bn = r.Bn;
   const long long HW = (long long)r.H * r.W, P = Bn * HW;
   const std::string& p = r.p;
@@ -814,9 +872,11 @@ int block_bwd(Ctx& c, const BlockRec& r, float* d) {
   }
   float* dxn1 = c.alloc(P * C);
   TRY(conv1_bwd(c, p + ".attn.qkv", {r.xn1, C}, {dqkv, C3}, C, C3, P, {dxn1, C}));
-  TRY(join(c));  // ln_bwd overwrites d, which the project_out weight gradient reads
-  TRY(ln_bwd(c, dxn1, r.x, r.st1, C, P, p + ".norm1.body", dx1, d));
-  TRY(flush_reduce(c));  // before the block's scratch (dtp) is released (joins the side stream)
+  if (!lag) TRY(join(c));
+  TRY(ln_bwd(c, dxn1, r.x, r.st1, C, P, p + ".norm1.body", dx1, d_out));
+  TRY(flush_reduce(c));  // the main list, before the block's scratch (dtp) is released
+  if (!lag) TRY(flush_all(c));
+  if (extent) *extent = c.off;
   c.off = mark;
   return KDLAE_OK;
 }
@@ -836,12 +896,42 @@ int stage_fwd(Ctx& c, const std::string& name, int n, int C, int heads, int Bn, 
   return KDLAE_OK;
 }
 
+// The blocks of a stage share one shape, so their scratch regions alternate between [base, e0) and
+// [e0, e0 + size), and block k reads gradient buffer k % 3 and writes (k + 1) % 3 (0 = d): before
+// block k reuses the region and the buffer of block k - 2, the main stream waits for the event
+// recorded after block k - 2's side launches (by then complete, as a rule), instead of joining the
+// side stream at every block (r05 trace: 240 joins, ≈13 µs of idle main stream each, plus waits for
+// the last weight gradients).  The marked backward keeps a full flush + join per block (the
+// gradient-ready marks need them); the stage ends with one either way, the result copied into d.
 int stage_bwd(Ctx& c, const std::string& name, float* d) {
   const auto& recs = c.h->sv.stages.at(name);
-  for (int i = (int)recs.size() - 1; i >= 0; --i) {
-    TRY(block_bwd(c, recs[i], d));
-    TRY(mark(c));
+  const bool lag = !c.record_marks && !c.dry && c.side_s && KDLAE_TRAIN_LAG;
+  const BlockRec& r0 = recs.front();
+  const size_t dn = (size_t)r0.Bn * r0.H * r0.W * r0.C;
+  const size_t off0 = c.off;
+  float* dbuf[3] = {d, c.alloc(dn), c.alloc(dn)};
+  const size_t base = c.off;
+  size_t e0 = base;
+  c.blk_rec[0] = c.blk_rec[1] = false;
+  for (int i = (int)recs.size() - 1, k = 0; i >= 0; --i, ++k) {
+    const int par = k & 1;
+    c.off = par ? e0 : base;  // the same layout with or without lag, so the dry run sizes it
+    if (lag && c.blk_rec[par]) TRY(main_wait(c, c.ev_blk[par]));
+    size_t ext = 0;
+    TRY(block_bwd(c, recs[i], dbuf[k % 3], dbuf[(k + 1) % 3], lag, &ext));
+    if (par == 0) e0 = ext;
+    if (lag) {
+      TRY(side_record(c, c.ev_blk[par]));
+      c.blk_rec[par] = true;
+      ++c.cur_mark;  // mark() without its flush and join
+    } else {
+      TRY(mark(c));
+    }
   }
+  if (lag) TRY(flush_all(c));
+  const float* res = dbuf[recs.size() % 3];
+  if (res != d) LAUNCH(hipMemcpyAsync(d, res, dn * sizeof(float), hipMemcpyDeviceToDevice, c.s));
+  c.off = off0;
   return KDLAE_OK;
 }
 
@@ -1067,7 +1157,8 @@ void ctx_init(Ctx& c, const kdlae_tt_handle* h, void* ws, size_t ws_bytes, bool 
   c.splitk_main = c.splitk = c.alloc(kSplitCap);
   c.splitk_side = c.alloc(kSplitCap);
   c.red_cap = red_floats(h->cfg, B, H, W);
-  c.red = c.alloc(c.red_cap);
+  c.rl[0].red = c.alloc(c.red_cap);
+  c.rl[1].red = c.alloc(c.red_cap);
 }
 
 // the backward's side stream (created once per handle, on its device); KDLAE_DEBUG=train_serial
@@ -1078,11 +1169,15 @@ int use_side_stream(Ctx& c, kdlae_tt_handle* h) {
     hipError_t e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
+    for (hipEvent_t* ev : {&h->ev_blk[0], &h->ev_blk[1]})
+      if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) return hip_fail(e, "backward side stream");
   }
   c.side_s = h->side;
   c.ev_fork = h->ev_fork;
   c.ev_join = h->ev_join;
+  c.ev_blk[0] = h->ev_blk[0];
+  c.ev_blk[1] = h->ev_blk[1];
   return KDLAE_OK;
 }
 
@@ -1217,7 +1312,7 @@ int kdlae_tt_backward(kdlae_tt_handle* h, const float* theta, const float* dhq, 
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
   rc = net_bwd(c, dhq, dsr, has_dsr);
-  if (rc == KDLAE_OK) rc = flush_reduce(c);
+  if (rc == KDLAE_OK) rc = flush_all(c);
   if (rc != KDLAE_OK) (void)join(c);  // leave no side launch unjoined, even on an error path
   trace_dump(h, c.s, "bwd");
   return rc;
@@ -1295,7 +1390,7 @@ int kdlae_tt_backward_marked(kdlae_tt_handle* h, const float* theta, const float
   hipError_t e = hipMemsetAsync(grad, 0, (size_t)h->total * sizeof(float), (hipStream_t)stream);
   if (e != hipSuccess) return fail(KDLAE_EHIP, hipGetErrorString(e));
   rc = net_bwd(c, dhq, dsr, has_dsr);
-  if (rc == KDLAE_OK) rc = flush_reduce(c);
+  if (rc == KDLAE_OK) rc = flush_all(c);
   if (rc != KDLAE_OK) (void)join(c);
   trace_dump(h, c.s, "bwd");
   if (rc) return rc;
