@@ -39,7 +39,9 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
   // PRE: the chunk's two 16-channel groups staged already split, [plane][quad][pixel] of bf16x8 (quad q:
   // channels 4q..4q+3 of group 0, then of group 1 = one lane's B operand), pixels padded to 16
   constexpr int FPXP = (FPX + 15) / 16 * 16;
-  __shared__ __attribute__((aligned(16))) f32x4 tile[PRE ? 12 * FPXP : NG * FPX * 4];
+  // PRE3 (KT = 3): fp32 halo as without PRE, the weights from tap-pair split records (kdlae_s.cpp)
+  constexpr bool PRE2 = PRE && KT == 1, PRE3 = PRE && KT == 3;
+  __shared__ __attribute__((aligned(16))) f32x4 tile[PRE2 ? 12 * FPXP : NG * FPX * 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int tx_n = (p.W + TC - 1) / TC, ty_n = (p.H + TR - 1) / TR;
@@ -55,7 +57,8 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
   const long long fhw = (long long)p.H * p.W;
   const float* inb = p.in + (long long)b * p.F * fhw * p.ldi;
   const int cgt = p.cin_pad / 16;               // channel groups per tap
-  static_assert(!PRE || (KT == 1 && CC == 32), "pre-split records: 2-D, 2-group chunks");
+  static_assert(!PRE2 || CC == 32, "pre-split records: 2-D, 2-group chunks");
+  static_assert(!PRE3 || CC == 16, "tap-pair records: 3-D, 1-group chunks");
   const int kpt = (p.kgroups + 1) / 2;           // record pairs per output tile
 
   f32x4 acc[NT][4];
@@ -74,7 +77,7 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
   for (int c0 = 0; c0 < p.cin_pad; c0 += CC) {
     __syncthreads();  // previous chunk's reads are done
     // stage channels [c0, c0 + CC): item = (group, halo pixel, quad)
-    if constexpr (PRE) {
+    if constexpr (PRE2) {
       // item = (quad, pixel): both groups' float4 of the quad, split, three 16-byte planes
       constexpr int SB = 4;
 #pragma unroll 1
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
         for (int n = 0; n < NT; ++n) wv[h][n] = kk < nk ? wfrag(n, g) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     };
-    if constexpr (PRE) {
+    if constexpr (PRE2) {
       // pre-split records: pair P of the chunk = k-groups (tap P, groups c0/16, c0/16 + 1) = the
       // record pair G = (P cgt + c0 / 16) / 2 of the GEMM pack (cgt and c0 / 16 even)
       auto wrec = [&](int P, F3 (&wv)[NT]) {
@@ -158,6 +161,48 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
           xs[t].m = __builtin_bit_cast(bf16x8, xp[4 * FPXP + 16 * t]);
           xs[t].l = __builtin_bit_cast(bf16x8, xp[8 * FPXP + 16 * t]);
         }
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[n][t] = mfma6(wq[n], xs[t], acc[n][t]);
+        if (P + 1 < np) {
+#pragma unroll
+          for (int n = 0; n < NT; ++n) wq[n] = wn3[n];
+        }
+      }
+    } else if constexpr (PRE3) {
+      // tap-pair records: pair P of the chunk (one group, taps 2P and 2P + 1; tap 27 zeros) is record
+      // (c0 / 16) * 14 + P of the tile; the same values and pairing as the in-register split below
+      const int kp3 = (p.cin_pad / 16) * 14;
+      auto wrec = [&](int P, F3 (&wv)[NT]) {
+        const int G = (c0 / 16) * 14 + P;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int tt = t0 + n;
+          if (tt < p.ntiles) {
+            wv[n] = load_w3(reinterpret_cast<const f32x4*>(p.wp3) + ((size_t)tt * kp3 + G) * kRec3, lane);
+          } else {
+            wv[n].h = wv[n].m = wv[n].l = bf16x8{};
+          }
+        }
+      };
+      F3 wq[NT];
+      wrec(0, wq);
+      for (int P = 0; P < np; ++P) {
+        F3 wn3[NT];
+        if (P + 1 < np) wrec(P + 1, wn3);  // the next pair's records load under this pair's MFMAs
+        f32x4 xv[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int tap = 2 * P + h;
+          const int df = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
+          const f32x4* row = tile + ((df * HR + wave + dy) * HC + dx + li) * 4 + lq;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) xv[h][t] = tap < nk ? row[t * 16 * 4] : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        F3 xs[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) xs[t] = split3(xv[0][t], xv[1][t]);
 #pragma unroll
         for (int n = 0; n < NT; ++n)
 #pragma unroll
@@ -244,7 +289,7 @@ hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s) {
   dim3 grid((unsigned)blocks, (unsigned)((p.ntiles + nt - 1) / nt));
   // staged chunk: 32 channels (2-D, 51 KiB) or 16 channels (3-D, 76 KiB) of halo; 2-D with split
   // weight records when the caller has them and the chunks pair like the records (cin_pad % 32 == 0)
-  const bool pre = p.kt == 1 && p.wp3 && p.cin_pad % 32 == 0;
+  const bool pre = p.kt == 1 && p.wp3 && p.cin_pad % 32 == 0;  // (kt = 3: wp3 holds tap-pair records)
   if (p.kt == 1) {
     if (nt == 2) {
       if (pre) hipLaunchKernelGGL((conv_lds_kernel<1, 2, 32, true>), grid, dim3(256), 0, s, p);
@@ -254,8 +299,14 @@ hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s) {
       else hipLaunchKernelGGL((conv_lds_kernel<1, 4, 32, false>), grid, dim3(256), 0, s, p);
     }
   } else {
-    if (nt == 2) hipLaunchKernelGGL((conv_lds_kernel<3, 2, 16, false>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((conv_lds_kernel<3, 4, 16, false>), grid, dim3(256), 0, s, p);
+    // tap-pair split records when the caller has them (KDLAE-S packs them for every conv_lds layer)
+    if (p.wp3) {
+      if (nt == 2) hipLaunchKernelGGL((conv_lds_kernel<3, 2, 16, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv_lds_kernel<3, 4, 16, true>), grid, dim3(256), 0, s, p);
+    } else {
+      if (nt == 2) hipLaunchKernelGGL((conv_lds_kernel<3, 2, 16, false>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv_lds_kernel<3, 4, 16, false>), grid, dim3(256), 0, s, p);
+    }
   }
   return hipGetLastError();
 }

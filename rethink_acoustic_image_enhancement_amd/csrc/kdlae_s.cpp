@@ -171,6 +171,18 @@ static int build_program_s(kdlae_s_handle* h) {
       return PEx{W + (n * cin + c) * 27 + tap, -1};
     }));
     g.w3 = ar.split(g.w, g.ntiles, g.kgroups);
+    if (conv_lds_supported(3, g.ntiles, cis)) {
+      // conv_lds stages one 16-channel group of the 3-frame halo at a time and pairs consecutive taps
+      // of that group: records of k-groups (group c, tap 2j) + (group c, tap 2j + 1), tap 27 = zeros,
+      // i.e. split records of the fragment block in k-group order c * 28 + tap
+      const int kg28 = 28 * (cis / 16);
+      const size_t wt = ar.add(pack_fragments(g.ntiles, kg28, [&](int n, int k) -> PEx {
+        const int kg = k / 16, grp = kg / 28, tap = kg - 28 * grp, c = 16 * grp + (k & 15);
+        if (n >= cout || c >= cin || tap >= 27) return PEx{};
+        return PEx{W + (n * cin + c) * 27 + tap, -1};
+      }));
+      g.w3t = ar.split(wt, g.ntiles, kg28);
+    }
     std::vector<PEx> b((size_t)g.ntiles * 16);
     for (int n = 0; n < cout; ++n) b[n].a = Bv + n;
     g.bias = ar.add(b);
@@ -355,6 +367,7 @@ int kdlae_s_forward(kdlae_s_handle* h, const float* x, int B, int F, int H, int 
       q.W = Ww;
       q.kt = g.kt;
       q.relu = relu;
+      q.wp3 = D.P3(g.w3t);
       HIPCHK(launch_conv_lds(q, s));
       return (int)KDLAE_OK;
     }

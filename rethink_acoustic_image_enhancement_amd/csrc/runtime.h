@@ -37,6 +37,7 @@ constexpr size_t kNone = (size_t)-1;
 struct Gemm {
   size_t w = kNone, bias = kNone;
   size_t w3 = kNone;  // the same weights in split fragment order (mfma3.h), offset into the split arena
+  size_t w3t = kNone;  // 3x3x3 convs (kt = 3): split records of tap pairs (conv_lds.hip), see kdlae_s.cpp
   int ntiles = 0, kgroups = 0, N = 0, K = 0, ksize = 1, cg_per_tap = 0, kt = 1;
   int out_mode = 0;  // store map the variant must support (0 plain, 1 unshuffle, 2 shuffle)
   int NT = 0, KG = 0, group_tiles = 0, WPE = 2;
