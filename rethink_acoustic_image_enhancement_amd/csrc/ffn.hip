@@ -39,11 +39,6 @@ using gdfnc::kGeluPacked;
 using gdfnc::kHalo;
 using gdfnc::kTile;
 
-constexpr int kTH = 8;                  // interior rows per tile
-constexpr int kHR = kTH + 2;            // halo rows
-constexpr int kHPx = kHR * kHalo;       // 180 halo pixels
-constexpr int kImg = kHPx * 8;          // f32x4 per halo image slot
-constexpr int kRPW = 2;                 // output rows per G wave
 constexpr unsigned kOOBf = 0x80000000u;
 
 typedef unsigned u32x4f __attribute__((ext_vector_type(4)));
@@ -99,15 +94,39 @@ __device__ __forceinline__ unsigned long long stamp() {
 #define FFN_ADD(k, d)
 #endif
 
+// Tile shape and wave counts (A/B knobs for C = 48; C = 96's LDS has room for nothing larger than its
+// 16 x 8 tile with 4 P + 4 G waves).  r05 same-box A/B on C48@1024^2 (profiles/r05zv_ffn48_shape_ab.txt):
+// the default 16 x 8 tile, 4 + 4 waves 8.09-8.11 ms; a 16 x 12 tile (halo 1.31x instead of 1.41x,
+// 4 + 4 waves, 17 spilled VGPRs) 8.05 ms; 12 waves (3 per SIMD, 168 VGPRs each) spill 35-130 VGPRs:
+// 4 P + 8 G 10.37 ms, 8 P + 4 G 11.65 ms.
+#ifndef KDLAE_FFN48_TH
+#define KDLAE_FFN48_TH 8
+#endif
+#ifndef KDLAE_FFN_NP
+#define KDLAE_FFN_NP 4
+#endif
+#ifndef KDLAE_FFN48_NGW
+#define KDLAE_FFN48_NGW 4
+#endif
 template <int C>
 struct FfnShape {
+  static constexpr int TH = C == 48 ? KDLAE_FFN48_TH : 8;  // interior rows per tile
+  static constexpr int HR = TH + 2;                        // halo rows
+  static constexpr int NGW = C == 48 ? KDLAE_FFN48_NGW : 4;  // G waves: TH / NGW output rows each
+  static constexpr int RPW = TH / NGW;
+  static constexpr int NPT = HR + 2;                       // halo pixel tiles of 16: HR rows, 2 columns
+  static constexpr int NP = C == 48 ? KDLAE_FFN_NP : 4;    // P waves
+  static constexpr int PT = (NPT + NP - 1) / NP;           // halo pixel tiles per P wave
+  static constexpr int NW = NP + NGW;
+  static constexpr int Img = HR * kHalo * 8;               // f32x4 per halo image slot
+  static_assert(TH % NGW == 0 && HR <= 16 && PT * NP >= NPT, "ffn tile shape");
   static constexpr bool kUniformDma = uniform_dma<C>();
   static constexpr int KG = C / 16;          // k-groups of project_in
   static constexpr int KP = (KG + 1) / 2;    // split pairs of project_in
   static constexpr int NTO = C / 16;         // project_out output tiles
   static constexpr int KCH = C == 48 ? 8 : 16;  // max hidden chunks (hidS <= 16 KCH)
   // LDS carve (f32x4): 2 halo image slots, every chunk's dw block, 2 W slots, biases
-  static constexpr int kDw = 2 * kImg;
+  static constexpr int kDw = 2 * Img;
   static constexpr int kW = kDw + KCH * kDwF4;
   static constexpr int kBin = kW + 2 * NTO * kRec3;
   static constexpr int kBout = kBin + KCH * 8;
@@ -116,17 +135,48 @@ struct FfnShape {
   static constexpr int kDummy = kWin + 2 * kWinSlot;           // 1 KiB landing slot of padding DMA pieces
   static constexpr int kLds = (kDummy + (kUniformDma ? 64 : 0)) * 16;
   // project_out W pieces (1 KiB) of one pair dealt over the 4 G waves: piece k -> wave k % 4
-  static constexpr int pw(int w) { return kUniformDma ? (3 * NTO + 3) / 4 : (3 * NTO - w + 3) / 4; }
-  // project_in pieces of one chunk dealt over the 4 P waves
-  static constexpr int pwin(int w) { return kUniformDma ? (6 * KP + 3) / 4 : (6 * KP - w + 3) / 4; }
+  static constexpr int pw(int w) { return kUniformDma ? (3 * NTO + NGW - 1) / NGW : (3 * NTO - w + NGW - 1) / NGW; }
+  // project_in pieces of one chunk dealt over the NP P waves
+  static constexpr int pwin(int w) { return kUniformDma ? (6 * KP + NP - 1) / NP : (6 * KP - w + NP - 1) / NP; }
 };
+
+// G wave wi: wait until at most its W pieces of this pair (+ E older ops) are outstanding
+template <class S, int E, int W = 0>
+__device__ __forceinline__ void wait_w_of(int wi) {
+  if constexpr (S::kUniformDma || W + 1 == S::NGW) {
+    wait_vm<S::pw(W) + E>();
+  } else {
+    if (wi == W) {
+      wait_vm<S::pw(W) + E>();
+      return;
+    }
+    wait_w_of<S, E, W + 1>(wi);
+  }
+}
+
+// P wave wi at the last chunk of a tile: at most its W-in pieces of this chunk and the next tile's
+// x1 loads outstanding (a compile-time count per wave)
+template <class S, int W = 0>
+__device__ __forceinline__ void wait_pin_last(int wi) {
+  if constexpr (S::kUniformDma || W + 1 == S::NP) {
+    wait_vm<S::pwin(W) + S::PT * S::KG>();
+  } else {
+    if (wi == W) {
+      wait_vm<S::pwin(W) + S::PT * S::KG>();
+      return;
+    }
+    wait_pin_last<S, W + 1>(wi);
+  }
+}
 
 }  // namespace
 
 template <int C>
-__global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
+__global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn_fused_kernel(FfnParams p) {
   using S = FfnShape<C>;
   constexpr int KG = S::KG, KP = S::KP, NTO = S::NTO;
+  constexpr int kTH = S::TH, kHR = S::HR, kRPW = S::RPW, kImg = S::Img, PT = S::PT, NP = S::NP;
+  constexpr int NT = 64 * S::NW;
   extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -145,15 +195,15 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
 #endif
 
   // resident: every chunk's dw block, both biases
-  for (int i = tid; i < kch * kDwF4; i += 512) lds[S::kDw + i] = reinterpret_cast<const f32x4*>(p.dw)[i];
-  for (int i = tid; i < kch * 8; i += 512)
+  for (int i = tid; i < kch * kDwF4; i += NT) lds[S::kDw + i] = reinterpret_cast<const f32x4*>(p.dw)[i];
+  for (int i = tid; i < kch * 8; i += NT)
     lds[S::kBin + i] = p.bias_in ? reinterpret_cast<const f32x4*>(p.bias_in)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int i = tid; i < NTO * 4; i += 512)
+  for (int i = tid; i < NTO * 4; i += NT)
     lds[S::kBout + i] = p.bias_out ? reinterpret_cast<const f32x4*>(p.bias_out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 
   const long long HW = (long long)p.H * p.W;
-  const bool gw = wave < 4;                 // G wave (gate + project_out) or P wave (project_in)
-  const int wi = gw ? wave : wave - 4;
+  const bool gw = wave < S::NGW;            // G wave (gate + project_out) or P wave (project_in)
+  const int wi = gw ? wave : wave - S::NGW;
 
   // ---- G-wave state
   // project_out split records [NTO][npairs][kRec3] -> W slot s: pieces k = 3 t + plane
@@ -163,8 +213,8 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
     f32x4* dst = lds + S::kW + slot * (NTO * kRec3);
     if constexpr (S::kUniformDma) {
 #pragma unroll
-      for (int j = 0; j < (3 * NTO + 3) / 4; ++j) {
-        const int k = wi + 4 * j;
+      for (int j = 0; j < (3 * NTO + S::NGW - 1) / S::NGW; ++j) {
+        const int k = wi + S::NGW * j;
         const bool real = k < 3 * NTO;
         const int t = k / 3, pl = k - 3 * t;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lptr_f)(real ? dst + 64 * k : lds + S::kDummy), 16,
@@ -174,7 +224,7 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
     } else {
 #pragma unroll
       for (int k = 0; k < 3 * NTO; ++k)
-        if (k % 4 == wi) {
+        if (k % S::NGW == wi) {
           const int t = k / 3, pl = k - 3 * t;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lptr_f)(dst + 64 * k), 16, (int)(16u * lane),
                                                    ((t * npairs + pair) * 3 + pl) * 1024, 0, 0);
@@ -184,12 +234,7 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
   // wait until at most N VMEM ops of this G wave are outstanding (exact per-wave counts)
   auto wait_w = [&](auto extra) {
     constexpr int E = decltype(extra)::value;
-    switch (wi) {
-      case 0: wait_vm<S::pw(0) + E>(); break;
-      case 1: wait_vm<S::pw(1) + E>(); break;
-      case 2: wait_vm<S::pw(2) + E>(); break;
-      default: wait_vm<S::pw(3) + E>(); break;
-    }
+    wait_w_of<S, E>(wi);
   };
   int lo[2][3];
 #pragma unroll
@@ -200,15 +245,16 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
       lo[h][j] = (kRPW * wi * kHalo + hx) * 8 + ((4 * h + lq) ^ (hx & 7));
     }
 
-  // ---- P-wave state: pixel tiles 3 wi .. 3 wi + 2 of the halo (0..9 rows, 10 / 11 columns 0 / 17)
-  int phy[3], phx[3];
-  bool plv[3];
+  // ---- P-wave state: halo pixel tiles PT wi .. PT wi + PT - 1 (rows 0..HR-1 over the interior columns,
+  // then columns 0 and 17)
+  int phy[PT], phx[PT];
+  bool plv[PT];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int pt = 3 * wi + k;
+  for (int k = 0; k < PT; ++k) {
+    const int pt = PT * wi + k;
     phy[k] = pt < kHR ? pt : li;
     phx[k] = pt < kHR ? li + 1 : (pt == kHR ? 0 : kHalo - 1);
-    plv[k] = pt < kHR || li < kHR;
+    plv[k] = pt < kHR || (pt < S::NPT && li < kHR);
   }
 
   // ---- P-wave state: project_in records of chunk g DMA'd into W-in slot g & 1 (issued two chunks
@@ -220,8 +266,8 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
     f32x4* dst = lds + S::kWin + (g & 1) * S::kWinSlot;
     if constexpr (S::kUniformDma) {
 #pragma unroll
-      for (int i = 0; i < (6 * KP + 3) / 4; ++i) {
-        const int k = wi + 4 * i;  // piece k = (tile j = k / (3 KP), pair G, plane) of records (2g + j, G)
+      for (int i = 0; i < (6 * KP + NP - 1) / NP; ++i) {
+        const int k = wi + NP * i;  // piece k = (tile j = k / (3 KP), pair G, plane) of records (2g + j, G)
         const bool real = k < 6 * KP;
         const int j = k / (3 * KP), rem = k - j * 3 * KP;
         const int G = rem / 3, pl = rem - 3 * G;
@@ -232,7 +278,7 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
     } else {
 #pragma unroll
       for (int k = 0; k < 6 * KP; ++k)
-        if (k % 4 == wi) {  // piece k = (tile j = k / (3 KP), pair G, plane) of records (2g + j, G)
+        if (k % NP == wi) {  // piece k = (tile j = k / (3 KP), pair G, plane) of records (2g + j, G)
           const int j = k / (3 * KP), rem = k - j * 3 * KP;
           const int G = rem / 3, pl = rem - 3 * G;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rwin, (lptr_f)(dst + 64 * k), 16, (int)(16u * lane),
@@ -240,7 +286,7 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
         }
     }
   };
-  f32x4 a[3][KG];  // P waves: the x1 rows of the next tile (loaded ahead)
+  f32x4 a[PT][KG];  // P waves: the x1 rows of the next tile (loaded ahead)
   auto load_x1 = [&](int t) {
     const int b = t / per_img;
     const int rem = t - b * per_img;
@@ -249,7 +295,7 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(p.x + (long long)b * HW * p.ldx), 0, (int)(HW * p.ldx * 4), 0x00020000);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < PT; ++k) {
       const int yy = y0 - 1 + phy[k], xx = x0 - 1 + phx[k];
       const bool ok = plv[k] && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
       const unsigned off = ok ? (unsigned)((yy * p.W + xx) * p.ldx) * 4u + 16u * lq : kOOBf;
@@ -285,16 +331,16 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
       tile_geo(t, b, x0, y0);
       (void)b;
       // ================================================================ P waves: project_in producer
-      F3 xs[KP][3];
-      bool in[3];
+      F3 xs[KP][PT];
+      bool in[PT];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
+      for (int k = 0; k < PT; ++k) {
         const int yy = y0 - 1 + phy[k], xx = x0 - 1 + phx[k];
         in[k] = plv[k] && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
       }
-      ln_rows<KG, 3>(p.ln, C, KG, a);
+      ln_rows<KG, PT>(p.ln, C, KG, a);
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
+      for (int k = 0; k < PT; ++k)
 #pragma unroll
         for (int G = 0; G < KP; ++G)
           xs[G][k] = split3(a[k][2 * G], 2 * G + 1 < KG ? a[k][2 * G + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
@@ -302,9 +348,9 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
       // image slot g & 1
       auto pin = [&](int g) {
         const f32x4* wl = lds + S::kWin + (g & 1) * S::kWinSlot + lane;
-        f32x4 a1[3], a2[3];
+        f32x4 a1[PT], a2[PT];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) a1[k] = a2[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < PT; ++k) a1[k] = a2[k] = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (kPinPipe) {
           // the W planes one step ahead of their MFMAs (steps = (pair, plane l / m / h): mfma6_pair's
           // term order), fenced so each step's reads issue under the previous step's MFMAs
@@ -323,20 +369,20 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
             const bf16x8 p0 = w[st & 1][0], p1 = w[st & 1][1];
             if (pl == 2) {
 #pragma unroll
-              for (int r = 0; r < 3; ++r) {
+              for (int r = 0; r < PT; ++r) {
                 a1[r] = mfma_bf(p0, xs[G][r].l, a1[r]);
                 a2[r] = mfma_bf(p1, xs[G][r].l, a2[r]);
               }
             }
             if (pl >= 1) {
 #pragma unroll
-              for (int r = 0; r < 3; ++r) {
+              for (int r = 0; r < PT; ++r) {
                 a1[r] = mfma_bf(p0, xs[G][r].m, a1[r]);
                 a2[r] = mfma_bf(p1, xs[G][r].m, a2[r]);
               }
             }
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
+            for (int r = 0; r < PT; ++r) {
               a1[r] = mfma_bf(p0, xs[G][r].h, a1[r]);
               a2[r] = mfma_bf(p1, xs[G][r].h, a2[r]);
             }
@@ -344,12 +390,12 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
           }
         } else {
 #pragma unroll
-          for (int G = 0; G < KP; ++G) mfma6_pair<3, true>(wl + G * kRec3, wl + (KP + G) * kRec3, xs[G], a1, a2);
+          for (int G = 0; G < KP; ++G) mfma6_pair<PT, true>(wl + G * kRec3, wl + (KP + G) * kRec3, xs[G], a1, a2);
         }
         const f32x4 b1 = lds[S::kBin + 4 * (2 * g) + lq], b2 = lds[S::kBin + 4 * (2 * g + 1) + lq];
         f32x4* img = lds + (g & 1) * kImg;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < PT; ++k) {
           if (!plv[k]) continue;
           const int px = phy[k] * kHalo + phx[k], sw = phx[k] & 7;
           img[px * 8 + (lq ^ sw)] = in[k] ? a1[k] + b1 : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -374,12 +420,7 @@ __global__ __launch_bounds__(512, 2) void ffn_fused_kernel(FfnParams p) {
           if (more) load_x1(t + nxb);  // the next tile's rows, during this chunk and the G epilogue
           // past B_kch pin(0) of the next tile reads W-in slot 0 (issued at chunk kch - 2): at most this
           // chunk's W-in pieces and the x1 loads may still be outstanding
-          switch (wi) {
-            case 0: wait_vm<S::pwin(0) + 3 * KG>(); break;
-            case 1: wait_vm<S::pwin(1) + 3 * KG>(); break;
-            case 2: wait_vm<S::pwin(2) + 3 * KG>(); break;
-            default: wait_vm<S::pwin(3) + 3 * KG>(); break;
-          }
+          wait_pin_last<S>(wi);
         } else {
           wait_vm<0>();  // W-in of chunk g + 2 (read by pin(g + 2) in the next chunk)
         }
@@ -535,12 +576,13 @@ static hipError_t launch_ffn1(const FfnParams& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr[dev] = true;
   }
-  const long long tiles = (long long)p.Bn * ((p.H + kTH - 1) / kTH) * ((p.W + kTile - 1) / kTile);
+  constexpr int TH = FfnShape<C>::TH;
+  const long long tiles = (long long)p.Bn * ((p.H + TH - 1) / TH) * ((p.W + kTile - 1) / kTile);
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   long long grid = std::min<long long>(tiles, cus);  // one resident block per CU
   grid = (grid + 7) / 8 * 8;
-  hipLaunchKernelGGL((ffn_fused_kernel<C>), dim3((unsigned)grid), dim3(512), lds, s, p);
+  hipLaunchKernelGGL((ffn_fused_kernel<C>), dim3((unsigned)grid), dim3(64 * FfnShape<C>::NW), lds, s, p);
   return hipGetLastError();
 }
 
