@@ -44,12 +44,21 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
   if (g.ksize == 1) {
     int best_nt = 0, best_w = 2;
     double best = 1e30;
+// r05: weigh one or two more weight groups than the LDS budget needs, counting every computed tile
+// (the last group's padding too).  A/B (profiles/r05zx_gemm_groups_ab.txt): C192 qkv (36 tiles) as
+// 6 groups of 6 instead of 5 of 8 (the last half empty): 588 -> 382 us per launch at 16 x 128^2.
+#ifndef KDLAE_GEMM_GROUPS_ALT
+#define KDLAE_GEMM_GROUPS_ALT 1
+#endif
+    int best_groups = 0;
     for (int w : {2}) {
       // two resident blocks per CU at 4 waves/SIMD -> half the LDS budget each
       const int budget_kb = w == 4 ? 76 : kLdsBudgetKB;
       const int budget = (int)std::max<long long>(1, budget_kb * 1024LL / tile_lds_bytes(g.kgroups));
-      const int ngroups = (int)ceil_div(g.ntiles, budget);
+      const int ngroups0 = (int)ceil_div(g.ntiles, budget);
+      for (int ngroups = ngroups0; ngroups <= ngroups0 + (KDLAE_GEMM_GROUPS_ALT ? 2 : 0); ++ngroups) {
       const int gt = (int)ceil_div(g.ntiles, ngroups);
+      if (ngroups > ngroups0 && (int)ceil_div(g.ntiles, gt) != ngroups) continue;
       for (int nt : nts) {
         if (!gemm_has_variant(nt, g.kgroups, false, w, true, g.out_mode)) continue;
         const long long padded = ceil_div(gt, nt) * nt;
@@ -64,20 +73,25 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
         // (profiles/r02_gemm_odd_nt_probe.txt); riding that tile along with the first pair instead
         // measured no gain
         if (nt % 2) cost += 0.05;
+        if (KDLAE_GEMM_GROUPS_ALT) {
+          // (with an odd-NT penalty of 0.10 the C96 qkv took 3 groups of 6 and lost 2-8%)
+          const double computed = (double)ngroups * padded / g.ntiles;
+          cost = computed * (1.0 + 0.05 * (ngroups - 1)) + 0.01 * (12 - nt) + ((nt % 2) ? 0.05 : 0.0);
+        }
         if (cost < best) {
           best = cost;
           best_nt = nt;
           best_w = w;
+          best_groups = ngroups;
         }
+      }
       }
     }
     if (best_nt) {
-      const int budget_kb = best_w == 4 ? 76 : kLdsBudgetKB;
-      const int budget = (int)std::max<long long>(1, budget_kb * 1024LL / tile_lds_bytes(g.kgroups));
       g.NT = best_nt;
       g.KG = g.kgroups;
       g.WPE = best_w;
-      g.group_tiles = (int)ceil_div(g.ntiles, ceil_div(g.ntiles, budget));
+      g.group_tiles = (int)ceil_div(g.ntiles, best_groups);
       return;
     }
   }
