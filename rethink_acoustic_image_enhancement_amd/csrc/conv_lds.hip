@@ -249,6 +249,29 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
 
   const int y = y0 + wave;
   if (y >= p.H) return;
+  if (p.out_mode == 1) {  // PixelUnshuffle(2) store (block-uniform branch)
+    const int Ho = p.H >> 1, Wo = p.W >> 1;
+    float* ob = p.out + ((long long)b * p.F + fr) * Ho * Wo * p.ldo;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int tt = t0 + n;
+      if (tt >= p.ntiles) break;
+      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + tt * 16 + 4 * lq) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int x = x0 + t * 16 + li;
+        if (x >= p.W) continue;
+        f32x4 v = acc[n][t] + bias;
+        float* o = ob + ((long long)(y >> 1) * Wo + (x >> 1)) * p.ldo + 2 * (y & 1) + (x & 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ch = tt * 16 + 4 * lq + e;
+          if (ch < p.nout) o[4 * ch] = p.relu ? fmaxf(v[e], 0.f) : v[e];
+        }
+      }
+    }
+    return;
+  }
   float* outb = p.out + ((long long)b * p.F * fhw + (long long)fr * fhw + (long long)y * p.W) * p.ldo;
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
@@ -279,7 +302,11 @@ bool conv_lds_supported(int kt, int ntiles, int cin_pad) {
 
 hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s) {
   if (!conv_lds_supported(p.kt, p.ntiles, p.cin_pad) || p.ldi % 4 || p.ldo % 4 || p.ldi < p.cin_pad ||
-      p.ldo < 16 * p.ntiles || p.kgroups != 9 * p.kt * (p.cin_pad / 16))
+      p.kgroups != 9 * p.kt * (p.cin_pad / 16))
+    return hipErrorInvalidValue;
+  if (p.out_mode == 0 ? p.ldo < 16 * p.ntiles
+                      : (p.out_mode != 1 || p.kt != 1 || p.H % 2 || p.W % 2 || p.nout <= 0 ||
+                         p.nout > 16 * p.ntiles || p.ldo < 4 * p.nout))
     return hipErrorInvalidValue;
   const long long blocks = (long long)p.Bn * p.F * ((p.H + TR - 1) / TR) * ((p.W + TC - 1) / TC);
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;

@@ -411,6 +411,9 @@ struct Plan {
 // at least 32 rows (512^2: 64 rows, the 2-row halo costs 3%; 1024^2: 128 rows; 4 and 16 segments
 // measured no better, profiles/r02_gram_nseg_probe.txt); generic kernel: 64-pixel steps grouped 16
 // per slot.
+#ifndef KDLAE_T_DOWN_LDS
+#define KDLAE_T_DOWN_LDS 1  // Downsample convs on conv_lds (0: the implicit GEMM)
+#endif
 #ifndef KDLAE_GRAM_MAXSEG  // diagnostics builds (tools/config1_taps.py) vary the slot size
 #define KDLAE_GRAM_MAXSEG 8
 #endif
@@ -540,12 +543,41 @@ struct Fwd {
     c.stats_buf = buf(pl.stats);
     int rc = probe_begin(1, probeC);
     if (rc) return rc;
+    // the Downsample convs (3x3, PixelUnshuffle store) on the LDS-tiled conv (conv_lds.hip): the
+    // implicit GEMM gathers every input pixel through L1 for each of the 9 taps and, with 24..96
+    // outputs, feeds each gathered fragment to only 2..6 MFMAs
+    const bool lds_conv = KDLAE_T_DOWN_LDS && g.ksize == 3 && out_mode == 1 && !R && !ln &&
+                          conv_lds_supported(1, g.ntiles, g.cg_per_tap * 16);
     if (h->probe_class == 1)
       tag = "gemm C" + std::to_string(probeC) + " HW" + std::to_string(HW) + " N" + std::to_string(g.n_true) + " K" +
-            std::to_string(g.k_true) + " k" + std::to_string(g.ksize) + " v" + std::to_string(g.NT) + "x" +
-            std::to_string(g.KG) + (g.group_tiles ? "r" : "c") + "w" + std::to_string(g.WPE) + (ln ? " ln" : "") +
-            (R ? " res" : "");
-    if ((rc = run_gemm(c, s))) return rc;
+            std::to_string(g.k_true) + " k" + std::to_string(g.ksize) +
+            (lds_conv ? std::string(" conv_lds") : " v" + std::to_string(g.NT) + "x" + std::to_string(g.KG) +
+                                                       (g.group_tiles ? "r" : "c") + "w" + std::to_string(g.WPE)) +
+            (ln ? " ln" : "") + (R ? " res" : "");
+    if (lds_conv) {
+      ConvLdsParams q{};
+      q.in = in.p;
+      q.ldi = in.ld;
+      q.cin_pad = g.cg_per_tap * 16;
+      q.wp = h->P(g.w);
+      q.wp3 = W;
+      q.ntiles = g.ntiles;
+      q.kgroups = g.kgroups;
+      q.bias = h->P(g.bias);
+      q.out = out.p;
+      q.ldo = out.ld;
+      q.Bn = B;
+      q.F = 1;
+      q.H = Hh;
+      q.W = Ww;
+      q.kt = 1;
+      q.relu = 0;
+      q.out_mode = 1;
+      q.nout = g.n_true;
+      HIPCHK(launch_conv_lds(q, s));
+    } else if ((rc = run_gemm(c, s))) {
+      return rc;
+    }
     const double P = (double)B * HW;
     const double kin = g.ksize == 3 ? g.k_true / 9.0 : g.k_true;
     const double bytes = 4.0 * (P * kin + P * g.n_true * (R ? 2.0 : 1.0) + (double)g.n_true * g.k_true);

@@ -215,6 +215,9 @@ struct ConvLdsParams {
   // optional: the same weights as split records (mfma3.h, pairs of consecutive k-groups); used by the
   // 2-D kernel when cin_pad % 32 == 0, where its (tap, 2-group chunk) pairs are exactly those pairs
   const float* wp3 = nullptr;
+  // store map: 0 plain [px][ldo]; 1 PixelUnshuffle(2) into the half-resolution image (KDLAE-T
+  // Downsample, KDLAE_model.py:186-187: channel 4 n + 2 (y & 1) + (x & 1)), outputs n < nout only
+  int out_mode = 0, nout = 0;
 };
 bool conv_lds_supported(int kt, int ntiles, int cin_pad);
 hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s);
