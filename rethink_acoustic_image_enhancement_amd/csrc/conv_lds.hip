@@ -272,6 +272,28 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvLdsParams p) {
     }
     return;
   }
+  if (p.out_mode == 2) {  // PixelShuffle(2) store: a lane's 4 outputs fill one 2 x 2 output block
+    const int Wo = 2 * p.W;
+    float* ob = p.out + ((long long)b * p.F + fr) * 4 * fhw * p.ldo;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int tt = t0 + n;
+      if (tt >= p.ntiles) break;
+      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + tt * 16 + 4 * lq) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int ch = tt * 4 + lq;  // (tt * 16 + 4 lq + e) >> 2
+      if (4 * ch >= p.nout) continue;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int x = x0 + t * 16 + li;
+        if (x >= p.W) continue;
+        f32x4 v = acc[n][t] + bias;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          ob[((long long)(2 * y + (e >> 1)) * Wo + 2 * x + (e & 1)) * p.ldo + ch] = p.relu ? fmaxf(v[e], 0.f) : v[e];
+      }
+    }
+    return;
+  }
   float* outb = p.out + ((long long)b * p.F * fhw + (long long)fr * fhw + (long long)y * p.W) * p.ldo;
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
@@ -305,8 +327,10 @@ hipError_t launch_conv_lds(const ConvLdsParams& p, hipStream_t s) {
       p.kgroups != 9 * p.kt * (p.cin_pad / 16))
     return hipErrorInvalidValue;
   if (p.out_mode == 0 ? p.ldo < 16 * p.ntiles
-                      : (p.out_mode != 1 || p.kt != 1 || p.H % 2 || p.W % 2 || p.nout <= 0 ||
-                         p.nout > 16 * p.ntiles || p.ldo < 4 * p.nout))
+      : p.out_mode == 1 ? (p.kt != 1 || p.H % 2 || p.W % 2 || p.nout <= 0 || p.nout > 16 * p.ntiles ||
+                           p.ldo < 4 * p.nout)
+      : p.out_mode == 2 ? (p.kt != 1 || p.nout <= 0 || p.nout % 4 || p.nout > 16 * p.ntiles || 4 * p.ldo < p.nout)
+                        : true)
     return hipErrorInvalidValue;
   const long long blocks = (long long)p.Bn * p.F * ((p.H + TR - 1) / TR) * ((p.W + TC - 1) / TC);
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;

@@ -414,6 +414,9 @@ struct Plan {
 #ifndef KDLAE_T_DOWN_LDS
 #define KDLAE_T_DOWN_LDS 1  // Downsample convs on conv_lds (0: the implicit GEMM)
 #endif
+#ifndef KDLAE_T_UP_LDS
+#define KDLAE_T_UP_LDS 1  // Upsample convs on conv_lds (0: the implicit GEMM)
+#endif
 #ifndef KDLAE_GRAM_MAXSEG  // diagnostics builds (tools/config1_taps.py) vary the slot size
 #define KDLAE_GRAM_MAXSEG 8
 #endif
@@ -546,8 +549,8 @@ struct Fwd {
     // the Downsample convs (3x3, PixelUnshuffle store) on the LDS-tiled conv (conv_lds.hip): the
     // implicit GEMM gathers every input pixel through L1 for each of the 9 taps and, with 24..96
     // outputs, feeds each gathered fragment to only 2..6 MFMAs
-    const bool lds_conv = KDLAE_T_DOWN_LDS && g.ksize == 3 && out_mode == 1 && !R && !ln &&
-                          conv_lds_supported(1, g.ntiles, g.cg_per_tap * 16);
+    const bool lds_conv = g.ksize == 3 && ((KDLAE_T_DOWN_LDS && out_mode == 1) || (KDLAE_T_UP_LDS && out_mode == 2)) &&
+                          !R && !ln && conv_lds_supported(1, g.ntiles, g.cg_per_tap * 16);
     if (h->probe_class == 1)
       tag = "gemm C" + std::to_string(probeC) + " HW" + std::to_string(HW) + " N" + std::to_string(g.n_true) + " K" +
             std::to_string(g.k_true) + " k" + std::to_string(g.ksize) +
@@ -572,7 +575,7 @@ struct Fwd {
       q.W = Ww;
       q.kt = 1;
       q.relu = 0;
-      q.out_mode = 1;
+      q.out_mode = out_mode;
       q.nout = g.n_true;
       HIPCHK(launch_conv_lds(q, s));
     } else if ((rc = run_gemm(c, s))) {

@@ -216,7 +216,9 @@ struct ConvLdsParams {
   // 2-D kernel when cin_pad % 32 == 0, where its (tap, 2-group chunk) pairs are exactly those pairs
   const float* wp3 = nullptr;
   // store map: 0 plain [px][ldo]; 1 PixelUnshuffle(2) into the half-resolution image (KDLAE-T
-  // Downsample, KDLAE_model.py:186-187: channel 4 n + 2 (y & 1) + (x & 1)), outputs n < nout only
+  // Downsample, KDLAE_model.py:186-187: channel 4 n + 2 (y & 1) + (x & 1)); 2 PixelShuffle(2) into the
+  // double-resolution image (Upsample, :196-197: output n -> pixel (2y + (n >> 1 & 1), 2x + (n & 1)),
+  // channel n >> 2); outputs n < nout only
   int out_mode = 0, nout = 0;
 };
 bool conv_lds_supported(int kt, int ntiles, int cin_pad);
