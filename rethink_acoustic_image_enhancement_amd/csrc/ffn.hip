@@ -305,10 +305,25 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
     }
   };
 
+// Wave issue priority (s_setprio) of the P / G roles (A/B knobs; 0 = the default priority).  r05 A/B
+// (profiles/r05p_ffn_prio_ab.txt): the P waves at priority 1..3 over the G waves, C48@1024^2
+// 8.17-8.34 -> 7.83-7.88 ms per launch, C96 unchanged within noise; P priority only in the tile
+// prologue (3, then 0 in the chunk loop) no gain; the G waves raised instead: smaller gain.
+#ifndef KDLAE_FFN_PRIO_P
+#define KDLAE_FFN_PRIO_P 1
+#endif
+#ifndef KDLAE_FFN_PRIO_G
+#define KDLAE_FFN_PRIO_G 0
+#endif
+#ifndef KDLAE_FFN_PRIO_P_LOOP  // P priority inside the chunk loop (-1: the same as KDLAE_FFN_PRIO_P)
+#define KDLAE_FFN_PRIO_P_LOOP -1
+#endif
   if (gw) {
+    if (KDLAE_FFN_PRIO_G) __builtin_amdgcn_s_setprio(KDLAE_FFN_PRIO_G);
     issue_w(0, 0);
     wait_vm<0>();
   } else {
+    if (KDLAE_FFN_PRIO_P) __builtin_amdgcn_s_setprio(KDLAE_FFN_PRIO_P);
     issue_win(0);
     issue_win(1);
     wait_vm<0>();
@@ -331,6 +346,7 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
       tile_geo(t, b, x0, y0);
       (void)b;
       // ================================================================ P waves: project_in producer
+      if (KDLAE_FFN_PRIO_P_LOOP >= 0) __builtin_amdgcn_s_setprio(KDLAE_FFN_PRIO_P);
       F3 xs[KP][PT];
       bool in[PT];
 #pragma unroll
@@ -404,6 +420,7 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
       };
       pin(0);
       lds_barrier();  // B_0
+      if (KDLAE_FFN_PRIO_P_LOOP >= 0) __builtin_amdgcn_s_setprio(KDLAE_FFN_PRIO_P_LOOP);
       const bool more = t + nxb < t_hi;
       for (int g = 0; g < kch; ++g) {
         FFN_ST(s0);
