@@ -55,6 +55,11 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (vector = MFMA f32), MI355X_MICRO
 # 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz = 2516.6 TF/s bf16 -> 419.4 TF/s of fp32 products.
 PEAK_SPLIT_TFLOPS = 2516.6 / 6
 PEAK_HBM_GBS = 8000.0      # HBM3E spec
+# roofline definition versions: 1 (r01-r04) = the GEMM class (probe 1) against the 157.3 TF/s fp32 MFMA
+# peak; 2 (r05-) = the dominant class by share of step (the feed-forward half, probe 3) against the
+# 419.4 TF/s split-bf16 ceiling, the fp32-peak fraction kept as compute_view.frac_of_fp32_mfma_peak
+ROOF_DEF_VERSION = 2
+NESTED_TRAIN_STEPS, NESTED_TRAIN_WARMUP = 20, 5  # the training leg nested in the default T16 line
 PROBE_CLASSES = {1: "conv_gemm (split-bf16 MFMA 1x1 / implicit-GEMM 3x3)", 2: "dwconv_gram (MDTA pass 1)",
                  3: "feed-forward half (fused FFN / GDFN tail)"}
 
@@ -288,11 +293,13 @@ def bench_secondary(args, world, rank, dev, distributed, workload, batch=0, size
             "peak_definition": "fp32 products via split-bf16 MFMAs: dense bf16 2516.6 TF/s / 6",
             "traffic": None, "kernel": "whole forward (all launches)", "algorithmic_flops_per_step": flops}
     tr = pmc_workload_traffic(workload) if (B, H) == ((8, 512) if workload == "s8" else (64, 256)) else None
-    if tr is not None:  # HBM bytes of one forward of this exact batch, and the rate they imply here
-        roof["traffic"], roof["traffic_source"] = tr
+    if tr is not None:  # HBM bytes of one forward of this exact batch from a recorded PMC pass
+        roof["traffic"], roof["traffic_source"], same = tr
         roof["traffic_unit"] = "bytes per forward (all launches)"
-        roof["traffic_rate_GBps"] = round(tr[0] * args.steps / (dev_ms / 1e3) / 1e9, 1)
-        roof["traffic_frac_of_hbm"] = round(roof["traffic_rate_GBps"] / PEAK_HBM_GBS, 4)
+        roof["traffic_same_build"] = same  # the PMC pass profiled this exact libkdlae.so (sha256)
+        if same:  # the rate those bytes imply at this run's step time (only for the profiled build)
+            roof["traffic_rate_GBps"] = round(tr[0] * args.steps / (dev_ms / 1e3) / 1e9, 1)
+            roof["traffic_frac_of_hbm"] = round(roof["traffic_rate_GBps"] / PEAK_HBM_GBS, 4)
     total = world * B * args.steps
     res = {"metric": metric, "value": round(total / elapsed, 3), "unit": "images/s" if workload == "a64"
            else "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -327,15 +334,18 @@ def bench_secondary(args, world, rank, dev, distributed, workload, batch=0, size
     return res
 
 
-def bench_train(args, world, rank, dev, distributed):
+def bench_train(args, world, rank, dev, distributed, nested=False):
     """KDLAE-T training iterations: ImageCleanModel.optimize_parameters with the
     KDLAET.yml fixed-patch setting (batch_size_per_gpu 6, gt_size 128, AdamW lr 1e-5 wd 5e-5 betas
     (0.2, 0.999), clip_grad_norm_ 0.01, L1LossSr); for N>1 every step all-reduces the flat gradient
-    (107.5 MB) over RCCL, as DDP does.  One step = forward + loss + backward + all-reduce + clip + AdamW."""
+    (107.5 MB) over RCCL, as DDP does.  One step = forward + loss + backward + all-reduce + clip + AdamW.
+    nested: timed inside the default T16 run (its own steps / warm-up, no CPU baseline); returns the
+    result instead of printing it."""
     from rethink_acoustic_image_enhancement_amd.train import KDLAETrainer
 
-    B = args.batch or 6
-    H = W = args.size or 128
+    B = 6 if nested else (args.batch or 6)
+    H = W = 128 if nested else (args.size or 128)
+    steps, warmup = (NESTED_TRAIN_STEPS, NESTED_TRAIN_WARMUP) if nested else (args.steps, args.warmup)
     model = KDLAE_teacher(**KW)
     load_hash_weights(model)
     model = model.to(dev)
@@ -356,7 +366,7 @@ def bench_train(args, world, rank, dev, distributed):
         return trainer.optimize_parameters(lq_m, gt_m)
 
     loss = None
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         loss = train_step()
     torch.cuda.synchronize(dev)
     if distributed:
@@ -365,7 +375,7 @@ def bench_train(args, world, rank, dev, distributed):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss = train_step()
     ev1.record()
     torch.cuda.synchronize(dev)
@@ -378,11 +388,11 @@ def bench_train(args, world, rank, dev, distributed):
         elapsed = float(t.item())
     # SURVEY §8d forward FLOPs (1.9177 TFLOP per 512^2 image, linear in pixels) x 3 for fwd + dX + dW
     flops = 3 * 1.9177e12 * (H * W) / (512 * 512) * B
-    ach = flops * args.steps / (dev_ms / 1e3) / 1e12
-    total = world * B * args.steps
+    ach = flops * steps / (dev_ms / 1e3) / 1e12
+    total = world * B * steps
     res = {"metric": "images/sec KDLAE-T training step 128x128 patches fp32 (KDLAET.yml, SURVEY 8f rank 1)",
-           "value": round(total / elapsed, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+           "value": round(total / elapsed, 3), "unit": "images/s", "n_gpus": world, "steps": steps,
+           "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 2), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
            "data": "synthetic (hash-uniform images and targets, hash weights of the real architecture)",
            "config": {"workload": f"KDLAE-T train step bs={B}/GPU {H}x{W} (+sr {2 * H}x{2 * W}), L1LossSr, "
@@ -394,6 +404,8 @@ def bench_train(args, world, rank, dev, distributed):
                         "kernel": "whole training step (all launches, algorithmic 3x forward FLOPs)",
                         "algorithmic_flops_per_step": flops},
            "final_loss": float(loss)}
+    if nested:
+        return res
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.kdlae_oracle import TeacherCfg
         from oracle.train_oracle import TrainStep
@@ -532,6 +544,8 @@ def main():
     ap.add_argument("--no-bs1", action="store_true", help="t16: skip the single-image latency line")
     ap.add_argument("--no-secondary", action="store_true",
                     help="t16: skip the S8 / A64 lines (BASELINE configs[2], [3]) nested in the output")
+    ap.add_argument("--no-train", action="store_true",
+                    help="t16: skip the KDLAE-T training step (SURVEY 8f rank 1) nested in the output")
     ap.add_argument("--cpu-standin", action="store_true",
                     help="CPU rehearsal of the N-rank launch/shard/timing path (gloo, stand-in forward; tests)")
     args = ap.parse_args()
@@ -644,6 +658,7 @@ def main():
             ach = by.value / sec / 1e9
             r = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                  "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
+        r["definition_version"] = ROOF_DEF_VERSION
         if fl.value:  # the FLOP side of the same launches, against both fp32-product peaks
             tf = fl.value / sec / 1e12
             r["compute_view"] = {"achieved_tflops": round(tf, 2),
@@ -653,8 +668,8 @@ def main():
                                          "ceiling of this arithmetic, the fp32 MFMA peak (157.3) the "
                                          "ceiling of the r04 kernels"}
         tr = pmc_traffic(cls)
-        if tr is not None:
-            r["traffic"], r["traffic_source"] = tr
+        if tr is not None:  # PMC HBM bytes per launch from a recorded pass; same_build: that pass
+            r["traffic"], r["traffic_source"], r["traffic_same_build"] = tr  # profiled this exact .so
         if launch_roof is not None:
             r["per_shape_roof"] = launch_roof
         r.update({"kernel": PROBE_CLASSES[cls], "launches": int(n.value),
@@ -755,6 +770,15 @@ def main():
             keep = ("metric", "value", "unit", "ms_per_step", "config", "roofline", "cpu_baseline", "parity")
             res[wl] = {k: sec[k] for k in keep if k in sec}
             torch.cuda.empty_cache()
+    if not args.no_train and not args.batch and not args.size:
+        # SURVEY §8f rank 1, KDLAET.yml's 6 x 128^2 step, timed in the same run
+        if "model" in locals():
+            del model, batch, out, eng
+        torch.cuda.empty_cache()
+        tr = bench_train(args, world, rank, dev, distributed, nested=True)
+        keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "config", "roofline", "final_loss")
+        res["train"] = {k: tr[k] for k in keep if k in tr}
+        torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if distributed:
@@ -784,6 +808,16 @@ def per_launch_roof(path):
                           "419.4 TF/s (split-bf16 fp32 products), hbm_peak = 8 TB/s"}
 
 
+def lib_sha256():
+    """sha256 of the libkdlae.so this process loaded (KDLAE_LIB or the in-tree build)."""
+    import hashlib
+    path = os.environ.get("KDLAE_LIB") or os.path.join(ROOT, "rethink_acoustic_image_enhancement_amd", "libkdlae.so")
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
 def pmc_traffic(cls):
     """HBM bytes per launch of a kernel class from the committed rocprofv3 PMC summary
     (profiles/*pmc_traffic*.json, produced by tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE)."""
@@ -800,7 +834,7 @@ def pmc_traffic(cls):
     c = d.get("classes", {}).get(str(cls))
     if not c:
         return None
-    return c["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return c["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT), d.get("lib_sha256") == lib_sha256()
 
 
 def pmc_workload_traffic(workload):
@@ -812,7 +846,7 @@ def pmc_workload_traffic(workload):
         return None
     with open(files[-1]) as f:
         d = json.load(f)
-    return d["traffic_bytes_per_forward"], os.path.relpath(files[-1], ROOT)
+    return d["traffic_bytes_per_forward"], os.path.relpath(files[-1], ROOT), d.get("lib_sha256") == lib_sha256()
 
 
 def cpu_baseline(model, batch, out, threads):

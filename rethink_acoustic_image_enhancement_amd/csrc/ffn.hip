@@ -57,25 +57,13 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-#ifndef KDLAE_FFN_UNIFORM_DMA
-#define KDLAE_FFN_UNIFORM_DMA 48
-#endif
 // every wave issues the same number of DMA pieces, straight-line (piece k = w + 4 j; the padding
 // pieces past the chunk's last read nothing and land in a dummy slot): no per-piece branch.  A/B
 // (profiles/r05r_ffn_dma_ab.txt): C = 48 -5%, C = 96 +4% (3 more spilled VGPRs), so C = 48 only
-// (the knob: 0 = never, 1 = both widths, 48 / 96 = that width)
 template <int C>
 constexpr bool uniform_dma() {
-  return KDLAE_FFN_UNIFORM_DMA == 1 || KDLAE_FFN_UNIFORM_DMA == C;
+  return C == 48;
 }
-#ifndef KDLAE_FFN_PIN_PIPE
-#define KDLAE_FFN_PIN_PIPE 1
-#endif
-constexpr bool kPinPipe = KDLAE_FFN_PIN_PIPE != 0;  // project_in W planes read one step ahead
-#ifndef KDLAE_FFN_ABL
-#define KDLAE_FFN_ABL 0  // timing-only ablations (wrong outputs): 1 no gate, 2 no gate + no project_out,
-                         // 3 no project_in in the chunk loop
-#endif
 #ifdef KDLAE_FFN_STAMPS
 // Diagnostic build only (tools/ffn_stamps.py): per-segment cycle sums of every wave, [C48 / C96][P / G]
 // [segment]; the stamps fence the schedule, so read shares, not lengths.
@@ -94,28 +82,19 @@ __device__ __forceinline__ unsigned long long stamp() {
 #define FFN_ADD(k, d)
 #endif
 
-// Tile shape and wave counts (A/B knobs for C = 48; C = 96's LDS has room for nothing larger than its
-// 16 x 8 tile with 4 P + 4 G waves).  r05 same-box A/B on C48@1024^2 (profiles/r05zv_ffn48_shape_ab.txt):
-// the default 16 x 8 tile, 4 + 4 waves 8.09-8.11 ms; a 16 x 12 tile (halo 1.31x instead of 1.41x,
-// 4 + 4 waves, 17 spilled VGPRs) 8.05 ms; 12 waves (3 per SIMD, 168 VGPRs each) spill 35-130 VGPRs:
-// 4 P + 8 G 10.37 ms, 8 P + 4 G 11.65 ms.
-#ifndef KDLAE_FFN48_TH
-#define KDLAE_FFN48_TH 8
-#endif
-#ifndef KDLAE_FFN_NP
-#define KDLAE_FFN_NP 4
-#endif
-#ifndef KDLAE_FFN48_NGW
-#define KDLAE_FFN48_NGW 4
-#endif
+// Tile shape and wave counts.  C = 96's LDS has room for nothing larger than its 16 x 8 tile with
+// 4 P + 4 G waves; for C = 48 r05 same-box A/B on C48@1024^2 (profiles/r05zv_ffn48_shape_ab.txt): the
+// 16 x 8 tile, 4 + 4 waves 8.09-8.11 ms; a 16 x 12 tile (halo 1.31x instead of 1.41x, 17 spilled
+// VGPRs) 8.05 ms; 12 waves (3 per SIMD, 168 VGPRs each) spill 35-130 VGPRs: 4 P + 8 G 10.37 ms,
+// 8 P + 4 G 11.65 ms.
 template <int C>
 struct FfnShape {
-  static constexpr int TH = C == 48 ? KDLAE_FFN48_TH : 8;  // interior rows per tile
+  static constexpr int TH = 8;                             // interior rows per tile
   static constexpr int HR = TH + 2;                        // halo rows
-  static constexpr int NGW = C == 48 ? KDLAE_FFN48_NGW : 4;  // G waves: TH / NGW output rows each
+  static constexpr int NGW = 4;                            // G waves: TH / NGW output rows each
   static constexpr int RPW = TH / NGW;
   static constexpr int NPT = HR + 2;                       // halo pixel tiles of 16: HR rows, 2 columns
-  static constexpr int NP = C == 48 ? KDLAE_FFN_NP : 4;    // P waves
+  static constexpr int NP = 4;                             // P waves
   static constexpr int PT = (NPT + NP - 1) / NP;           // halo pixel tiles per P wave
   static constexpr int NW = NP + NGW;
   static constexpr int Img = HR * kHalo * 8;               // f32x4 per halo image slot
@@ -305,25 +284,15 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
     }
   };
 
-// Wave issue priority (s_setprio) of the P / G roles (A/B knobs; 0 = the default priority).  r05 A/B
-// (profiles/r05p_ffn_prio_ab.txt): the P waves at priority 1..3 over the G waves, C48@1024^2
-// 8.17-8.34 -> 7.83-7.88 ms per launch, C96 unchanged within noise; P priority only in the tile
-// prologue (3, then 0 in the chunk loop) no gain; the G waves raised instead: smaller gain.
-#ifndef KDLAE_FFN_PRIO_P
-#define KDLAE_FFN_PRIO_P 1
-#endif
-#ifndef KDLAE_FFN_PRIO_G
-#define KDLAE_FFN_PRIO_G 0
-#endif
-#ifndef KDLAE_FFN_PRIO_P_LOOP  // P priority inside the chunk loop (-1: the same as KDLAE_FFN_PRIO_P)
-#define KDLAE_FFN_PRIO_P_LOOP -1
-#endif
+  // The P waves at issue priority 1 (s_setprio): the SIMD's arbiter favours the project_in producer
+  // over the gate wave it shares the SIMD with.  r05 A/B (profiles/r05p_ffn_prio_ab.txt): C48@1024^2
+  // 8.17-8.34 -> 7.83-7.88 ms per launch, C96 unchanged within noise; the G waves raised instead, or
+  // P priority only in the tile prologue: smaller gains.
   if (gw) {
-    if (KDLAE_FFN_PRIO_G) __builtin_amdgcn_s_setprio(KDLAE_FFN_PRIO_G);
     issue_w(0, 0);
     wait_vm<0>();
   } else {
-    if (KDLAE_FFN_PRIO_P) __builtin_amdgcn_s_setprio(KDLAE_FFN_PRIO_P);
+    __builtin_amdgcn_s_setprio(1);
     issue_win(0);
     issue_win(1);
     wait_vm<0>();
@@ -346,7 +315,6 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
       tile_geo(t, b, x0, y0);
       (void)b;
       // ================================================================ P waves: project_in producer
-      if (KDLAE_FFN_PRIO_P_LOOP >= 0) __builtin_amdgcn_s_setprio(KDLAE_FFN_PRIO_P);
       F3 xs[KP][PT];
       bool in[PT];
 #pragma unroll
@@ -367,46 +335,41 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
         f32x4 a1[PT], a2[PT];
 #pragma unroll
         for (int k = 0; k < PT; ++k) a1[k] = a2[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (kPinPipe) {
-          // the W planes one step ahead of their MFMAs (steps = (pair, plane l / m / h): mfma6_pair's
-          // term order), fenced so each step's reads issue under the previous step's MFMAs
-          bf16x8 w[2][2];
-          auto ld = [&](int st, int buf) {
-            const int G = st / 3, off = (2 - (st - 3 * G)) * 64;  // planes l, m, h at +128, +64, +0
-            w[buf][0] = __builtin_bit_cast(bf16x8, wl[G * kRec3 + off]);
-            w[buf][1] = __builtin_bit_cast(bf16x8, wl[(KP + G) * kRec3 + off]);
-          };
-          ld(0, 0);
+        // the W planes one step ahead of their MFMAs (steps = (pair, plane l / m / h): mfma6_pair's
+        // term order), fenced so each step's reads issue under the previous step's MFMAs
+        bf16x8 w[2][2];
+        auto ld = [&](int st, int buf) {
+          const int G = st / 3, off = (2 - (st - 3 * G)) * 64;  // planes l, m, h at +128, +64, +0
+          w[buf][0] = __builtin_bit_cast(bf16x8, wl[G * kRec3 + off]);
+          w[buf][1] = __builtin_bit_cast(bf16x8, wl[(KP + G) * kRec3 + off]);
+        };
+        ld(0, 0);
 #pragma unroll
-          for (int st = 0; st < 3 * KP; ++st) {
-            if (st + 1 < 3 * KP) ld(st + 1, (st + 1) & 1);
-            __builtin_amdgcn_sched_barrier(0);
-            const int G = st / 3, pl = st - 3 * G;
-            const bf16x8 p0 = w[st & 1][0], p1 = w[st & 1][1];
-            if (pl == 2) {
-#pragma unroll
-              for (int r = 0; r < PT; ++r) {
-                a1[r] = mfma_bf(p0, xs[G][r].l, a1[r]);
-                a2[r] = mfma_bf(p1, xs[G][r].l, a2[r]);
-              }
-            }
-            if (pl >= 1) {
-#pragma unroll
-              for (int r = 0; r < PT; ++r) {
-                a1[r] = mfma_bf(p0, xs[G][r].m, a1[r]);
-                a2[r] = mfma_bf(p1, xs[G][r].m, a2[r]);
-              }
-            }
+        for (int st = 0; st < 3 * KP; ++st) {
+          if (st + 1 < 3 * KP) ld(st + 1, (st + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+          const int G = st / 3, pl = st - 3 * G;
+          const bf16x8 p0 = w[st & 1][0], p1 = w[st & 1][1];
+          if (pl == 2) {
 #pragma unroll
             for (int r = 0; r < PT; ++r) {
-              a1[r] = mfma_bf(p0, xs[G][r].h, a1[r]);
-              a2[r] = mfma_bf(p1, xs[G][r].h, a2[r]);
+              a1[r] = mfma_bf(p0, xs[G][r].l, a1[r]);
+              a2[r] = mfma_bf(p1, xs[G][r].l, a2[r]);
             }
-            __builtin_amdgcn_sched_barrier(0);
           }
-        } else {
+          if (pl >= 1) {
 #pragma unroll
-          for (int G = 0; G < KP; ++G) mfma6_pair<PT, true>(wl + G * kRec3, wl + (KP + G) * kRec3, xs[G], a1, a2);
+            for (int r = 0; r < PT; ++r) {
+              a1[r] = mfma_bf(p0, xs[G][r].m, a1[r]);
+              a2[r] = mfma_bf(p1, xs[G][r].m, a2[r]);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < PT; ++r) {
+            a1[r] = mfma_bf(p0, xs[G][r].h, a1[r]);
+            a2[r] = mfma_bf(p1, xs[G][r].h, a2[r]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
         const f32x4 b1 = lds[S::kBin + 4 * (2 * g) + lq], b2 = lds[S::kBin + 4 * (2 * g + 1) + lq];
         f32x4* img = lds + (g & 1) * kImg;
@@ -420,18 +383,13 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
       };
       pin(0);
       lds_barrier();  // B_0
-      if (KDLAE_FFN_PRIO_P_LOOP >= 0) __builtin_amdgcn_s_setprio(KDLAE_FFN_PRIO_P_LOOP);
       const bool more = t + nxb < t_hi;
       for (int g = 0; g < kch; ++g) {
         FFN_ST(s0);
         // W-in slot g & 1 was last read by pin(g) (before B_g): chunk g + 2 (mod kch: the next tile)
         issue_win((g + 2) % kch);
         FFN_ST(s1);
-#if KDLAE_FFN_ABL == 3
-        if (g + 1 < kch && lds[0].x == 12345.f) pin(g + 1);  // ablation: (never) project_in
-#else
         if (g + 1 < kch) pin(g + 1);
-#endif
         FFN_ST(s2);
         if (g == kch - 1) {
           if (more) load_x1(t + nxb);  // the next tile's rows, during this chunk and the G epilogue
@@ -485,18 +443,10 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
         if ((g & 1) == 0) issue_w((g >> 1) + 1 < npairs ? (g >> 1) + 1 : 0, (pc + 1) & 1);
         FFN_ST(s1);
         f32x4 gn[kRPW];
-#if KDLAE_FFN_ABL == 1 || KDLAE_FFN_ABL == 2
-        for (int r = 0; r < kRPW; ++r) gn[r] = sl[lo[0][1] + r * kHalo * 8];  // ablation: no gate
-#else
         gate_rows<kRPW, kGeluPacked>(sl, lds + S::kDw + g * kDwF4, lo, lq, gn);
-#endif
         FFN_ST(s2);
         if (g & 1) {
-#if KDLAE_FFN_ABL == 2
-          if (gn[0].x == 12345.f) mfma_pair(gbp, gn, pc & 1);  // ablation: (never) project_out
-#else
           mfma_pair(gbp, gn, pc & 1);  // chunks g - 1, g
-#endif
           ++pc;
         } else {
 #pragma unroll

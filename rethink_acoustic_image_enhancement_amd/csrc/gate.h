@@ -9,10 +9,7 @@ namespace gdfnc {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef KDLAE_GELU_PACKED
-#define KDLAE_GELU_PACKED 1
-#endif
-constexpr bool kGeluPacked = KDLAE_GELU_PACKED != 0;  // A/B knob: packed-FP32 GELU gate
+constexpr bool kGeluPacked = true;  // packed-FP32 GELU gate in the C = 48 / 96 kernels
 constexpr int kTile = 16;                          // output tile width (pixels)
 constexpr int kHalo = kTile + 2;                   // 18 halo columns
 constexpr int kDwF4 = 128;                         // per-chunk dw block: [9][8] weights, [8] bias, pad
@@ -22,9 +19,6 @@ constexpr int kDwF4 = 128;                         // per-chunk dw block: [9][8]
 // interleaved with.  The GELU error is <= 7.5e-8 |x|, at the level of fp32 rounding of the result.
 __device__ __forceinline__ float gelu_erf_g(float x) {
 #pragma clang fp contract(off)  // every fused multiply-add is written out: the same bits in every kernel
-#ifdef KDLAE_PRECISE_GELU  // diagnostics build (tools/config1_taps.py): the device library's erff
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
-#endif
   const float z = fabsf(x) * 0.70710678118654752f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
   float poly = fmaf(1.061405429f, t, -1.453152027f);
@@ -43,9 +37,6 @@ __device__ __forceinline__ float gelu_erf_g(float x) {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_gate2(f32x2 x, f32x2 v) {
 #pragma clang fp contract(off)
-#ifdef KDLAE_PRECISE_GELU
-  return f32x2{gelu_erf_g(x.x) * v.x, gelu_erf_g(x.y) * v.y};
-#endif
   const f32x2 z = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
   const f32x2 a = __builtin_elementwise_fma(f32x2{0.3275911f, 0.3275911f}, z, f32x2{1.0f, 1.0f});
   const f32x2 t = f32x2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)};

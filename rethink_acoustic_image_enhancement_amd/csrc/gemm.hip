@@ -366,19 +366,14 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* base, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)bytes, 0x00020000);
 }
-// cache policy of the streaming activation loads / output stores (gfx950 CPol: 1 sc0, 2 nt, 16 sc1);
-// A/B knobs, default policy
-#ifndef KDLAE_GEMM_LD_POL
-#define KDLAE_GEMM_LD_POL 0
-#endif
-#ifndef KDLAE_GEMM_ST_POL
-#define KDLAE_GEMM_ST_POL 0
-#endif
+// cache policy of the streaming activation loads / output stores: the default (0).  r05 A/B
+// (profiles/r05zz4_cache_policy_ab.txt): non-temporal stores or loads were level or slower on every shape
+constexpr int kLdPol = 0, kStPol = 0;
 __device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, KDLAE_GEMM_LD_POL));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kLdPol));
 }
 __device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, KDLAE_GEMM_ST_POL);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, kStPol);
 }
 constexpr unsigned kOOB = 0x80000000u;  // a byte offset past every descriptor's range
 
@@ -389,21 +384,12 @@ constexpr unsigned kOOB = 0x80000000u;  // a byte offset past every descriptor's
 // by side over the same tiles, and all but the first read of each A tile hit that XCD's L2 instead
 // of HBM (with x-fastest 2-D grids the first ceil(gx / CUs) rounds were all group 0: every group
 // re-read A from HBM).  gy = 1 keeps bx = id.  Ids past gx (the round-up to 8) exit.
-#ifndef KDLAE_GEMM_XCD_PAIR
-#define KDLAE_GEMM_XCD_PAIR 1
-#endif
 __device__ __forceinline__ void block_tile_group(int gy, int& bx, int& by) {
-  if (!KDLAE_GEMM_XCD_PAIR) {
-    bx = blockIdx.x;
-    by = blockIdx.y;
-    return;
-  }
   const int id = blockIdx.x, sgrp = id / (8 * gy), r = id - sgrp * 8 * gy;
   by = r >> 3;
   bx = sgrp * 8 + (r & 7);
 }
 static dim3 gemm_grid(int grid_x, int grid_y) {
-  if (!KDLAE_GEMM_XCD_PAIR) return dim3(grid_x, grid_y);
   return dim3((unsigned)(((grid_x + 7) / 8) * 8 * grid_y));
 }
 
@@ -560,7 +546,7 @@ __global__ __launch_bounds__(kGemmThreads * WPE / 2, WPE) void gemm_res_kernel(G
             f32x4 v = (q == 0 ? a0[r] : a1[r]) + bias;
             if constexpr (HASR) v += rs[q][r];
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
-                                                   tile_voff(ch * NT + t + q, vo[r], o_bytes), 0, KDLAE_GEMM_ST_POL);
+                                                   tile_voff(ch * NT + t + q, vo[r], o_bytes), 0, kStPol);
           }
         }
       }
@@ -594,7 +580,7 @@ __global__ __launch_bounds__(kGemmThreads * WPE / 2, WPE) void gemm_res_kernel(G
           f32x4 v = acc[t][r] + bias;
           if constexpr (HASR) v += res[t][r];
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro, tile_voff(ch * NT + t, vo[r], o_bytes),
-                                                 0, KDLAE_GEMM_ST_POL);
+                                                 0, kStPol);
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
@@ -676,10 +662,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
   // v rows are prefetched a tile ahead at K = 48; at K = 96 the extra 48 VGPRs would spill, and the
   // SIMD partner wave's MFMAs cover the load instead
   constexpr bool PFV = KG < 6;
-#ifndef KDLAE_ATTN_IN_PFX
-#define KDLAE_ATTN_IN_PFX 0
-#endif
-  constexpr bool PFX = PFV && KDLAE_ATTN_IN_PFX;  // x rows a tile ahead as well
+  constexpr bool PFX = false;  // x rows a tile ahead as well: r04 A/B no gain (kept for the layout notes)
   f32x4 a[kGemmRT][KG];
   [[maybe_unused]] f32x4 an[kGemmRT][KG];
   [[maybe_unused]] f32x4 xn[kGemmRT][KG];
@@ -764,7 +747,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_attn_in_kernel(GemmParam
 #pragma unroll
         for (int r = 0; r < kGemmRT; ++r)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t][r] + bias), ro,
-                                                 tile_voff(ch * NT + t, vo[r], o_bytes), 0, KDLAE_GEMM_ST_POL);
+                                                 tile_voff(ch * NT + t, vo[r], o_bytes), 0, kStPol);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep one chunk's accumulators live at a time
     }
@@ -1033,14 +1016,12 @@ static hipError_t launch_variant(const GemmParams& p, int grid_x, int grid_y, si
 template <int NT, int KG, int NCH>
 constexpr bool res2_hasr_ok() { return NT * NCH <= 12 && NT * NCH * KG <= 72 && KG <= 8; }
 
-// waves per SIMD of the resident kernel for K <= 96 (A/B knob): 2 = 8 waves x 32 rows, 4 = 16 waves x 16 rows
-#ifndef KDLAE_RES_WPE
-#define KDLAE_RES_WPE 2
-#endif
+// waves per SIMD of the resident kernel: 2 = 8 waves x 32 rows (16 waves x 16 rows at K <= 96 measured
+// no faster in r05)
 template <int NT, int KG, int NCH, bool PF>
 static hipError_t launch_res2(const GemmParams& p, int grid_x, int grid_y, size_t lds, hipStream_t s) {
   constexpr bool RK = res2_hasr_ok<NT, KG, NCH>();
-  constexpr int W = (KDLAE_RES_WPE == 4 && KG <= 6) ? 4 : 2;
+  constexpr int W = 2;
   constexpr int TH = kGemmThreads * W / 2;
   static size_t attr_lds[64] = {};
   int dev = 0;

@@ -417,16 +417,11 @@ struct Plan {
 #ifndef KDLAE_T_UP_LDS
 #define KDLAE_T_UP_LDS 1  // Upsample convs on conv_lds (0: the implicit GEMM)
 #endif
-#ifndef KDLAE_GRAM_MAXSEG  // diagnostics builds (tools/config1_taps.py) vary the slot size
-#define KDLAE_GRAM_MAXSEG 8
-#endif
-#ifndef KDLAE_GRAM_MINROWS
-#define KDLAE_GRAM_MINROWS 32
-#endif
+constexpr int kGramMaxSeg = 8, kGramMinRows = 32;  // Gram slots: row segments per strip, rows per segment
 static int nslots_for(int H, int W, int /*B*/, int /*heads*/) {
   if (W % 16 == 0) {
     const int strips = W / 16;
-    const int nseg = std::max(1, std::min(KDLAE_GRAM_MAXSEG, (H + KDLAE_GRAM_MINROWS - 1) / KDLAE_GRAM_MINROWS));
+    const int nseg = std::max(1, std::min(kGramMaxSeg, (H + kGramMinRows - 1) / kGramMinRows));
     return strips * nseg;
   }
   const int steps = (H * W + 63) / 64;

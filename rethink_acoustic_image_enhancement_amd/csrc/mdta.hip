@@ -469,11 +469,8 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
   // column within an image row, ~0u -> zero line
   const bool dma_wave = !R::has_v(wave);
   const int drank = R::dma_rank(wave);
-#ifndef KDLAE_RING_PRIO_DMA  // A/B: issue priority of the DMA waves (>0) or of the v waves (<0); r05: DMA 1 +4%, v 1 +-1% (profiles/r05p3_ring_prio_ab.txt)
-#define KDLAE_RING_PRIO_DMA 0
-#endif
-  if (KDLAE_RING_PRIO_DMA > 0 && dma_wave) __builtin_amdgcn_s_setprio(KDLAE_RING_PRIO_DMA);
-  if (KDLAE_RING_PRIO_DMA < 0 && !dma_wave) __builtin_amdgcn_s_setprio(-KDLAE_RING_PRIO_DMA);
+  // (issue priority of either wave class: r05 A/B, DMA waves +4%, v waves +-1%: default priority,
+  // profiles/r05p3_ring_prio_ab.txt)
   unsigned colo[PPD];
 #pragma unroll
   for (int j = 0; j < PPD; ++j) {

@@ -66,7 +66,9 @@ __global__ __launch_bounds__(kThreads) void im2col3d_kernel(const float* __restr
   const int sub = KV <= kThreads ? (int)threadIdx.x / KV : 0;
   if (sub >= ppb) return;
   const int kv0 = KV <= kThreads ? (int)threadIdx.x - sub * KV : (int)threadIdx.x;
-  for (int p = blockIdx.x * ppb + sub; p < P; p += gridDim.x * ppb) {
+  // 64-bit loop index: p + the grid stride must not wrap for P close to 2^31
+  for (long long pl = (long long)blockIdx.x * ppb + sub; pl < P; pl += (long long)gridDim.x * ppb) {
+    const int p = (int)pl;
     int bf, f, y, xx;
     g.coords(p, bf, f, y, xx);
     T* dst = reinterpret_cast<T*>(col + (long long)p * 27 * C);
@@ -93,7 +95,9 @@ __global__ __launch_bounds__(kThreads) void col2im3d_kernel(const float* __restr
   const int CV = C / V;
   const int n = P * CV;  // < 2^31 (checked by the launcher)
   const long long K = 27LL * C;
-  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+  // 64-bit loop index: i + the grid stride (up to 2^28) must not wrap for n close to 2^31
+  for (long long il = (long long)blockIdx.x * kThreads + threadIdx.x; il < n; il += (long long)gridDim.x * kThreads) {
+    const int i = (int)il;
     const int q = i / CV;
     const int c = (i - q * CV) * V;
     int bf, f, y, x;

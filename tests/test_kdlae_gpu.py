@@ -78,21 +78,21 @@ def test_mdd_512_config1():
     """Config 1 (MDD sonar sample 512x512, denoise_rate 0.6), judged against the reference's fp64 output.
 
     On this input the forward is ill-conditioned: every fp32 evaluation of it is a draw from a spread
-    of errors, not a level an implementation can aim at.  The reference's own fp32 forward lands
-    3.1e-3 / 1.2e-3 / 7.5e-4 / 4.0e-3 (hq) from fp64 at torch thread counts 8 / 4 / 2 / 1 (nothing else
-    changed) and is up to 8.6e-3 away from itself (profiles/r04_config1_threads.txt); multiplying its
+    of errors.  The reference's own fp32 forward lands 3.1e-3 / 1.2e-3 / 7.5e-4 / 4.0e-3 (hq) from fp64
+    at torch thread counts 8 / 4 / 2 / 1 (nothing else changed) and the other thread counts are 1.9e-3
+    .. 8.6e-3 away from its default (8-thread) output (profiles/r04_config1_threads.txt); multiplying its
     LayerNorm outputs by (1 + u 2^-24), u ~ U[-1, 1], gives 1.0e-3 .. 2.4e-3 over 8 seeds
-    (profiles/r04_config1_ensemble.txt).  The sensitivity sits in the full- and double-resolution
-    stages (profiles/r04_config1_sensitivity.txt).  r05 changed every GEMM's rounding (split-bf16
-    products, mfma3.h: more accurate per GEMM than the f32 MFMA, tools/micro/bf16x6_probe.hip) and the
-    output moved from 1.5e-3 to 3.0e-3 of fp64 (hq) — another draw; r04's bar (the median of the 8
-    perturbed runs) holds about half of all equally accurate evaluations, the reference's own default
-    run included.  The bar, per output over every fixture sample (the [::8, ::8] subsample plus one
-    full row): ours is within the envelope of the reference's own fp32 runs (no farther from fp64 than
-    its worst thread count), its mean error within 10% of the reference fp32's, it is no farther from
-    the reference fp32 output than the reference's thread counts are from each other, and PSNR >= 60 dB
-    against the reference fp32.  The 1e-3 bar against the reference fp32 holds on every
-    well-conditioned input (all other fixtures, the 512^2 hash image included)."""
+    (profiles/r04_config1_ensemble.txt).  The bar, per output (hq, sr) over every fixture sample (the
+    [::8, ::8] subsample plus one full row), against the reference run the fixture holds (torch fp32,
+    8 threads, its default):
+      * ours is no farther from fp64 than the reference fp32 is, in max-abs and in mean-abs error;
+      * ours is no farther from the reference fp32 output than the nearest other reference thread
+        count is (1.9e-3 hq / 2.1e-3 sr);
+      * PSNR >= 60 dB against the reference fp32.
+    r06 at the benched HEAD (profiles/r06_config1_mdd.txt): hq 2.71e-3 max / 1.82e-5 mean vs the
+    reference's 3.07e-3 / 1.95e-5; sr 3.12e-3 / 1.66e-5 vs 3.40e-3 / 1.92e-5; ours-vs-ref32 1.44e-3 /
+    1.59e-3.  The 1e-3 bar against the reference fp32 holds on every well-conditioned input (all other
+    fixtures, the 512^2 hash image included)."""
     d, _ = load_fixture("t_mdd_512")
     ens = json.load(open(os.path.join(GOLDEN, "t_mdd_512_ensemble.json")))
     thr = ens["ref32_threads"]
@@ -105,13 +105,15 @@ def test_mdd_512_config1():
         e_ours, e_ref = float((ours - ref64).abs().max()), float((ref32 - ref64).abs().max())
         m_ours, m_ref = float((ours - ref64).abs().mean()), float((ref32 - ref64).abs().mean())
         e_vs32 = float((ours - ref32).abs().max())
+        nearest = min(v for v in thr[k + "_vs_8t"] if v > 0)
         print(f"t_mdd_512 {k}: ours-vs-fp64 max {e_ours:.3e} mean {m_ours:.3e}; ref32 (8 threads) max {e_ref:.3e} "
               f"mean {m_ref:.3e}; ref32 thread counts {thr['threads']}: {thr[k]}; perturbed-ref32 median "
               f"{ens[k + '_median']:.3e} (range {min(ens[k + '_max']):.3e} .. {max(ens[k + '_max']):.3e}); "
-              f"ours-vs-ref32 max {e_vs32:.3e} (ref32 thread counts vs 8 threads up to {max(thr[k + '_vs_8t']):.3e})")
-        assert e_ours <= max(thr[k]), (k, e_ours, thr[k])
-        assert m_ours <= 1.1 * m_ref, (k, m_ours, m_ref)
-        assert e_vs32 <= max(thr[k + "_vs_8t"]), (k, e_vs32)
+              f"ours-vs-ref32 max {e_vs32:.3e} (nearest other ref32 thread count {nearest:.3e}); "
+              f"PSNR vs ref32 {psnr(sub[k], torch.from_numpy(d[r32])):.1f} dB")
+        assert e_ours <= e_ref, (k, e_ours, e_ref)
+        assert m_ours <= m_ref, (k, m_ours, m_ref)
+        assert e_vs32 <= nearest, (k, e_vs32, nearest)
         assert psnr(sub[k], torch.from_numpy(d[r32])) >= 60.0
 
 

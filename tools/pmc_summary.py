@@ -8,11 +8,24 @@ usage: python tools/pmc_summary.py <fetch run_counter_collection.csv> <write csv
 """
 import collections
 import csv
+import hashlib
 import json
+import os
 import sys
 
 CLASSES = {"conv_gemm_kernel": 1, "gemm_res_kernel": 1, "gemm_chunk_kernel": 1, "gemm_attn_in_kernel": 1, "dwconv_gram": 2,
            "dwconv_gate_kernel": 3, "ffn_fused_kernel": 3, "gdfn_out_kernel": 3, "gdfn2_kernel": 3}
+
+
+def lib_sha256():
+    """sha256 of the libkdlae.so the profiled run loaded (KDLAE_LIB or the in-tree build): bench.py
+    reports the traffic as "this build's" only when its own library has the same hash."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.environ.get("KDLAE_LIB") or os.path.join(root, "rethink_acoustic_image_enhancement_amd", "libkdlae.so")
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
 
 
 def load(path, counter):
@@ -36,7 +49,7 @@ def main():
         cls[c]["fetch_bytes_corrected"] += 2.0 * b
         cls[c]["write_bytes"] += W.get(k, [0, 0.0])[1]
     res = {"note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; fetch doubled per gfx950 rule",
-           "classes": {}}
+           "lib_sha256": lib_sha256(), "classes": {}}
     for c, v in sorted(cls.items()):
         t = v["fetch_bytes_corrected"] + v["write_bytes"]
         res["classes"][str(c)] = dict(v, traffic_bytes=t,

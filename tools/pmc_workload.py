@@ -9,10 +9,23 @@ usage: python tools/pmc_workload.py <fetch csv> <write csv> <out.json> <workload
 """
 import collections
 import csv
+import hashlib
 import json
+import os
 import sys
 
 SETUP = ("pack_", "split3_kernel", "__amd_rocclr")
+
+
+def lib_sha256():
+    """sha256 of the libkdlae.so the profiled run loaded (KDLAE_LIB or the in-tree build): bench.py
+    reports the traffic as "this build's" only when its own library has the same hash."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.environ.get("KDLAE_LIB") or os.path.join(root, "rethink_acoustic_image_enhancement_amd", "libkdlae.so")
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
 
 
 def load(path, counter):
@@ -38,7 +51,7 @@ def main():
         kern[k] = {"launches_per_forward": n / fwd, "fetch_bytes_corrected": 2.0 * b / fwd, "write_bytes": w / fwd,
                    "traffic_bytes": (2.0 * b + w) / fwd}
     tot = sum(v["traffic_bytes"] for v in kern.values())
-    res = {"workload": workload, "forwards": fwd,
+    res = {"workload": workload, "forwards": fwd, "lib_sha256": lib_sha256(),
            "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py --workload "
                    f"{workload} --steps 1 --warmup 0; fetch doubled per the gfx950 rule; weight packing excluded",
            "traffic_bytes_per_forward": tot,
