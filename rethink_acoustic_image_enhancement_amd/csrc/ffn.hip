@@ -64,23 +64,6 @@ template <int C>
 constexpr bool uniform_dma() {
   return C == 48;
 }
-#ifdef KDLAE_FFN_STAMPS
-// Diagnostic build only (tools/ffn_stamps.py): per-segment cycle sums of every wave, [C48 / C96][P / G]
-// [segment]; the stamps fence the schedule, so read shares, not lengths.
-__device__ unsigned long long g_ffn_stamps[2][2][8];
-__device__ __forceinline__ unsigned long long stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define FFN_ST(v) const unsigned long long v = stamp()
-#define FFN_ADD(k, d) seg[k] += (d)
-#else
-#define FFN_ST(v)
-#define FFN_ADD(k, d)
-#endif
 
 // Tile shape and wave counts.  C = 96's LDS has room for nothing larger than its 16 x 8 tile with
 // 4 P + 4 G waves; for C = 48 r05 same-box A/B on C48@1024^2 (profiles/r05zv_ffn48_shape_ab.txt): the
@@ -168,10 +151,6 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
   const int xcd = (int)(blockIdx.x & 7), nxb = (int)(gridDim.x >> 3), xb = (int)(blockIdx.x >> 3);
   const int t_lo = (int)((long long)ntiles * xcd / 8), t_hi = (int)((long long)ntiles * (xcd + 1) / 8);
   if (t_lo + xb >= t_hi) return;  // block-uniform
-#ifdef KDLAE_FFN_STAMPS
-  unsigned long long seg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  FFN_ST(k0);
-#endif
 
   // resident: every chunk's dw block, both biases
   for (int i = tid; i < kch * kDwF4; i += NT) lds[S::kDw + i] = reinterpret_cast<const f32x4*>(p.dw)[i];
@@ -384,29 +363,32 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
       pin(0);
       lds_barrier();  // B_0
       const bool more = t + nxb < t_hi;
-      for (int g = 0; g < kch; ++g) {
-        FFN_ST(s0);
-        // W-in slot g & 1 was last read by pin(g) (before B_g): chunk g + 2 (mod kch: the next tile)
-        issue_win((g + 2) % kch);
-        FFN_ST(s1);
-        if (g + 1 < kch) pin(g + 1);
-        FFN_ST(s2);
-        if (g == kch - 1) {
-          if (more) load_x1(t + nxb);  // the next tile's rows, during this chunk and the G epilogue
-          // past B_kch pin(0) of the next tile reads W-in slot 0 (issued at chunk kch - 2): at most this
-          // chunk's W-in pieces and the x1 loads may still be outstanding
-          wait_pin_last<S>(wi);
-        } else {
-          wait_vm<0>();  // W-in of chunk g + 2 (read by pin(g + 2) in the next chunk)
-        }
-        FFN_ST(s3);
+      // unrolled by chunk pairs (kch is even) with the last pair peeled: every image / W-in slot index
+      // is a compile-time constant, and the loop carries no per-parity copies of the live state
+      for (int g = 0; g < kch - 2; g += 2) {
+        // chunk g (even): W-in slot 0 was last read by pin(g) (before B_g): chunk g + 2 into it;
+        // project_in of chunk g + 1 into image slot 1
+        issue_win(g + 2);
+        pin(g + 1);
+        wait_vm<0>();   // W-in of chunk g + 2 (read by pin(g + 2) in the next chunk)
         lds_barrier();  // B_{g+1}
-        FFN_ST(s4);
-        FFN_ADD(0, s1 - s0);
-        FFN_ADD(1, s2 - s1);
-        FFN_ADD(2, s3 - s2);
-        FFN_ADD(3, s4 - s3);
+        // chunk g + 1 (odd): chunk g + 3 into W-in slot 1; project_in of chunk g + 2 into image slot 0
+        issue_win(g + 3);
+        pin(g + 2);
+        wait_vm<0>();
+        lds_barrier();  // B_{g+2}
       }
+      // the last pair: the next tile's chunks 0 and 1 into the W-in slots
+      issue_win(0);
+      pin(kch - 1);
+      wait_vm<0>();
+      lds_barrier();  // B_{kch-1}
+      issue_win(1);
+      if (more) load_x1(t + nxb);  // the next tile's rows, during this chunk and the G epilogue
+      // past B_kch pin(0) of the next tile reads W-in slot 0 (issued at chunk kch - 2): at most this
+      // chunk's W-in pieces and the x1 loads may still be outstanding
+      wait_pin_last<S>(wi);
+      lds_barrier();  // B_kch
     }
   } else {
     int pc = 0;  // pairs consumed by this block (W slot = pc & 1)
@@ -435,38 +417,27 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
       };
       f32x4 gbp[kRPW];
       lds_barrier();  // B_0: chunk 0's image
-      for (int g = 0; g < kch; ++g) {
-        const f32x4* sl = lds + (g & 1) * kImg;
-        FFN_ST(s0);
-        // chunk 2j (even): the W of pair j + 1 (or of the next tile's pair 0) into the other W slot;
-        // its last reader, pair j - 1, finished before this chunk's barrier
-        if ((g & 1) == 0) issue_w((g >> 1) + 1 < npairs ? (g >> 1) + 1 : 0, (pc + 1) & 1);
-        FFN_ST(s1);
+      // unrolled by chunk pairs (kch is even): chunk g reads image slot 0, chunk g + 1 slot 1, and the
+      // accumulators stay in one register set (a parity branch made hipcc copy them every chunk)
+      for (int g = 0; g < kch; g += 2) {
+        // chunk g: the W of pair g / 2 + 1 (or of the next tile's pair 0) into the other W slot; its
+        // last reader, pair g / 2 - 1, finished before this chunk's barrier
+        issue_w((g >> 1) + 1 < npairs ? (g >> 1) + 1 : 0, (pc + 1) & 1);
+        gate_rows<kRPW, kGeluPacked>(lds, lds + S::kDw + g * kDwF4, lo, lq, gbp);
+        // chunk g + 1 consumes pair g / 2: its W DMA must have landed.  Issued after it by this wave:
+        // this chunk's W issue (pw pieces) and, at a tile's first pair, the previous tile's output
+        // stores (the previous pair 0 landed in the prologue or before the previous tile's epilogue
+        // read its residual)
+        if (g == 0)
+          wait_w(std::integral_constant<int, kRPW * NTO>{});
+        else
+          wait_w(std::integral_constant<int, 0>{});
+        lds_barrier();  // B_{g+1}: chunk g + 1's image
         f32x4 gn[kRPW];
-        gate_rows<kRPW, kGeluPacked>(sl, lds + S::kDw + g * kDwF4, lo, lq, gn);
-        FFN_ST(s2);
-        if (g & 1) {
-          mfma_pair(gbp, gn, pc & 1);  // chunks g - 1, g
-          ++pc;
-        } else {
-#pragma unroll
-          for (int r = 0; r < kRPW; ++r) gbp[r] = gn[r];
-          // the next (odd) chunk consumes pair g / 2: its W DMA must have landed.  Issued after it by
-          // this wave: this chunk's W issue (pw pieces) and, at a tile's first pair, the previous
-          // tile's output stores (the previous pair 0 landed in the prologue or before the previous
-          // tile's epilogue read its residual)
-          if (g == 0)
-            wait_w(std::integral_constant<int, kRPW * NTO>{});
-          else
-            wait_w(std::integral_constant<int, 0>{});
-        }
-        FFN_ST(s3);
-        lds_barrier();  // B_{g+1}: the next chunk's image
-        FFN_ST(s4);
-        FFN_ADD(0, s1 - s0);
-        FFN_ADD(1, s2 - s1);
-        FFN_ADD((g & 1) ? 2 : 5, s3 - s2);
-        FFN_ADD(3, s4 - s3);
+        gate_rows<kRPW, kGeluPacked>(lds + kImg, lds + S::kDw + (g + 1) * kDwF4, lo, lq, gn);
+        mfma_pair(gbp, gn, pc & 1);  // chunks g, g + 1
+        ++pc;
+        lds_barrier();  // B_{g+2}: chunk g + 2's image
       }
       // epilogue: y = acc + x1 + bias (gdfn_out's order); rows / columns past the image dropped
       const int xo = x0 + li;
@@ -496,32 +467,8 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) W DMA lands before exit
-#ifdef KDLAE_FFN_STAMPS
-  FFN_ST(k1);
-  seg[7] = k1 - k0;
-  seg[6] = seg[7] - seg[0] - seg[1] - seg[2] - seg[3] - seg[5];  // tile prologue / epilogue, rest
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      unsigned long long v = seg[k];
-      v = (unsigned)__builtin_amdgcn_readfirstlane((int)v) |
-          ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32);
-      atomicAdd(&g_ffn_stamps[C == 96][gw ? 1 : 0][k], v);
-    }
-  }
-#endif
 }
 
-#ifdef KDLAE_FFN_STAMPS
-extern "C" int kdlae_debug_ffn_stamps(unsigned long long* out, int reset) {
-  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ffn_stamps), sizeof(g_ffn_stamps)) != hipSuccess) return -1;
-  if (reset) {
-    static const unsigned long long zero[2][2][8] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ffn_stamps), zero, sizeof(zero)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif
 
 // an even chunk count (the released config: hidS = 128 / 256), so every pair is full
 bool ffn_fused_supported(int C, int hidS) {
