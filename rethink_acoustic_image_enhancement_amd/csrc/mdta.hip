@@ -14,6 +14,7 @@
 //      written directly in the packed GEMM fragment order, so "A v then project_out" is ONE GEMM
 //      (conv_gemm with per-image weights M and the residual add in its epilogue).
 #include <type_traits>
+#include <utility>
 
 #include "kernels.h"
 #include "mfma3.h"
@@ -378,6 +379,12 @@ __global__ __launch_bounds__(64 * gram_waves(CT)) void dwconv_gram_sweep_kernel(
 //    instantiated per class, so neither carries the other's branches;
 //  * Gram MFMA k-step s takes pixel 4 s + (lane >> 4), so the q/k operand reads are
 //    bank-conflict-free (S = Ch padded to 16 mod 32).
+// f(std::integral_constant<int, J>) for J = 0 .. N-1 (compile-time job slots)
+template <int... J, class F>
+__device__ __forceinline__ void for_each_int(std::integer_sequence<int, J...>, F&& f) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+
 template <int CT>
 struct GramRing {
   static constexpr int Ch = CT * 16;
@@ -412,6 +419,26 @@ struct GramRing {
   }
   static constexpr int NDW = dma_waves();
   static constexpr int PPD = (Pieces + NDW - 1) / NDW;  // pieces per DMA wave per row
+  // what stencil job slot j is for every wave of a class (D: the DMA waves, !D: the v waves), so the
+  // row loop carries no per-job branches: 0 no wave of the class has the slot, 1 q or k (-> LDS
+  // staging) for every wave that has it, 2 v (-> HBM) for every wave that has it, 3 mixed
+  static constexpr int job_kind(bool D, int j) {
+    bool any = false, lds = false, v = false;
+    for (int w = 0; w < NW; ++w) {
+      if (has_v(w) == D) continue;
+      const int jb = w + NW * j;
+      if (jb >= NJ) continue;
+      any = true;
+      (jb / CT == 2 ? v : lds) = true;
+    }
+    return !any ? 0 : (lds && v) ? 3 : lds ? 1 : 2;
+  }
+  // every wave of the class has job slot j
+  static constexpr bool job_all(bool D, int j) {
+    for (int w = 0; w < NW; ++w)
+      if (has_v(w) != D && w + NW * j >= NJ) return false;
+    return true;
+  }
 };
 
 #ifndef KDLAE_RING_XCD
@@ -524,6 +551,7 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
       const float* rp = ringf + ((r + 1) % R::NSlot) * R::RowF4 * 4 + 4 * lq * PS + li;
 #pragma unroll
       for (int j = 0; j < JPW; ++j) {
+        if (R::job_kind(D, j) == 0) continue;  // no wave of this class has job slot j
         const int co = part[j] * Ch + ctj[j] * 16;
 #pragma unroll
         for (int c6 = 0; c6 < 6; ++c6) {
@@ -534,24 +562,36 @@ __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_ker
       }
     };
     auto stencil = [&](int r, int sb, int s) {
+      const int lp = 4 * lq + s;
+      auto one = [&](auto jtag) {
+        constexpr int j = decltype(jtag)::value;
+        constexpr int K = R::job_kind(D, j);
+        if constexpr (K != 0) {
+          if (R::job_all(D, j) || wave + NW * j < NJ) {
+            float a = bias[j];
 #pragma unroll
-      for (int j = 0; j < JPW; ++j) {
-        if (NJ % NW == 0 || wave + NW * j < NJ) {
-          float a = bias[j];
+            for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
-          for (int rr = 0; rr < 3; ++rr)
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx) a = fmaf(win[j][rr][s + dx], w[j][3 * rr + dx], a);
-          const int lp = 4 * lq + s;
-          if (D || part[j] < 2) {
-            float* dst = part[j] == 0 ? qs : ks;
-            dst[sb * 16 * S + lp * S + ctj[j] * 16 + li] = a;
-            n2[j] = fmaf(a, a, n2[j]);
-          } else {
-            V[(r * p.W + xs + lp) * p.ldv + h * Ch + ctj[j] * 16 + li] = a;
+              for (int dx = 0; dx < 3; ++dx) a = fmaf(win[j][rr][s + dx], w[j][3 * rr + dx], a);
+            auto to_lds = [&]() {
+              float* dst = part[j] == 0 ? qs : ks;
+              dst[sb * 16 * S + lp * S + ctj[j] * 16 + li] = a;
+              n2[j] = fmaf(a, a, n2[j]);
+            };
+            auto to_v = [&]() { V[(r * p.W + xs + lp) * p.ldv + h * Ch + ctj[j] * 16 + li] = a; };
+            if constexpr (K == 1) {
+              to_lds();
+            } else if constexpr (K == 2) {
+              to_v();
+            } else if (part[j] < 2) {
+              to_lds();
+            } else {
+              to_v();
+            }
           }
         }
-      }
+      };
+      for_each_int(std::make_integer_sequence<int, JPW>{}, one);
     };
 
     // prologue: rows y0-1 .. min(y0+4, y1) in flight; stencil(y0) once rows y0-1..y0+1 landed
