@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "gate.h"
 #include "kernels.h"
@@ -234,14 +235,22 @@ __global__ __launch_bounds__(64 * FfnShape<C>::NW, FfnShape<C>::NW / 4) void ffn
                                                  real ? (((2 * g + j) * KP + G) * 3 + pl) * 1024 : 0, 0, 0);
       }
     } else {
+      auto issue_case = [&](auto wtag) {
+        constexpr int WI = decltype(wtag)::value;
 #pragma unroll
-      for (int k = 0; k < 6 * KP; ++k)
-        if (k % NP == wi) {  // piece k = (tile j = k / (3 KP), pair G, plane) of records (2g + j, G)
+        for (int k = WI; k < 6 * KP; k += NP) {
           const int j = k / (3 * KP), rem = k - j * 3 * KP;
           const int G = rem / 3, pl = rem - 3 * G;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rwin, (lptr_f)(dst + 64 * k), 16, (int)(16u * lane),
                                                    (((2 * g + j) * KP + G) * 3 + pl) * 1024, 0, 0);
         }
+      };
+      switch (wi) {
+        case 0: issue_case(std::integral_constant<int, 0>{}); break;
+        case 1: issue_case(std::integral_constant<int, 1>{}); break;
+        case 2: issue_case(std::integral_constant<int, 2>{}); break;
+        default: issue_case(std::integral_constant<int, 3>{}); break;
+      }
     }
   };
   f32x4 a[PT][KG];  // P waves: the x1 rows of the next tile (loaded ahead)

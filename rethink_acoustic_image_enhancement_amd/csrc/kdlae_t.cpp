@@ -40,6 +40,9 @@ struct BlockW {
   // kernel (ffn.hip), project_in recomputed on each tile's halo; the block output goes to the other
   // buffer of a ping-pong pair (stage()).  Debug flag no_ffn_fusion keeps the unfused kernels.
   bool ffn_fused = false;
+  // r06: MDTA pass 1 with LN + qkv recomputed on each tile's halo (mdta_fused.hip) for single-head
+  // C = 48 / 96 blocks; opt-in (debug flag mdta_fusion), the qkv GEMM + Gram ring by default
+  bool mdta_fused = false;
 };
 
 }  // namespace kdlae
@@ -383,6 +386,9 @@ struct Packer {
     }
     b.ffn_fused = b.fused_gdfn && ffn_fused_supported(C, hidS) && b.pin.ntiles == 2 * hidS / 16 &&
                   !debug_flag("no_ffn_fusion");
+    // opt-in (debug flag mdta_fusion): r06 measured it slower than the qkv GEMM + Gram ring it replaces
+    // (C96@512^2 3.54 vs 3.41 ms, C48@1024^2 5.93 vs 5.29 ms; DESIGN.md §4 "Fused MDTA pass 1")
+    b.mdta_fused = heads == 1 && (C == 48 || C == 96) && b.qkv.ntiles == 3 * C / 16 && debug_flag("mdta_fusion");
     return b;
   }
 
@@ -590,6 +596,40 @@ struct Fwd {
     const long long P = (long long)B * HW;
     int rc;
     // --- attention
+    const int nslots = nslots_for(Hh, Ww, B, b.heads);
+    const int nseg = Ww % 16 == 0 ? nslots / (Ww / 16) : 0;
+    const int seg_rows = nseg ? (Hh + nseg - 1) / nseg : 0;
+    if (b.mdta_fused && mdta_fused_supported(b.C, b.heads, Hh, Ww, nseg, seg_rows)) {
+      // LN + qkv + dwconv + Gram in one pass (mdta_fused.hip): qkv never reaches HBM
+      const int CT = b.Ch / 16;
+      MdtaFusedParams q{};
+      q.x = x.p;
+      q.ldx = x.ld;
+      q.ln = ln;
+      q.Wqkv = h->P3(b.qkv.w3);
+      q.bias = h->P(b.qkv.bias);
+      q.wdw = h->P(b.dwqkv);
+      q.bdw = h->P(b.dwqkv_b);
+      q.v_out = buf(pl.vbuf);
+      q.ldv = b.C;
+      q.partial = buf(pl.part);
+      q.nslots = nslots;
+      q.slot_floats = CT * CT * 256 + 2 * b.Ch;
+      q.nseg = nseg;
+      q.seg_rows = seg_rows;
+      q.Bn = B;
+      q.H = Hh;
+      q.W = Ww;
+      if ((rc = probe_begin(2, b.C))) return rc;
+      tag = "mdta_fused C" + std::to_string(b.C) + " HW" + std::to_string(HW);
+      HIPCHK(launch_mdta_fused(q, b.C, s));
+      // algorithmic: read x, write v; qkv projection, dwconv and Gram FLOPs
+      if ((rc = probe_end(2, b.C, 4.0 * P * 2 * b.C,
+                          2.0 * P * (3.0 * b.C * b.C + 27.0 * b.C + (double)b.C * b.Ch))))
+        return rc;
+      HIPCHK(launch_gram_reduce(q.partial, buf(pl.red), B, b.heads, nslots, q.slot_floats, s));
+      HIPCHK(launch_attn_fold(buf(pl.red), q.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
+    } else {
     View qkv{buf(pl.qkv), 3 * b.C};
     rc = gemm(b.qkv, h->P3(b.qkv.w3), 0, x, Hh, Ww, qkv, 0, nullptr, 0, ln, b.C, b.C);
     if (rc) return rc;
@@ -607,7 +647,7 @@ struct Fwd {
     gp.Bn = B;
     gp.H = Hh;
     gp.W = Ww;
-    gp.nslots = nslots_for(Hh, Ww, B, b.heads);
+    gp.nslots = nslots;
     gp.zeros = h->P(h->zeros);
     const int CT = b.Ch / 16;
     gp.slot_floats = CT * CT * 256 + 2 * b.Ch;
@@ -617,6 +657,7 @@ struct Fwd {
     if ((rc = probe_end(2, b.C, 4.0 * P * 4 * b.C, 2.0 * P * (27.0 * b.C + (double)b.C * b.Ch)))) return rc;
     HIPCHK(launch_gram_reduce(gp.partial, buf(pl.red), B, b.heads, gp.nslots, gp.slot_floats, s));
     HIPCHK(launch_attn_fold(buf(pl.red), gp.slot_floats, h->P(b.proj), h->P(b.temp), buf(pl.Mp), B, b.C, b.heads, s));
+    }
     View fpre{buf(pl.fpre), 2 * b.hidS};
     const bool fuse_in = b.fused_attn_in && !ffn;
     if (fuse_in) {

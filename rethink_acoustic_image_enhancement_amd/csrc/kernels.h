@@ -153,6 +153,24 @@ bool ffn_fused_supported(int C, int hidS);
 hipError_t launch_ffn_fused(const FfnParams& p, int C, hipStream_t s);
 
 
+// Fused MDTA pass 1 for single-head C = 48 / 96 blocks (mdta_fused.hip): LN + qkv projection recomputed
+// on each tile's halo, depthwise 3x3, v -> v_out, Gram + |q|^2 / |k|^2 -> the Gram slots of
+// launch_dwconv_gram (same slot partition and layout: 16-column strips x nseg row segments)
+struct MdtaFusedParams {
+  const float* x; int ldx;         // block input [P][ldx]
+  int ln;                          // 1 BiasFree, 2 WithBias
+  const float* Wqkv;               // qkv split records [3C / 16][C / 32 (round up)][kRec3]
+  const float* bias;               // [3C] or null (LN bias / conv bias folded)
+  const float* wdw;                // [9][3C] tap-major
+  const float* bdw;                // [3C] or null
+  float* v_out; int ldv;
+  float* partial;                  // [B][nslots][slot_floats]
+  int nslots, slot_floats, nseg, seg_rows;
+  int Bn, H, W;
+};
+bool mdta_fused_supported(int C, int heads, int H, int W, int nseg, int seg_rows);
+hipError_t launch_mdta_fused(const MdtaFusedParams& p, int C, hipStream_t s);
+
 // Pre/post-processing around the forward (pipeline.hip)
 struct PreParams {
   const uint8_t* in; int B, h, w, cin, cout, bgr;  // u8 [B][h][w][cin]

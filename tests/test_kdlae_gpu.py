@@ -86,13 +86,14 @@ def test_mdd_512_config1():
     [::8, ::8] subsample plus one full row), against the reference run the fixture holds (torch fp32,
     8 threads, its default):
       * ours is no farther from fp64 than the reference fp32 is, in max-abs and in mean-abs error;
-      * ours is no farther from the reference fp32 output than the nearest other reference thread
-        count is (1.9e-3 hq / 2.1e-3 sr);
       * PSNR >= 60 dB against the reference fp32.
-    r06 at the benched HEAD (profiles/r06_config1_mdd.txt): hq 2.71e-3 max / 1.82e-5 mean vs the
-    reference's 3.07e-3 / 1.95e-5; sr 3.12e-3 / 1.66e-5 vs 3.40e-3 / 1.92e-5; ours-vs-ref32 1.44e-3 /
-    1.59e-3.  The 1e-3 bar against the reference fp32 holds on every well-conditioned input (all other
-    fixtures, the 512^2 hash image included)."""
+    No bar is put on ours-vs-ref32 beyond the PSNR: a more accurate evaluation sits about as far from
+    the reference fp32 output as that output is from fp64 (r06: one build of the opt-in fused MDTA
+    kernel landed 4.7e-4 from fp64, 6.5x closer than the reference's own fp32 run, and 3.0e-3 from
+    it).  r06 at the benched HEAD (profiles/r06_config1_mdd.txt): hq 2.71e-3 max / 1.82e-5 mean vs the
+    reference's 3.07e-3 / 1.95e-5; sr 3.12e-3 / 1.66e-5 vs 3.40e-3 / 1.92e-5.  The 1e-3 bar against
+    the reference fp32 holds on every well-conditioned input (all other fixtures, the 512^2 hash image
+    included)."""
     d, _ = load_fixture("t_mdd_512")
     ens = json.load(open(os.path.join(GOLDEN, "t_mdd_512_ensemble.json")))
     thr = ens["ref32_threads"]
@@ -105,15 +106,13 @@ def test_mdd_512_config1():
         e_ours, e_ref = float((ours - ref64).abs().max()), float((ref32 - ref64).abs().max())
         m_ours, m_ref = float((ours - ref64).abs().mean()), float((ref32 - ref64).abs().mean())
         e_vs32 = float((ours - ref32).abs().max())
-        nearest = min(v for v in thr[k + "_vs_8t"] if v > 0)
         print(f"t_mdd_512 {k}: ours-vs-fp64 max {e_ours:.3e} mean {m_ours:.3e}; ref32 (8 threads) max {e_ref:.3e} "
               f"mean {m_ref:.3e}; ref32 thread counts {thr['threads']}: {thr[k]}; perturbed-ref32 median "
               f"{ens[k + '_median']:.3e} (range {min(ens[k + '_max']):.3e} .. {max(ens[k + '_max']):.3e}); "
-              f"ours-vs-ref32 max {e_vs32:.3e} (nearest other ref32 thread count {nearest:.3e}); "
+              f"ours-vs-ref32 max {e_vs32:.3e} (other ref32 thread counts vs 8 threads {thr[k + '_vs_8t'][1:]}); "
               f"PSNR vs ref32 {psnr(sub[k], torch.from_numpy(d[r32])):.1f} dB")
         assert e_ours <= e_ref, (k, e_ours, e_ref)
         assert m_ours <= m_ref, (k, m_ours, m_ref)
-        assert e_vs32 <= nearest, (k, e_vs32, nearest)
         assert psnr(sub[k], torch.from_numpy(d[r32])) >= 60.0
 
 
@@ -194,6 +193,27 @@ def test_fused_ffn_equals_unfused_bit_for_bit(ln, bias, shape, monkeypatch):
     monkeypatch.setenv("KDLAE_DEBUG", "no_ffn_fusion")  # read when a new handle builds its blocks
     unfused = _run(_model(kw), img, rate)
     assert torch.equal(fused["hq"], unfused["hq"]) and torch.equal(fused["sr"], unfused["sr"])
+
+
+@pytest.mark.parametrize("ln,bias,shape", [
+    ("BiasFree", False, (2, 3, 64, 48)),    # whole 16 x 8 tiles, 2 images per launch
+    ("WithBias", True, (1, 3, 72, 32)),     # WithBias LN + conv biases; 3 row segments of 24
+])
+def test_fused_mdta_matches_unfused(ln, bias, shape, monkeypatch):
+    """mdta_fused_kernel (mdta_fused.hip, opt-in KDLAE_DEBUG=mdta_fusion: LN + qkv recomputed on each
+    tile's halo, dwconv, Gram into the same slots) against the default qkv GEMM + Gram ring for the
+    single-head C = 48 / 96 stages.  The Gram products run on split-bf16 MFMAs instead of the ring's
+    f32 MFMA chain, so the two agree to fp32 rounding (1e-5 here), not bit for bit; both are held to
+    the oracle at 1e-3 by the golden tests."""
+    kw = dict(dim=48, LayerNorm_type=ln, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, bias=bias)
+    img = torch.from_numpy(hash_images("mdf", shape))
+    rate = torch.from_numpy(hash_images("mdfr", (shape[0], 1) + shape[2:]))
+    unfused = _run(_model(kw), img, rate)
+    monkeypatch.setenv("KDLAE_DEBUG", "mdta_fusion")  # read when a new handle builds its blocks
+    fused = _run(_model(kw), img, rate)
+    e_hq, e_sr = max_abs(fused["hq"], unfused["hq"]), max_abs(fused["sr"], unfused["sr"])
+    print(f"fused vs unfused MDTA: hq {e_hq:.3e} sr {e_sr:.3e}")
+    assert e_hq <= 1e-5 and e_sr <= 1e-5, (e_hq, e_sr)
 
 
 def test_weight_reload_is_picked_up():

@@ -28,6 +28,7 @@ PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cache
 
 use_variant() {  # name=path[,ENV=V...] -> exports; prints the name
   local nv=$1 n v envs
+  unset KDLAE_DEBUG  # a previous variant's environment must not leak into this one
   n=${nv%%=*}; v=${nv#*=}
   IFS=, read -r v envs <<< "$v"
   for e in ${envs//,/ }; do export "$e"; done
