@@ -57,7 +57,7 @@ bench)
   ;;
 prof)
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-bs1 --no-secondary > $O/prof_bench.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-bs1 --no-secondary --no-train > $O/prof_bench.log 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run -- python3 $R/bench.py --workload train --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_train.log 2>&1 || exit $?
   ;;
 profb)  # rocprofv3 kernel trace + stats of one bench.py invocation (args)
@@ -84,10 +84,14 @@ pmc_sec)  # FETCH_SIZE / WRITE_SIZE passes over one S8 and one A64 forward -> pr
   ;;
 pmc)
   cd /tmp && export TMPDIR=/tmp
-  B="python3 $R/bench.py --steps 1 --warmup 0 --probe 0 --no-cpu-baseline --no-bs1 --no-secondary"
+  B="python3 $R/bench.py --steps 1 --warmup 0 --probe 0 --no-cpu-baseline --no-bs1 --no-secondary --no-train"
   timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- $B > $O/pmc_fetch.log 2>&1 || exit $?
   timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- $B > $O/pmc_write.log 2>&1 || exit $?
   timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_busy -o run -- $B > $O/pmc_busy.log 2>&1 || exit $?
+  # per-class traffic of this build (lib_sha256 recorded), warm-up forward included: 2 forwards
+  python3 $R/tools/pmc_summary.py $(ls $O/pmc_fetch/*counter_collection.csv | head -1) \
+    $(ls $O/pmc_write/*counter_collection.csv | head -1) $O/pmc_traffic.json > $O/pmc_traffic.log 2>&1 || exit $?
+  python3 $R/tools/pmc_busy.py $(ls $O/pmc_busy/*counter_collection.csv | head -1) $O/pmc_busy.json r06 > $O/pmc_busy_sum.log 2>&1 || exit $?
   ;;
 pmc_lds)  # one T16 step: wave-state and LDS counters per kernel (one pass)
   cd /tmp && export TMPDIR=/tmp
