@@ -95,7 +95,7 @@ pmc)
   ;;
 pmc_lds)  # one T16 step: wave-state and LDS counters per kernel (one pass)
   cd /tmp && export TMPDIR=/tmp
-  B="python3 $R/bench.py --steps 1 --warmup 0 --probe 0 --no-cpu-baseline --no-bs1 --no-secondary"
+  B="python3 $R/bench.py --steps 1 --warmup 0 --probe 0 --no-cpu-baseline --no-bs1 --no-secondary --no-train"
   timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --output-format csv -d $O/pmc_lds -o run -- $B > $O/pmc_lds.log 2>&1 || exit $?
   ;;
 split)  # two half-batches on two streams vs one stream (tools/stream_split_probe.py)
