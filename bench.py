@@ -44,6 +44,7 @@ from rethink_acoustic_image_enhancement_amd import _lib  # noqa: E402
 from rethink_acoustic_image_enhancement_amd.hashweights import hash_images, hash_uniform, load_hash_weights  # noqa: E402
 from rethink_acoustic_image_enhancement_amd.KDLAE_model import KDLAE_student, KDLAE_teacher  # noqa: E402
 from rethink_acoustic_image_enhancement_amd.ASDQE_model import DenoiseRatePredictor  # noqa: E402
+from rethink_acoustic_image_enhancement_amd.shard import OverlappedGather  # noqa: E402
 
 METRIC = "images/sec KDLAE-T 1×512×512 fp32 at 1/2/4/8 MI355X; PSNR vs ref"
 KW = dict(inp_channels=3, out_channels=3, dim=48, num_blocks=[4, 6, 6, 8], num_refinement_blocks=4,
@@ -130,8 +131,10 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
-def timed_steps(step, steps: int, distributed: bool, dev):
+def timed_steps(step, steps: int, distributed: bool, dev, drain=None):
     """Exactly `steps` calls of `step` bracketed by a barrier + device sync on both sides.
+    `drain` (OverlappedGather.drain) runs inside the timed window, before the closing sync: every
+    step's output gather is complete when the clock stops.
     Returns (max-over-ranks seconds, this rank's seconds, last output)."""
     _sync(dev)
     if distributed:
@@ -141,6 +144,8 @@ def timed_steps(step, steps: int, distributed: bool, dev):
     out = None
     for _ in range(steps):
         out = step()
+    if drain is not None:
+        drain()
     _sync(dev)
     local = time.perf_counter() - t0
     elapsed = local
@@ -174,21 +179,22 @@ def bench_standin(args, world, rank):
     """CPU rehearsal of the N-rank path (gloo, no GPU): the T16 sharding, timing and gather with a
     per-image stand-in for the forward.  Each rank sleeps rank-dependent time per step so the
     max-over-ranks timing is observable.  Used by tests/test_bench_launch.py."""
-    from rethink_acoustic_image_enhancement_amd.shard import gather_outputs
-
     dev = torch.device("cpu")
     B, H = args.batch or 16, args.size or 16
     img, rate = make_inputs(rank * B, B, H, H)
     delay = 0.01 * rank
+    gather = OverlappedGather() if world > 1 else None
 
     def step():
         hq = img * 2 + rate
         time.sleep(delay)
-        return gather_outputs(hq) if world > 1 else hq
+        return gather({"hq": hq})["hq"] if gather else hq
 
     for _ in range(args.warmup):
         step()
-    elapsed, local, full = timed_steps(step, args.steps, world > 1, dev)
+    if gather:
+        gather.drain()
+    elapsed, local, full = timed_steps(step, args.steps, world > 1, dev, drain=gather.drain if gather else None)
     info = [{"rank": rank, "first": rank * B, "last": rank * B + B - 1, "local_s": local}]
     if world > 1:
         info = [None] * world
@@ -594,16 +600,15 @@ def main():
     img, rate = make_inputs(rank * B, B, H, W)
     batch = {"img": img.to(dev), "denoise_rate": rate.to(dev)}
 
-    gather = distributed and not args.no_gather
-    if gather:
-        from rethink_acoustic_image_enhancement_amd.shard import gather_outputs
+    # the scaling metric runs to the end of the output all-gather.  Step i's gather
+    # runs on RCCL's stream beside step i + 1's forward (the module returns fresh output tensors,
+    # never the graph's buffers); timed_steps drains the last ones inside the timed window.
+    gather = OverlappedGather() if distributed and not args.no_gather else None
 
     def step():
         with torch.no_grad():
             out = model(batch)
-            if gather:  # the scaling metric runs to the end of the output all-gather
-                out = {k: gather_outputs(v) if v is not None else None for k, v in out.items()}
-            return out
+            return gather(out) if gather else out
 
     eng = model.engine(dev)
     L = _lib.lib()
@@ -612,11 +617,14 @@ def main():
     # captures).  The roofline comes from a separate probe pass AFTER the timed steps: the probe
     # brackets each launch of one kernel class with HIP events, so that pass runs launch by launch.
     model.hip_graphs = True
+    drain = gather.drain if gather else None
     for _ in range(max(args.warmup, 2)):
         step()
+    if drain:
+        drain()
     torch.cuda.synchronize(dev)
 
-    elapsed, _, out = timed_steps(step, args.steps, distributed, dev)
+    elapsed, _, out = timed_steps(step, args.steps, distributed, dev, drain=drain)
     if gather:  # this rank's own images of the gathered batch (for the parity leg)
         out = {k: (v[rank * B:(rank + 1) * B] if v is not None else None) for k, v in out.items()}
 
@@ -628,9 +636,11 @@ def main():
         model.hip_graphs = False
         L.kdlae_t_probe_arm(eng.handle, cls, args.probe_level)
         step()  # untimed: creates the probe's event pool outside the measured window
+        if drain:
+            drain()
         torch.cuda.synchronize(dev)
         L.kdlae_t_probe_arm(eng.handle, cls, args.probe_level)
-        p_elapsed, _, _ = timed_steps(step, probe_steps, distributed, dev)
+        p_elapsed, _, _ = timed_steps(step, probe_steps, distributed, dev, drain=drain)
         model.hip_graphs = True
         ms, n, by, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
         dump = os.environ.get("KDLAE_PROBE_DUMP")
@@ -741,7 +751,8 @@ def main():
                    "global_batch": world * B, "per_gpu_batch": B, "H": H, "W": W,
                    "timed_path": "the module's default forward (HIP-graph replay of the repeated shape), "
                                  "no probe armed",
-                   "parallelism": f"dp{world} (batch-sharded" + (", RCCL all-gather of hq/sr in every step)"
+                   "parallelism": f"dp{world} (batch-sharded" + (", RCCL all-gather of hq/sr in every step, "
+                                                                 "overlapped with the next step's forward)"
                                                                 if gather else ", no data-path collective)")},
         "roofline": roof,
     }

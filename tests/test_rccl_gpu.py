@@ -57,6 +57,32 @@ def test_rccl_output_gather_of_the_hip_module(rccl_world1):
     assert g.is_cuda and torch.equal(g, ref["sr"])
 
 
+def test_rccl_overlapped_gather_of_the_hip_module(rccl_world1):
+    """bench.py's N > 1 step on RCCL: each forward's hq / sr gather enqueued asynchronously on the
+    collective stream while the next forward (HIP-graph replay) runs; after drain() every step's
+    gathered output equals that step's local output bit for bit (world 1: the identity)."""
+    from rethink_acoustic_image_enhancement_amd.shard import OverlappedGather
+    kw = dict(dim=48, num_blocks=[1, 1, 1, 1], num_refinement_blocks=1, LayerNorm_type="BiasFree")
+    m = KDLAE_teacher(**kw)
+    load_hash_weights(m)
+    m = m.to(DEV).eval()
+    m.hip_graphs = True
+    g = OverlappedGather(depth=2)
+    outs, refs = [], []
+    with torch.no_grad():
+        for step in range(4):
+            img = torch.from_numpy(hash_images(f"ovl{step}", (2, 3, 32, 48))).to(DEV)
+            rate = torch.full((2, 1, 32, 48), 0.3 + 0.1 * step, device=DEV)
+            o = m({"img": img, "denoise_rate": rate})
+            refs.append({k: v.clone() for k, v in o.items()})
+            outs.append(g(o))
+            assert len(g.inflight) <= 2
+        g.drain()
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert torch.equal(o["hq"], r["hq"]) and torch.equal(o["sr"], r["sr"])
+
+
 def test_rccl_bucketed_allreduce_behind_gradient_events(rccl_world1):
     from rethink_acoustic_image_enhancement_amd.train import KDLAETrainer, allreduce_buckets_rccl
     m = KDLAE_teacher(LayerNorm_type="BiasFree")

@@ -113,3 +113,52 @@ def test_sharded_asdqe_scores_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert all(res[r] for r in range(world)), res
+
+
+def _overlap_worker(rank, world, port, q):
+    """bench.py's overlapped output gather: 5 steps with step-dependent outputs and a rank-dependent
+    delay (uneven arrival), at most two steps in flight; after drain() every step's gathered
+    tensor must equal the rank-ordered concatenation of that step's shards."""
+    import time
+
+    from rethink_acoustic_image_enhancement_amd.shard import OverlappedGather, gather_outputs_async
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B = 3
+
+    def shard(step, r):
+        base = torch.arange(B * 4, dtype=torch.float32).view(B, 1, 2, 2)
+        return base + 100.0 * r + 1000.0 * step
+
+    g = OverlappedGather(depth=2)
+    outs = []
+    for step in range(5):
+        time.sleep(0.005 * ((rank + step) % world))
+        outs.append(g({"hq": shard(step, rank), "sr": None}))
+        assert len(g.inflight) <= 2
+    g.drain()
+    ok = not g.inflight
+    for step, o in enumerate(outs):
+        want = torch.cat([shard(step, r) for r in range(world)])
+        ok = ok and o["sr"] is None and torch.equal(o["hq"], want)
+    full, work = gather_outputs_async(shard(7, rank))
+    if work is not None:
+        work.wait()
+    ok = ok and torch.equal(full, torch.cat([shard(7, r) for r in range(world)]))
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_overlapped_gather_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r] for r in range(world)), res
