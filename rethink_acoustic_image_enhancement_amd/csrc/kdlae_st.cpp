@@ -470,6 +470,11 @@ int kdlae_st_create(const kdlae_s_config* cfg, int device, kdlae_st_handle** out
       delete h;
       return fail(KDLAE_EINVAL_CONFIG, "bad hidden_channels");
     }
+    if (cfg->hidden_channels[i] % 4) {  // the step's pool / gather kernels move float4 channel groups
+      delete h;
+      return fail(KDLAE_EINVAL_CONFIG,
+                  "KDLAE_student training on the HIP path needs hidden_channels divisible by 4 (inference takes any)");
+    }
     h->hc.push_back(cfg->hidden_channels[i]);
   }
   auto add = [&](const std::string& k, int64_t n) {

@@ -309,12 +309,11 @@ hipError_t launch_col2im3d(const float* dcol, int C, int B, int F, int H, int W,
   const long long P = (long long)B * F * H * W;
   if (P * C >= (1LL << 31)) return hipErrorInvalidValue;
   const Geo32 g{F, H, W};
-  if (vec4_ok(dx, lddx, C) && ((uintptr_t)dcol & 15) == 0)
-    hipLaunchKernelGGL(col2im3d_kernel<4>, dim3(grid_for(P * C / 4)), dim3(kThreads), 0, s, dcol, C, g, (int)P, dx,
-                       lddx, accumulate);
-  else
-    hipLaunchKernelGGL(col2im3d_kernel<1>, dim3(grid_for(P * C)), dim3(kThreads), 0, s, dcol, C, g, (int)P, dx, lddx,
-                       accumulate);
+  // float4 only: the training handle admits widths divisible by 4 only (kdlae_st.cpp), so a scalar
+  // instance would be dead code (r06 kernel coverage: never launched)
+  if (!vec4_ok(dx, lddx, C) || ((uintptr_t)dcol & 15) != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(col2im3d_kernel<4>, dim3(grid_for(P * C / 4)), dim3(kThreads), 0, s, dcol, C, g, (int)P, dx,
+                     lddx, accumulate);
   return hipGetLastError();
 }
 

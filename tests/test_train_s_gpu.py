@@ -61,6 +61,23 @@ def test_dropin_backward_matches_oracle(name):
     _check_grads(m, g_ref, name)
 
 
+def test_odd_channel_training_is_rejected():
+    """Hidden widths not divisible by 4 ([6, 10]): the training handle refuses them with a clear error
+    before anything launches (its pool / column-gather kernels move float4 channel groups); the eval
+    forward of the same model still runs and matches the oracle."""
+    cfg_kw = dict(inp_channels=1, out_channels=1, residual=True, hidden_channels=[6, 10])
+    m = _model(cfg_kw)
+    x = torch.from_numpy(hash_images("odd_s_x", (2, 3, 8, 12)))
+    with pytest.raises((NotImplementedError, RuntimeError), match="divisible by 4"):
+        m(x.to(DEV))
+    m.eval()
+    with torch.no_grad():
+        out = m(x.to(DEV)).cpu()
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref = student_forward(sd, x, StudentCfg(**cfg_kw))
+    assert float((out - ref).abs().max()) <= 1e-5
+
+
 def test_trainer_two_steps_match_oracle():
     """KDLAESTrainer (flat buffers, fused clip + AdamW) over two steps vs the oracle with torch AdamW."""
     d, js = _case("train_s_kdlaes")
