@@ -333,7 +333,8 @@ int kdlae_train_ema(float* ema, const float* theta, int64_t n, float decay, void
  * every key 16-byte aligned (pads zero), as for kdlae_tt_*; kdlae_train_clip_adamw / _ema / _mixup
  * apply unchanged. */
 typedef struct kdlae_st_handle kdlae_st_handle;
-/* replaces KDLAE_student.__init__ for training (KDLAE_model.py:341-384); inp/out_channels 1, kernel_size 3 */
+/* replaces KDLAE_student.__init__ for training (KDLAE_model.py:341-384); inp/out_channels 1, kernel_size 3,
+ * hidden_channels divisible by 4 (KDLAE_EINVAL_CONFIG otherwise) */
 int kdlae_st_create(const kdlae_s_config* cfg, int device, kdlae_st_handle** out);
 int kdlae_st_destroy(kdlae_st_handle* h);
 int kdlae_st_num_params(const kdlae_st_handle* h);
