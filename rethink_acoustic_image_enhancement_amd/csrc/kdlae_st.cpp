@@ -55,12 +55,8 @@ struct kdlae_st_handle {
 namespace {
 
 constexpr size_t kPartialFloats = 16u << 20;  // split-K partials of the weight-gradient GEMMs
-#ifndef KDLAE_ST_DX_CONV
-#define KDLAE_ST_DX_CONV 1
-#endif
-#ifndef KDLAE_ST_DIRECT
-#define KDLAE_ST_DIRECT 1
-#endif
+constexpr auto KDLAE_ST_DX_CONV = 1;
+constexpr auto KDLAE_ST_DIRECT = 1;
 constexpr int kColsumBlocks = 256;
 
 struct SPlanT {

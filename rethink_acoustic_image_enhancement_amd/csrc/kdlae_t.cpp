@@ -417,12 +417,8 @@ struct Plan {
 // at least 32 rows (512^2: 64 rows, the 2-row halo costs 3%; 1024^2: 128 rows; 4 and 16 segments
 // measured no better, profiles/r02_gram_nseg_probe.txt); generic kernel: 64-pixel steps grouped 16
 // per slot.
-#ifndef KDLAE_T_DOWN_LDS
-#define KDLAE_T_DOWN_LDS 1  // Downsample convs on conv_lds (0: the implicit GEMM)
-#endif
-#ifndef KDLAE_T_UP_LDS
-#define KDLAE_T_UP_LDS 1  // Upsample convs on conv_lds (0: the implicit GEMM)
-#endif
+constexpr auto KDLAE_T_DOWN_LDS = 1;  // Downsample convs on conv_lds (0: the implicit GEMM)
+constexpr auto KDLAE_T_UP_LDS = 1;  // Upsample convs on conv_lds (0: the implicit GEMM)
 constexpr int kGramMaxSeg = 8, kGramMinRows = 32;  // Gram slots: row segments per strip, rows per segment
 static int nslots_for(int H, int W, int /*B*/, int /*heads*/) {
   if (W % 16 == 0) {

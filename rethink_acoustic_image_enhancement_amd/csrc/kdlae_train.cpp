@@ -433,12 +433,8 @@ int queue_reduce(Ctx& c, const float* part, int nblk, int ncols, int pstride, fl
 // The K >= 1024 ones take the split-K partials too (launch_tgemm splits only where the grid is short).
 // r04 trace A/B (gpurun_out/trab): dX 1536 x 384 K 2042 0.544 -> 0.386 ms, 6144 x 192 K 1020 0.688 ->
 // 0.660; at K = 510 / 576 the partial round trip lost (0.42 -> 0.53, 0.42 -> 0.50 ms).
-#ifndef KDLAE_TRAIN_LAG
-#define KDLAE_TRAIN_LAG 1  // stage_bwd's lagged side-stream synchronisation (0: join per block)
-#endif
-#ifndef KDLAE_TRAIN_SPLIT_SMALL
-#define KDLAE_TRAIN_SPLIT_SMALL 1
-#endif
+constexpr auto KDLAE_TRAIN_LAG = 1;  // stage_bwd's lagged side-stream synchronisation (0: join per block)
+constexpr auto KDLAE_TRAIN_SPLIT_SMALL = 1;
 constexpr long long kSplitSmallRows = 24576;  // below the row-streaming kernel's threshold
 constexpr int kSplitSmallK = 1000;
 
@@ -462,12 +458,8 @@ int gemm(Ctx& c, const tr::TGemm& g0, size_t cap, const std::string& what) {
   return KDLAE_OK;
 }
 
-#ifndef KDLAE_LN_BWD_MAXB
-#define KDLAE_LN_BWD_MAXB 2048
-#endif
-#ifndef KDLAE_LN_BWD_ROWS
-#define KDLAE_LN_BWD_ROWS 32
-#endif
+constexpr auto KDLAE_LN_BWD_MAXB = 2048;
+constexpr auto KDLAE_LN_BWD_ROWS = 32;
 int nblk_for(long long rows, long long ncols, int maxb = 1024, int rows_per_blk = 128) {
   long long nb = rows / rows_per_blk;
   if (nb > maxb) nb = maxb;

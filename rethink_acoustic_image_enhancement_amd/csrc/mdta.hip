@@ -212,16 +212,12 @@ __host__ __device__ constexpr int gram_waves(int ct) {
 // issue (60-185 cycles a piece beside MFMAs) paced the row.  At 12 waves the v jobs ride as second jobs
 // on waves 0-5, waves 6-11 are DMA waves with 4 pieces each: 2170 -> 1847 us per C96@512^2 launch
 // (r04 same-box probe, gpurun_out/ring6b; 13 waves 1954, 14 1947, 16 2032)
-#ifndef KDLAE_RING6_WAVES
-#define KDLAE_RING6_WAVES 12
-#endif
+constexpr auto KDLAE_RING6_WAVES = 12;
 // r03 A/B (profiles/r03_gram_ab_probe.txt, retired): a stencil window rolled in registers across rows
 // (6 LDS reads per job and row instead of 18) and q / k staged transposed with a quad swizzle
 // (ds_read_b128 operands) were both no faster; neither LDS traffic nor issue is this kernel's limit
 // waves per block for the LDS-DMA ring kernel (one block per CU at CT = 6)
-#ifndef KDLAE_RING3_WAVES
-#define KDLAE_RING3_WAVES 9
-#endif
+constexpr auto KDLAE_RING3_WAVES = 9;
 __host__ __device__ constexpr int gram_ring_waves(int ct) {
   return ct == 6 ? KDLAE_RING6_WAVES : ct == 3 ? KDLAE_RING3_WAVES : gram_waves(ct);
 }
@@ -441,9 +437,7 @@ struct GramRing {
   }
 };
 
-#ifndef KDLAE_RING_XCD
-#define KDLAE_RING_XCD 1
-#endif
+constexpr auto KDLAE_RING_XCD = 1;
 template <int CT>
 __global__ __launch_bounds__(64 * gram_ring_waves(CT)) void dwconv_gram_ring_kernel(GramParams p, int seg_rows) {
   using R = GramRing<CT>;

@@ -47,9 +47,7 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
 // r05: weigh one or two more weight groups than the LDS budget needs, counting every computed tile
 // (the last group's padding too).  A/B (profiles/r05zx_gemm_groups_ab.txt): C192 qkv (36 tiles) as
 // 6 groups of 6 instead of 5 of 8 (the last half empty): 588 -> 382 us per launch at 16 x 128^2.
-#ifndef KDLAE_GEMM_GROUPS_ALT
-#define KDLAE_GEMM_GROUPS_ALT 1
-#endif
+constexpr auto KDLAE_GEMM_GROUPS_ALT = 1;
     int best_groups = 0;
     for (int w : {2}) {
       // two resident blocks per CU at 4 waves/SIMD -> half the LDS budget each
@@ -107,16 +105,10 @@ void choose_variant(Gemm& g, bool /*prefer_single_k*/) {
       // K = 510/1021 FFN project_out and the C384 GEMMs take 12x8 chunks (72 -> 85 and 76 -> 90 TF/s)
       // 3x3 (r01 probe): an n-chunk re-gathers the whole im2col A (12x3 beat 6x12 at N = 384, 768);
       // with 12-tile chunks, halving the k-chunks (12x6) saved 2%; with 3-tile chunks 3x6 lost 12%
-#ifndef KDLAE_NPEN_1X1
-#define KDLAE_NPEN_1X1 0.06
-#endif
-#ifndef KDLAE_NPEN_3X3
-#define KDLAE_NPEN_3X3 0.12
-#endif
+constexpr auto KDLAE_NPEN_1X1 = 0.06;
+constexpr auto KDLAE_NPEN_3X3 = 0.12;
       const double npen = g.ksize == 3 ? KDLAE_NPEN_3X3 : KDLAE_NPEN_1X1;
-#ifndef KDLAE_KPEN_1X1
-#define KDLAE_KPEN_1X1 0.02
-#endif
+constexpr auto KDLAE_KPEN_1X1 = 0.02;
       const double kpen = g.ksize == 3 ? (nt >= 12 ? 0.01 : 0.0) : KDLAE_KPEN_1X1;
       double cost = waste * (1.0 + npen * (nch - 1) + kpen * (kch - 1));
       if (cost < best - 1e-9) {

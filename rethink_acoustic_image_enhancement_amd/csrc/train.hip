@@ -514,21 +514,11 @@ static void launch_t(const TGemm& g, int kchunk, int flags, int rm, dim3 grid, h
 
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-#ifndef KDLAE_SPLITK_BLOCKS
-#define KDLAE_SPLITK_BLOCKS 2048
-#endif
-#ifndef KDLAE_SPLITK_MIN
-#define KDLAE_SPLITK_MIN 256
-#endif
-#ifndef KDLAE_TRAIN_ROWS
-#define KDLAE_TRAIN_ROWS 1
-#endif
-#ifndef KDLAE_TRAIN_COLS
-#define KDLAE_TRAIN_COLS 1
-#endif
-#ifndef KDLAE_RED_VEC
-#define KDLAE_RED_VEC 1
-#endif
+constexpr auto KDLAE_SPLITK_BLOCKS = 2048;
+constexpr auto KDLAE_SPLITK_MIN = 256;
+constexpr auto KDLAE_TRAIN_ROWS = 1;
+constexpr auto KDLAE_TRAIN_COLS = 1;
+constexpr auto KDLAE_RED_VEC = 1;
 hipError_t launch_tgemm_reduce(const TGemm& g, hipStream_t s) {
   const long long MN = (long long)g.M * g.N;
   const int vec = KDLAE_RED_VEC && MN % 4 == 0 && al16(g.partial);
@@ -1264,9 +1254,7 @@ hipError_t launch_part_reduce_multi(const RedDesc* d, int n, hipStream_t s) {
 
 hipError_t launch_colsum(const float* x, int ldx, int ncols, long long rows_per_seg, int nseg, int square, float* part,
                          int nblk, hipStream_t s) {
-#ifndef KDLAE_COLSUM4
-#define KDLAE_COLSUM4 1
-#endif
+constexpr auto KDLAE_COLSUM4 = 1;
   if (KDLAE_COLSUM4 && ncols % 4 == 0 && ldx % 4 == 0 && al16(x)) {
     hipLaunchKernelGGL(colsum4_kernel, dim3((ncols + 63) / 64, nblk, nseg), dim3(256), 0, s, x, ldx, ncols,
                        rows_per_seg, square, part);

@@ -196,12 +196,8 @@ int slots(int nw) {
 // split count: whole rounds of resident blocks (r03 sweep: a fixed wave target was up to 40% off
 // either way depending on the shape), chunks of at least KDLAE_COLS_MIN pixels, within the
 // partial-buffer capacity
-#ifndef KDLAE_COLS_MIN
-#define KDLAE_COLS_MIN 256
-#endif
-#ifndef KDLAE_COLS_NARROW
-#define KDLAE_COLS_NARROW 1
-#endif
+constexpr auto KDLAE_COLS_MIN = 256;
+constexpr auto KDLAE_COLS_NARROW = 1;
 template <int TM, int TN, bool IMPB>
 hipError_t launch_tt(TGemm g, ColsArgs a, int nw, int gy, long long batch, size_t partial_cap, hipStream_t s) {
   long long splits = ((long long)slots<TM, TN, IMPB>(nw) + gy * batch - 1) / (gy * batch);

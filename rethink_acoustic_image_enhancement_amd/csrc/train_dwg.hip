@@ -31,15 +31,9 @@ namespace train {
 
 namespace {
 
-#ifndef KDLAE_DWG_U
-#define KDLAE_DWG_U 4
-#endif
-#ifndef KDLAE_DWG_TY
-#define KDLAE_DWG_TY 16
-#endif
-#ifndef KDLAE_DWG_PF
-#define KDLAE_DWG_PF 1
-#endif
+constexpr auto KDLAE_DWG_U = 4;
+constexpr auto KDLAE_DWG_TY = 16;
+constexpr auto KDLAE_DWG_PF = 1;
 constexpr int kU = KDLAE_DWG_U;  // columns per thread
 // rows are loaded one row ahead of their use, so the next row's loads overlap this row's arithmetic
 // (r03 A/B at 6 x 128^2: qkv dwconv backward 3.32 -> 2.41 ms per step, GDFN forward 3.95 -> 3.74,

@@ -67,9 +67,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_rows_kernel(RowsArgs a) {
   // dispatch d runs on XCD d % 8: logical slot L = (d % 8) * (grid / 8) + d / 8 puts consecutive L
   // on one XCD, and the column blocks of a row block are consecutive L — they stream the same A
   // rows through that XCD's L2 at about the same time
-#ifndef KDLAE_ROWS_XCD
-#define KDLAE_ROWS_XCD 1
-#endif
+constexpr auto KDLAE_ROWS_XCD = 1;
   const int per = (int)(gridDim.x >> 3);
   const int L = KDLAE_ROWS_XCD ? (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   if (L >= a.ncb * a.gx) return;
@@ -353,12 +351,8 @@ hipError_t launch_tgemm_rows(const TGemm& g, hipStream_t s) {
   const int ntiles = (g.N + 15) / 16;
   // (residual variants: NT <= 4, the residual registers of wider tiles spill)
   static const int nts[] = {8, 6, 4, 3, 2, 1};
-#ifndef KDLAE_ROWS_LDS_KB
-#define KDLAE_ROWS_LDS_KB 144  // split-record LDS budget per block (KiB); r05 A/B: 96 116.5, 120 116.6, 144 119.6, 156 119.7 img/s
-#endif
-#ifndef KDLAE_ROWS_NTMAX
-#define KDLAE_ROWS_NTMAX 8
-#endif
+constexpr auto KDLAE_ROWS_LDS_KB = 144;  // split-record LDS budget per block (KiB); r05 A/B: 96 116.5, 120 116.6, 144 119.6, 156 119.7 img/s
+constexpr auto KDLAE_ROWS_NTMAX = 8;
   const int ntmax = g.R ? 4 : KDLAE_ROWS_NTMAX;
   int NT = 1;
   if (ntiles <= ntmax) {

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build a libkdlae.so variant for same-box A/Bs (tools/gpu.sh ab / VARIANTS=name=build_ab/<name>/libkdlae.so):
 #   tools/build_variant.sh <name> <git-rev|-> [file=path-to-replacement ...] [-- extra hipcc flags]
+# (tuning constants are constexpr in the sources since r06: change one through a file replacement)
 # Copies csrc (from <git-rev>, or the working tree with -) and include/ to build_ab/<name>/, replaces the
 # listed files, and builds build_ab/<name>/libkdlae.so.  build_ab/ is git-ignored.
 set -e
